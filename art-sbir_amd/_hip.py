@@ -1,0 +1,99 @@
+"""ctypes binding of libartsbir_hip.so (the C-ABI declared in include/artsbir.h).
+
+This module is the only place Python touches the native library.  It loads the
+in-tree shared object (built by ``make`` in this directory / ``__graft_entry__.build``)
+and fails loudly when it is missing: the product path has no CPU or PyTorch
+fallback.  ``import torch`` happens first so that the HIP runtime torch ships is
+the one the library binds to (same soname, loaded once per process).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the library is dlopen'ed)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libartsbir_hip.so")
+
+DT_F32 = 0
+DT_BF16 = 1
+NSLOT = 32
+
+_c_int = ctypes.c_int
+_c_ll = ctypes.c_longlong
+_c_float = ctypes.c_float
+_vp = ctypes.c_void_p
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("dtype", _c_int), ("N", _c_int), ("H", _c_int), ("W", _c_int), ("C", _c_int),
+                ("Cout", _c_int), ("R", _c_int), ("S", _c_int), ("stride", _c_int), ("pad", _c_int)]
+
+
+_P = ctypes.POINTER(ConvDesc)
+
+# name -> argtypes (restype is always int status unless listed in _RESTYPES)
+SIGNATURES = {
+    "artsbir_version": [],
+    "artsbir_last_error": [],
+    "artsbir_conv2d_fwd": [_P, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp],
+    "artsbir_conv2d_wgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
+    "artsbir_gemm_nt": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_gemm_tn": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _c_ll, _vp, _vp],
+}
+_RESTYPES = {"artsbir_last_error": ctypes.c_char_p}
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the native library; raise if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libartsbir_hip.so not found at {LIB_PATH}: build it with `make -C art-sbir_amd` "
+                "or __graft_entry__.build(); there is no fallback path")
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = argtypes
+            fn.restype = _RESTYPES.get(name, _c_int)
+        _lib = handle
+    return _lib
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def call(name: str, *args) -> None:
+    """Invoke a status-returning entry point; map a non-zero status to HipError."""
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().artsbir_last_error().decode(errors="replace")
+        raise HipError(f"{name} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Raw device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return DT_F32
+    if dt == torch.bfloat16:
+        return DT_BF16
+    raise TypeError(f"unsupported compute dtype {dt}")
+
+
+def conv_desc(dt: torch.dtype, N, H, W, C, Cout, R, S, stride, pad) -> ConvDesc:
+    return ConvDesc(dtype_code(dt), N, H, W, C, Cout, R, S, stride, pad)
