@@ -31,7 +31,19 @@ class ConvDesc(ctypes.Structure):
                 ("Cout", _c_int), ("R", _c_int), ("S", _c_int), ("stride", _c_int), ("pad", _c_int)]
 
 
+class BnBwdDesc(ctypes.Structure):
+    _fields_ = [("dtype", _c_int), ("kind", _c_int), ("pool", _c_int), ("d", _vp), ("mask", _vp),
+                ("mask_scale", _vp), ("mask_shift", _vp), ("ntarget", _c_int), ("y", _vp * 2),
+                ("mean", _vp * 2), ("istd", _vp * 2), ("slots", _vp * 2), ("coef", _vp * 2), ("dy", _vp * 2),
+                ("gout", _vp), ("B", _c_int), ("H", _c_int), ("W", _c_int), ("C", _c_int)]
+
+
+class AdamTensor(ctypes.Structure):
+    _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("numel", _c_ll)]
+
+
 _P = ctypes.POINTER(ConvDesc)
+_PB = ctypes.POINTER(BnBwdDesc)
 
 # name -> argtypes (restype is always int status unless listed in _RESTYPES)
 SIGNATURES = {
@@ -41,8 +53,30 @@ SIGNATURES = {
     "artsbir_conv2d_wgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_gemm_nt": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_gemm_tn": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _c_ll, _vp, _vp],
+    "artsbir_conv2d_dgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp],
+    "artsbir_pack_input": [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_pack_weight": [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_ll, _vp, _vp],
+    "artsbir_unpack_wgrad": [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_cast": [_c_int, _vp, _c_int, _vp, _c_ll, _vp],
+    "artsbir_bn_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float, _c_float, _c_int,
+                            _vp, _vp, _vp, _vp, _vp],
+    "artsbir_act_pool": [_c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp],
+    "artsbir_bn_bwd_reduce": [_PB, _vp],
+    "artsbir_bn_bwd_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_bn_bwd_apply": [_PB, _vp],
+    "artsbir_colsum": [_c_int, _vp, _c_ll, _c_ll, _c_ll, _vp, _vp],
+    "artsbir_tokens_fwd": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_tokens_bwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_attnpool_fwd": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_attnpool_bwd": [_c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_triplet_fwd": [_vp, _vp, _vp, _c_int, _c_int, _c_float, _c_float, _vp, _vp, _vp],
+    "artsbir_triplet_bwd": [_vp, _vp, _vp, _c_int, _c_int, _c_float, _c_float, _vp, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_adam_table_blocks": [_vp, _c_int, _c_ll],
+    "artsbir_adam_fill_table": [_vp, _c_int, _c_ll, _vp],
+    "artsbir_adam_step": [_vp, _vp, _c_ll, _c_ll, _c_float, _c_float, _c_float, _c_float, _c_float, _c_ll, _vp],
 }
-_RESTYPES = {"artsbir_last_error": ctypes.c_char_p}
+_RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll}
 
 _lib = None
 

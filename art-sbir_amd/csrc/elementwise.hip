@@ -1,0 +1,612 @@
+// Memory-bound kernels of the encoder hot path (NHWC, 8 channels per thread).
+//
+// Reference ops replaced (all /root/reference/models.py):
+//   x.type(conv1.weight.dtype) + NCHW->NHWC                       :352
+//   BatchNorm2d train/eval (batch stats finalize, running update)  :199,203,209,220,311,314,317
+//   ReLU, AvgPool2d(2)/(stride), residual add + ReLU               :200-206,218,234-235,312-319
+//   their autograd backward (BN backward, ReLU mask, unpool)
+//   AttentionPool2d token build (mean token + positional emb)      :250-252
+// plus parameter (re)packing between the reference layout and the kernel layouts.
+#include "common.h"
+#include "../../include/artsbir.h"
+
+namespace artsbir {
+
+template <typename T> __device__ __forceinline__ void load8(const T* p, float (&v)[8]);
+template <> __device__ __forceinline__ void load8<bf16>(const bf16* p, float (&v)[8]) {
+  Vec16<bf16> r = ld16<bf16>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)r.v[i];
+}
+template <> __device__ __forceinline__ void load8<float>(const float* p, float (&v)[8]) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8]);
+template <> __device__ __forceinline__ void store8<bf16>(bf16* p, const float (&v)[8]) {
+  Vec16<bf16> r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = (bf16)v[i];
+  st16<bf16>(p, r);
+}
+template <> __device__ __forceinline__ void store8<float>(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void loadf8(const float* p, float (&v)[8]) { load8<float>(p, v); }
+
+static inline unsigned grid_for(long long n, int block = 256, long long cap = 1 << 20) {
+  long long g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// ---------------------------------------------------------------- pack input
+// x [B][3][H][W] f32 (NCHW) -> out [B][H][W][8] T, channels 3..7 zero.
+template <typename T>
+__global__ void pack_input_kernel(const float* __restrict__ x, T* __restrict__ out, int B, int Cin, int H, int W) {
+  const long long npix = (long long)B * H * W;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix; i += (long long)gridDim.x * blockDim.x) {
+    long long b = i / ((long long)H * W);
+    long long hw = i - b * H * W;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v[c] = c < Cin ? x[(b * Cin + c) * H * W + hw] : 0.f;
+    store8<T>(out + i * 8, v);
+  }
+}
+
+// ------------------------------------------------------- bn finalize (forward)
+// stats [NSLOT][2][C] (sum, sum of squares) -> mean, istd, scale, shift;
+// train: update running stats (momentum, unbiased var) and num_batches_tracked.
+__global__ void bn_finalize_kernel(const float* __restrict__ stats, int C, double count, const float* gamma,
+                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                                   float eps, int train, float* mean_out, float* istd_out, float* scale, float* shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && train && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  double mean, var;
+  if (train) {
+    double s1 = 0, s2 = 0;
+    for (int k = 0; k < ARTSBIR_NSLOT; ++k) {
+      s1 += stats[(long long)k * 2 * C + c];
+      s2 += stats[(long long)k * 2 * C + C + c];
+    }
+    mean = s1 / count;
+    var = s2 / count - mean * mean;
+    if (var < 0) var = 0;
+    if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+    if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * count / (count > 1 ? count - 1 : 1));
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  float is = (float)(1.0 / sqrt(var + (double)eps));
+  float sc = gamma[c] * is;
+  mean_out[c] = (float)mean;
+  istd_out[c] = is;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+}
+
+// ------------------------------------------------ affine(+relu)(+avgpool 2x2)
+// out = pool?( act(x) ), act = x*sc+sh then ReLU (sc==NULL: identity, no relu)
+template <typename T>
+__global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict__ sc, const float* __restrict__ sh,
+                                int relu, int pool, int B, int H, int W, int C, T* __restrict__ out) {
+  const int CG = C / 8;
+  const int Ho = pool ? H / pool : H, Wo = pool ? W / pool : W;
+  const long long n = (long long)B * Ho * Wo * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int cg = (int)(i % CG);
+    long long pix = i / CG;
+    int ow = (int)(pix % Wo);
+    long long t = pix / Wo;
+    int oh = (int)(t % Ho);
+    long long b = t / Ho;
+    float s[8], h[8];
+    if (sc) { loadf8(sc + cg * 8, s); loadf8(sh + cg * 8, h); }
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int P = pool ? pool : 1;
+    for (int dy = 0; dy < P; ++dy)
+      for (int dx = 0; dx < P; ++dx) {
+        float v[8];
+        load8<T>(x + (((b * H + oh * P + dy) * W + ow * P + dx) * C + cg * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float a = sc ? v[e] * s[e] + h[e] : v[e];
+          if (relu) a = fmaxf(a, 0.f);
+          acc[e] += a;
+        }
+      }
+    const float inv = 1.f / (P * P);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    store8<T>(out + pix * C + cg * 8, acc);
+  }
+}
+
+// --------------------------------------------------------- bottleneck output
+// out = relu(y3*sc3+sh3 + (yd ? yd*scd+shd : idn))
+template <typename T>
+__global__ void block_out_kernel(const T* __restrict__ y3, const float* __restrict__ sc3, const float* __restrict__ sh3,
+                                 const T* __restrict__ yd, const float* __restrict__ scd, const float* __restrict__ shd,
+                                 const T* __restrict__ idn, long long rows, int C, T* __restrict__ out) {
+  const int CG = C / 8;
+  const long long n = rows * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int cg = (int)(i % CG);
+    long long off = (i / CG) * C + cg * 8;
+    float a[8], s[8], h[8], r[8];
+    load8<T>(y3 + off, a);
+    loadf8(sc3 + cg * 8, s);
+    loadf8(sh3 + cg * 8, h);
+    if (yd) {
+      float s2[8], h2[8];
+      load8<T>(yd + off, r);
+      loadf8(scd + cg * 8, s2);
+      loadf8(shd + cg * 8, h2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r[e] = r[e] * s2[e] + h2[e];
+    } else {
+      load8<T>(idn + off, r);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * s[e] + h[e] + r[e], 0.f);
+    store8<T>(out + off, a);
+  }
+}
+
+// ------------------------------------------------------------ BN backward
+// Two flavours of the upstream gradient g at an element of the BN output:
+//   RES: g = dout * (out > 0)                      (block output ReLU)
+//   ACT: g = up(d) * (y*sc + sh > 0)               (ReLU after BN; up = identity
+//        or 2x2 average-unpool when the forward pooled after the ReLU)
+// For up to two BN targets t (y3 and the downsample yd share g), with
+//   xhat_t = (y_t - mean_t) * istd_t:
+//   REDUCE: slots_t[k][0][c] += sum g, slots_t[k][1][c] += sum g*xhat_t
+//   APPLY : dy_t = c1_t*(g - c2_t - xhat_t*c3_t);  optional gout = g
+struct BnBwdArgs {
+  int kind;   // 0 RES, 1 ACT
+  int pool;   // ACT: forward pooled by `pool` after the ReLU (0/1 = none)
+  const void* d;     // RES: dout ; ACT: d (pooled resolution if pool>1)
+  const void* mask;  // RES: out
+  const float* msc;  // ACT: scale/shift of the BN feeding the ReLU (target 0)
+  const float* msh;
+  int ntarget;
+  const void* y[2];
+  const float* mean[2];
+  const float* istd[2];
+  float* slots[2];           // REDUCE
+  const float* coef[2];      // APPLY: [3][C] = c1, c2, c3
+  void* dy[2];               // APPLY outputs
+  void* gout;                // APPLY optional
+  int B, H, W, C;            // geometry of y (full resolution)
+};
+
+template <typename T>
+__device__ __forceinline__ void bnb_g(const BnBwdArgs& a, long long b, int h, int w, int cg, long long off, float (&g)[8]) {
+  if (a.kind == 0) {
+    float m[8];
+    load8<T>(reinterpret_cast<const T*>(a.d) + off, g);
+    load8<T>(reinterpret_cast<const T*>(a.mask) + off, m);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
+  } else {
+    if (a.pool > 1) {
+      const int Hp = a.H / a.pool, Wp = a.W / a.pool;
+      load8<T>(reinterpret_cast<const T*>(a.d) + (((b * Hp + h / a.pool) * Wp + w / a.pool) * a.C + cg * 8), g);
+      const float inv = 1.f / (a.pool * a.pool);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[e] *= inv;
+    } else {
+      load8<T>(reinterpret_cast<const T*>(a.d) + off, g);
+    }
+    float y[8], s[8], sh[8];
+    load8<T>(reinterpret_cast<const T*>(a.y[0]) + off, y);
+    loadf8(a.msc + cg * 8, s);
+    loadf8(a.msh + cg * 8, sh);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = (y[e] * s[e] + sh[e]) > 0.f ? g[e] : 0.f;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, long long rows_per_block) {
+  const int CG = a.C / 8;
+  const int RL = 256 / CG;  // row lanes
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, rl = tid / CG;
+  const long long rows = (long long)a.B * a.H * a.W;
+  const long long r0 = blockIdx.x * rows_per_block;
+  long long r1 = r0 + rows_per_block;
+  if (r1 > rows) r1 = rows;
+  float acc[2][2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t][q][e] = 0.f;
+  float mn[2][8], is[2][8];
+  if (rl < RL) {
+    for (int t = 0; t < a.ntarget; ++t) { loadf8(a.mean[t] + cg * 8, mn[t]); loadf8(a.istd[t] + cg * 8, is[t]); }
+    for (long long r = r0 + rl; r < r1; r += RL) {
+      int w = (int)(r % a.W);
+      long long q = r / a.W;
+      int h = (int)(q % a.H);
+      long long b = q / a.H;
+      const long long off = r * a.C + cg * 8;
+      float g[8];
+      bnb_g<T>(a, b, h, w, cg, off, g);
+      for (int t = 0; t < a.ntarget; ++t) {
+        float y[8];
+        load8<T>(reinterpret_cast<const T*>(a.y[t]) + off, y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          acc[t][0][e] += g[e];
+          acc[t][1][e] += g[e] * (y[e] - mn[t][e]) * is[t][e];
+        }
+      }
+    }
+  }
+  // reduce over row lanes in LDS, then one atomic per channel per block
+  __shared__ float red[256 * 8];
+  const int slot = blockIdx.x % ARTSBIR_NSLOT;
+  for (int t = 0; t < a.ntarget; ++t)
+    for (int q = 0; q < 2; ++q) {
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[tid * 8 + e] = (rl < RL) ? acc[t][q][e] : 0.f;
+      __syncthreads();
+      if (tid < CG) {
+        for (int e = 0; e < 8; ++e) {
+          float s = 0.f;
+          for (int l = 0; l < RL; ++l) s += red[(l * CG + tid) * 8 + e];
+          atomicAdd(a.slots[t] + (long long)slot * 2 * a.C + q * a.C + tid * 8 + e, s);
+        }
+      }
+    }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
+  const int CG = a.C / 8;
+  const long long n = (long long)a.B * a.H * a.W * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long r = i / CG;
+    int w = (int)(r % a.W);
+    long long q = r / a.W;
+    int h = (int)(q % a.H);
+    long long b = q / a.H;
+    const long long off = r * a.C + cg * 8;
+    float g[8];
+    bnb_g<T>(a, b, h, w, cg, off, g);
+    if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + off, g);
+    for (int t = 0; t < a.ntarget; ++t) {
+      float y[8], mn[8], is[8], c1[8], c2[8], c3[8], o[8];
+      load8<T>(reinterpret_cast<const T*>(a.y[t]) + off, y);
+      loadf8(a.mean[t] + cg * 8, mn);
+      loadf8(a.istd[t] + cg * 8, is);
+      loadf8(a.coef[t] + cg * 8, c1);
+      loadf8(a.coef[t] + a.C + cg * 8, c2);
+      loadf8(a.coef[t] + 2 * a.C + cg * 8, c3);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = c1[e] * (g[e] - c2[e] - (y[e] - mn[e]) * is[e] * c3[e]);
+      store8<T>(reinterpret_cast<T*>(a.dy[t]) + off, o);
+    }
+  }
+}
+
+// slots -> dgamma, dbeta (written into the parameter-gradient buffers) and the
+// apply coefficients c1 = gamma*istd, c2 = sum(g)/cnt, c3 = sum(g*xhat)/cnt
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ slots, int C, double count, const float* gamma,
+                                       const float* istd, float* dgamma, float* dbeta, float* coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int k = 0; k < ARTSBIR_NSLOT; ++k) {
+    s1 += slots[(long long)k * 2 * C + c];
+    s2 += slots[(long long)k * 2 * C + C + c];
+  }
+  if (dbeta) dbeta[c] = (float)s1;
+  if (dgamma) dgamma[c] = (float)s2;
+  coef[c] = gamma[c] * istd[c];
+  coef[C + c] = (float)(s1 / count);
+  coef[2 * C + c] = (float)(s2 / count);
+}
+
+// ------------------------------------------------------------------ colsum
+// out[c] += sum_{r<rows} x[r*ld + c]   (x is T or f32; 8 columns per thread)
+template <typename T>
+__global__ void colsum_kernel(const T* __restrict__ x, long long rows, long long ld, long long C, long long rows_per_block,
+                              float* __restrict__ out) {
+  const long long c0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  long long r0 = blockIdx.y * rows_per_block, r1 = r0 + rows_per_block;
+  if (r1 > rows) r1 = rows;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (long long r = r0; r < r1; ++r) {
+    float v[8];
+    load8<T>(x + r * ld + c0, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) atomicAdd(out + c0 + e, acc[e]);
+}
+
+// ------------------------------------------------------------ casts / packs
+template <typename TI, typename TO>
+__global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = from_f<TO>(to_f(x[i]));
+}
+
+// src [Co][Ci][R][S] f32 (reference layout) ->
+//   mode 0: dst[co][r][s][ci'] (ci' < ci_pad, zero beyond Ci)        forward operand
+//   mode 1: dst[(ci*R + r)*S + s)*ldo + co] = src[co][ci][R-1-r][S-1-s]  data-gradient operand
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ src, int Co, int Ci, int R, int S, int ci_pad, int mode,
+                                   long long ldo, T* __restrict__ dst) {
+  const long long n = mode == 0 ? (long long)Co * R * S * ci_pad : (long long)Ci * R * S * Co;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    if (mode == 0) {
+      int ci = (int)(i % ci_pad);
+      long long t = i / ci_pad;
+      int s = (int)(t % S); t /= S;
+      int r = (int)(t % R);
+      int co = (int)(t / R);
+      float v = ci < Ci ? src[(((long long)co * Ci + ci) * R + r) * S + s] : 0.f;
+      dst[i] = from_f<T>(v);
+    } else {
+      int co = (int)(i % Co);
+      long long t = i / Co;
+      int s = (int)(t % S); t /= S;
+      int r = (int)(t % R);
+      int ci = (int)(t / R);
+      float v = src[(((long long)co * Ci + ci) * R + (R - 1 - r)) * S + (S - 1 - s)];
+      dst[(((long long)ci * R + r) * S + s) * ldo + co] = from_f<T>(v);
+    }
+  }
+}
+
+// wgrad workspace [Co][R][S][Cp] f32 -> parameter-gradient layout [Co][Ci][R][S]
+__global__ void unpack_wgrad_kernel(const float* __restrict__ src, int Co, int Ci, int R, int S, int Cp,
+                                    float* __restrict__ dst) {
+  const long long n = (long long)Co * Ci * R * S;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    int s = (int)(i % S);
+    long long t = i / S;
+    int r = (int)(t % R); t /= R;
+    int ci = (int)(t % Ci);
+    int co = (int)(t / Ci);
+    dst[i] = src[(((long long)co * R + r) * S + s) * Cp + ci];
+  }
+}
+
+// ------------------------------------------------------- attention-pool tokens
+// h [B][P][C] (P = spatial positions) -> tok [B][P+1][C]:
+//   tok[b][0] = mean_p h[b][p] + pos[0];  tok[b][1+p] = h[b][p] + pos[1+p]
+template <typename T>
+__global__ void tokens_fwd_kernel(const T* __restrict__ h, const float* __restrict__ pos, int B, int P, int C,
+                                  T* __restrict__ tok) {
+  const int CG = C / 8;
+  const long long n = (long long)B * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long b = i / CG;
+    float sum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int p = 0; p < P; ++p) {
+      float v[8], pe[8];
+      load8<T>(h + (b * P + p) * C + cg * 8, v);
+      loadf8(pos + (long long)(p + 1) * C + cg * 8, pe);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sum[e] += v[e]; v[e] += pe[e]; }
+      store8<T>(tok + (b * (P + 1) + p + 1) * C + cg * 8, v);
+    }
+    float pe[8];
+    loadf8(pos + cg * 8, pe);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sum[e] = sum[e] / P + pe[e];
+    store8<T>(tok + (b * (P + 1)) * C + cg * 8, sum);
+  }
+}
+
+// dtok [B][P+1][C] f32 -> dh [B][P][C] T: dh[b][p] = dtok[b][1+p] + dtok[b][0] / P
+template <typename T>
+__global__ void tokens_bwd_kernel(const float* __restrict__ dtok, int B, int P, int C, T* __restrict__ dh) {
+  const int CG = C / 8;
+  const long long n = (long long)B * P * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long bp = i / CG;
+    const long long b = bp / P;
+    const int p = (int)(bp % P);
+    float d0[8], d[8];
+    loadf8(dtok + (b * (P + 1)) * C + cg * 8, d0);
+    loadf8(dtok + (b * (P + 1) + p + 1) * C + cg * 8, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] += d0[e] / P;
+    store8<T>(dh + bp * C + cg * 8, d);
+  }
+}
+
+}  // namespace artsbir
+
+using namespace artsbir;
+
+#define DISPATCH_T(dtype, ...)                      \
+  do {                                              \
+    if ((dtype) == ARTSBIR_DT_BF16) {               \
+      typedef bf16 T;                               \
+      __VA_ARGS__;                                  \
+    } else if ((dtype) == ARTSBIR_DT_F32) {         \
+      typedef float T;                              \
+      __VA_ARGS__;                                  \
+    } else {                                        \
+      set_error("unknown dtype %d", (int)(dtype));  \
+      return -1;                                    \
+    }                                               \
+  } while (0)
+
+extern "C" int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, void* out, void* stream) {
+  if (Cin > 8) { set_error("pack_input: Cin=%d > 8", Cin); return -1; }
+  hipStream_t st = (hipStream_t)stream;
+  long long n = (long long)B * H * W;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_input_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, x, (T*)out, B, Cin, H, W));
+  ARTSBIR_CHECK_LAUNCH("pack_input");
+  return 0;
+}
+
+extern "C" int artsbir_bn_finalize(const float* stats, int C, double count, const float* gamma, const float* beta,
+                                   float* running_mean, float* running_var, long long* num_batches_tracked,
+                                   float momentum, float eps, int train, float* mean, float* istd, float* scale,
+                                   float* shift, void* stream) {
+  if (train && !stats) { set_error("bn_finalize: train mode needs stats"); return -1; }
+  if (!train && (!running_mean || !running_var)) { set_error("bn_finalize: eval mode needs running stats"); return -1; }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, stats, C, count,
+                     gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, train, mean, istd,
+                     scale, shift);
+  ARTSBIR_CHECK_LAUNCH("bn_finalize");
+  return 0;
+}
+
+extern "C" int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* shift, int relu, int pool,
+                                int B, int H, int W, int C, void* out, void* stream) {
+  if (C % 8) { set_error("act_pool: C %% 8 != 0"); return -1; }
+  if (pool > 1 && (H % pool || W % pool)) { set_error("act_pool: H,W not divisible by pool"); return -1; }
+  const int Ho = pool > 1 ? H / pool : H, Wo = pool > 1 ? W / pool : W;
+  long long n = (long long)B * Ho * Wo * (C / 8);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(act_pool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)x, scale, shift, relu, pool > 1 ? pool : 0, B, H, W, C, (T*)out));
+  ARTSBIR_CHECK_LAUNCH("act_pool");
+  return 0;
+}
+
+extern "C" int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
+                                 const float* scd, const float* shd, const void* identity, long long rows, int C,
+                                 void* out, void* stream) {
+  if (C % 8) { set_error("block_out: C %% 8 != 0"); return -1; }
+  if (!yd && !identity) { set_error("block_out: need downsample or identity input"); return -1; }
+  long long n = rows * (C / 8);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)y3, sc3, sh3, (const T*)yd, scd, shd, (const T*)identity, rows, C,
+                                       (T*)out));
+  ARTSBIR_CHECK_LAUNCH("block_out");
+  return 0;
+}
+
+static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
+  if (d->C % 8 || 256 % (d->C / 8 > 256 ? 1 : d->C / 8) || d->C / 8 > 256) {
+    set_error("bn_bwd: C=%d unsupported (need C%%8==0, C/8 dividing 256)", d->C);
+    return -1;
+  }
+  if (d->ntarget < 1 || d->ntarget > 2) { set_error("bn_bwd: ntarget must be 1 or 2"); return -1; }
+  a.kind = d->kind; a.pool = d->pool; a.d = d->d; a.mask = d->mask; a.msc = d->mask_scale; a.msh = d->mask_shift;
+  a.ntarget = d->ntarget;
+  for (int t = 0; t < 2; ++t) {
+    a.y[t] = d->y[t]; a.mean[t] = d->mean[t]; a.istd[t] = d->istd[t];
+    a.slots[t] = d->slots[t]; a.coef[t] = d->coef[t]; a.dy[t] = d->dy[t];
+  }
+  a.gout = d->gout;
+  a.B = d->B; a.H = d->H; a.W = d->W; a.C = d->C;
+  return 0;
+}
+
+extern "C" int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream) {
+  BnBwdArgs a;
+  if (fill_bnb(a, d)) return -1;
+  const long long rows = (long long)d->B * d->H * d->W;
+  long long rpb = (rows + 2047) / 2048;
+  if (rpb < 32) rpb = 32;
+  const unsigned grid = (unsigned)((rows + rpb - 1) / rpb);
+  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a, rpb));
+  ARTSBIR_CHECK_LAUNCH("bn_bwd_reduce");
+  return 0;
+}
+
+extern "C" int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream) {
+  BnBwdArgs a;
+  if (fill_bnb(a, d)) return -1;
+  const long long n = (long long)d->B * d->H * d->W * (d->C / 8);
+  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a));
+  ARTSBIR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+extern "C" int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,
+                                       float* dgamma, float* dbeta, float* coef, void* stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, slots, C, count,
+                     gamma, istd, dgamma, dbeta, coef);
+  ARTSBIR_CHECK_LAUNCH("bn_bwd_finalize");
+  return 0;
+}
+
+extern "C" int artsbir_colsum(int dtype, const void* x, long long rows, long long ld, long long C, float* out,
+                              void* stream) {
+  if (C % 8 || ld % 8) { set_error("colsum: C and ld must be multiples of 8"); return -1; }
+  if (rows <= 0) return 0;
+  const unsigned gx = (unsigned)((C / 8 + 255) / 256);
+  long long rpb = 64;
+  long long gy = (rows + rpb - 1) / rpb;
+  if (gy > 65535) { rpb = (rows + 65534) / 65535; gy = (rows + rpb - 1) / rpb; }
+  DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, dim3(gx, (unsigned)gy), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)x, rows, ld, C, rpb, out));
+  ARTSBIR_CHECK_LAUNCH("colsum");
+  return 0;
+}
+
+extern "C" int artsbir_cast(int src_dtype, const void* x, int dst_dtype, void* y, long long n, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (src_dtype == ARTSBIR_DT_F32 && dst_dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid_for(n)), dim3(256), 0, st, (const float*)x, (bf16*)y, n);
+  else if (src_dtype == ARTSBIR_DT_BF16 && dst_dtype == ARTSBIR_DT_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (float*)y, n);
+  else if (src_dtype == ARTSBIR_DT_F32 && dst_dtype == ARTSBIR_DT_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st, (const float*)x, (float*)y, n);
+  else if (src_dtype == ARTSBIR_DT_BF16 && dst_dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n);
+  else { set_error("cast: bad dtypes"); return -1; }
+  ARTSBIR_CHECK_LAUNCH("cast");
+  return 0;
+}
+
+extern "C" int artsbir_pack_weight(int dtype, const float* src, int Co, int Ci, int R, int S, int ci_pad, int mode,
+                                   long long ldo, void* dst, void* stream) {
+  if (mode == 0 && ci_pad < Ci) { set_error("pack_weight: ci_pad < Ci"); return -1; }
+  const long long n = mode == 0 ? (long long)Co * R * S * ci_pad : (long long)Ci * R * S * Co;
+  if (ldo <= 0) ldo = Co;
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_weight_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                       src, Co, Ci, R, S, ci_pad, mode, ldo, (T*)dst));
+  ARTSBIR_CHECK_LAUNCH("pack_weight");
+  return 0;
+}
+
+extern "C" int artsbir_unpack_wgrad(const float* src, int Co, int Ci, int R, int S, int Cp, float* dst, void* stream) {
+  const long long n = (long long)Co * Ci * R * S;
+  hipLaunchKernelGGL(unpack_wgrad_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, Co, Ci, R, S, Cp, dst);
+  ARTSBIR_CHECK_LAUNCH("unpack_wgrad");
+  return 0;
+}
+
+extern "C" int artsbir_tokens_fwd(int dtype, const void* h, const float* pos, int B, int P, int C, void* tok,
+                                  void* stream) {
+  if (C % 8) { set_error("tokens_fwd: C %% 8 != 0"); return -1; }
+  long long n = (long long)B * (C / 8);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(tokens_fwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)h, pos, B, P, C, (T*)tok));
+  ARTSBIR_CHECK_LAUNCH("tokens_fwd");
+  return 0;
+}
+
+extern "C" int artsbir_tokens_bwd(int dtype, const float* dtok, int B, int P, int C, void* dh, void* stream) {
+  if (C % 8) { set_error("tokens_bwd: C %% 8 != 0"); return -1; }
+  long long n = (long long)B * P * (C / 8);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(tokens_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                       dtok, B, P, C, (T*)dh));
+  ARTSBIR_CHECK_LAUNCH("tokens_bwd");
+  return 0;
+}

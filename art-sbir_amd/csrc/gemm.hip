@@ -67,6 +67,8 @@ struct ConvArgs {
   int accumulate;
   const float* bias;
   float* stats;  // [NSLOT][2][Cout]
+  const void* res;  // epilogue residual (T): mode 1 same index, mode 2 2x2 average-unpool
+  int res_mode;
 };
 
 template <typename T, int BM, int BN>
@@ -216,6 +218,15 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
           float v = acc[i][j][r] + bval;
           s1 += v;
           s2 += v * v;
+          if (a.res_mode == 1) {
+            v += to_f(reinterpret_cast<const T*>(a.res)[gm * a.ldy + gn]);
+          } else if (a.res_mode == 2) {
+            const long long img = gm / HoWo;
+            const int rem = (int)(gm - img * HoWo);
+            const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+            const long long ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+            v += 0.25f * to_f(reinterpret_cast<const T*>(a.res)[ri * a.ldy + gn]);
+          }
           if (a.out_f32) {
             float* yp = reinterpret_cast<float*>(a.y) + gm * a.ldy + gn;
             if (a.accumulate) v += *yp;
@@ -508,6 +519,33 @@ extern "C" int artsbir_conv2d_fwd(const artsbir_conv_desc* d, const void* x, con
   a.M = (long long)d->N * Ho * Wo;
   a.y = y; a.ldy = ldy > 0 ? ldy : d->Cout;
   a.out_f32 = out_f32; a.accumulate = accumulate; a.bias = bias; a.stats = stats;
+  a.res = nullptr; a.res_mode = 0;
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
+}
+
+extern "C" int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx,
+                                    const void* res, int res_mode, void* stream) {
+  // data gradient of a stride-1 convolution: a convolution of dy [N][H][W][Cout]
+  // with the flipped, transposed weights wd [Cin][R][S][Cout] and padding R-1-pad.
+  if (d->stride != 1) { set_error("conv2d_dgrad: only stride 1 (got %d)", d->stride); return -1; }
+  if (d->Cout % 8 || d->C % 8) { set_error("conv2d_dgrad: channels must be multiples of 8"); return -1; }
+  if (res_mode < 0 || res_mode > 2 || (res_mode && !res)) { set_error("conv2d_dgrad: bad residual"); return -1; }
+  if (res_mode == 2 && (d->H % 2 || d->W % 2)) { set_error("conv2d_dgrad: unpool residual needs even H, W"); return -1; }
+  ConvArgs a;
+  const int pad = d->R - 1 - d->pad;
+  a.x = dy;
+  a.sW = d->Cout; a.sH = (long long)d->W * d->Cout; a.sN = (long long)d->H * d->W * d->Cout;
+  a.H = d->H; a.W = d->W; a.C = d->Cout;
+  a.R = d->R; a.S = d->S; a.stride = 1; a.pad = pad;
+  a.Ho = d->H + 2 * pad - d->R + 1; a.Wo = d->W + 2 * pad - d->S + 1;
+  if (a.Ho != d->H || a.Wo != d->W) { set_error("conv2d_dgrad: only 'same' convolutions"); return -1; }
+  a.in_scale = nullptr; a.in_shift = nullptr; a.in_relu = 0;
+  a.w = wd; a.Cout = d->C; a.K = d->R * d->S * d->Cout;
+  a.M = (long long)d->N * d->H * d->W;
+  a.y = dx; a.ldy = d->C;
+  a.out_f32 = 0; a.accumulate = 0; a.bias = nullptr; a.stats = nullptr;
+  a.res = res; a.res_mode = res_mode;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
 }
@@ -527,6 +565,7 @@ extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void*
   p.w = b; p.Cout = N; p.K = K; p.M = M;
   p.y = c; p.ldy = ldc > 0 ? ldc : N;
   p.out_f32 = out_f32; p.accumulate = accumulate; p.bias = bias; p.stats = stats;
+  p.res = nullptr; p.res_mode = 0;
   hipStream_t st = (hipStream_t)stream;
   return dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
 }

@@ -1,0 +1,484 @@
+"""Executor of the ModifiedResNet hot path on libartsbir_hip (MI355X / gfx950).
+
+The reference runs the encoder as a chain of PyTorch eager ops
+(models.py:344-360: stem -> layer1..4 -> attnpool; Bottleneck.forward
+models.py:223-236; AttentionPool2d.forward models.py:249-272) and lets
+autograd record the backward.  Here the whole encoder forward and backward are
+sequenced explicitly over the C-ABI kernels:
+
+  * activations live in HBM as NHWC tensors of the compute dtype (bf16 for
+    throughput, f32 for parity); only the raw convolution outputs y are stored,
+    BatchNorm+ReLU is re-applied on load by the consuming convolution and by
+    the weight-gradient GEMM (in_scale/in_shift/in_relu), so the normalised
+    activations are never materialised except where an AvgPool or the
+    residual join needs them;
+  * BN batch statistics come out of the convolution epilogue (sum / sum of
+    squares) and are finalised per call -> per-branch statistics exactly as the
+    reference's three separate forward calls (train.py:28-30);
+  * weights are re-packed from the f32 parameters (reference layout, so
+    state_dicts interchange) into the kernel layouts whenever a parameter
+    changes (torch version counter or an optimizer step of optim.Adam here).
+
+No op of this module runs on the CPU or through a PyTorch kernel except
+allocation (torch.empty / torch.zeros) — the product path fails if the
+native library is missing.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+
+import _hip
+from _hip import call, ptr
+
+NSLOT = _hip.NSLOT
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+# bumped by optim.Adam (which updates parameters through raw pointers, invisible
+# to torch's version counters) so packed weights are rebuilt after every step
+WEIGHTS_GENERATION = [0]
+
+
+def bump_weights_generation():
+    WEIGHTS_GENERATION[0] += 1
+
+
+def _s():
+    return _hip.stream()
+
+
+@dataclass
+class BNState:
+    """per-call batch-norm parameters: mean, istd, scale, shift [4][C] f32"""
+    buf: torch.Tensor
+    count: float
+
+    @property
+    def mean(self):
+        return self.buf[0]
+
+    @property
+    def istd(self):
+        return self.buf[1]
+
+    @property
+    def scale(self):
+        return self.buf[2]
+
+    @property
+    def shift(self):
+        return self.buf[3]
+
+
+@dataclass
+class Act:
+    """an NHWC activation tensor [B][H][W][C] and the affine(+ReLU) that must be
+    applied when it is read (None: read as is)."""
+    t: torch.Tensor
+    bn: BNState | None = None
+    relu: int = 0
+
+    @property
+    def shape(self):
+        return tuple(self.t.shape)
+
+
+class Engine:
+    """Owns the packed weights of one ModifiedResNet and runs it on the GPU."""
+
+    def __init__(self, model):
+        self.model = model
+        self._packed = None
+        self._packed_key = None
+        self.dtype = torch.float32
+
+    # ------------------------------------------------------------------ utils
+    @property
+    def dt(self):
+        return _hip.dtype_code(self.dtype)
+
+    def _empty(self, *shape, dtype=None, device=None):
+        return torch.empty(*shape, dtype=dtype or self.dtype, device=device)
+
+    def _desc(self, N, H, W, C, Cout, R, S, stride, pad):
+        return _hip.conv_desc(self.dtype, N, H, W, C, Cout, R, S, stride, pad)
+
+    # ---------------------------------------------------------- weight packing
+    def _params_key(self):
+        return (self.dtype, WEIGHTS_GENERATION[0],
+                tuple((p.data_ptr(), p._version) for p in self.model.parameters()))
+
+    def packed(self):
+        key = self._params_key()
+        if self._packed_key != key:
+            self._packed = self._pack_all()
+            self._packed_key = key
+        return self._packed
+
+    def _pack_conv(self, conv, ci_pad=None, need_dgrad=True):
+        w = conv.weight.detach()
+        co, ci, r, s = w.shape
+        ci_pad = ci_pad or ci
+        fw = self._empty(co, r, s, ci_pad, device=w.device)
+        call("artsbir_pack_weight", self.dt, ptr(w), co, ci, r, s, ci_pad, 0, 0, ptr(fw), _s())
+        dw = None
+        if need_dgrad:
+            dw = self._empty(ci, r, s, co, device=w.device)
+            call("artsbir_pack_weight", self.dt, ptr(w), co, ci, r, s, ci, 1, co, ptr(dw), _s())
+        return fw, dw
+
+    def _pack_linear_pair(self, lins, device):
+        """rows-concatenated forward weight [sum out][in] and its transpose [in][sum out]"""
+        outs = [l.weight.shape[0] for l in lins]
+        fin = lins[0].weight.shape[1]
+        tot = sum(outs)
+        fw = self._empty(tot, fin, device=device)
+        tw = self._empty(fin, tot, device=device)
+        bias = torch.empty(tot, dtype=torch.float32, device=device)
+        off = 0
+        for l, o in zip(lins, outs):
+            w = l.weight.detach()
+            call("artsbir_pack_weight", self.dt, ptr(w), o, fin, 1, 1, fin, 0, 0, ptr(fw[off:]), _s())
+            call("artsbir_pack_weight", self.dt, ptr(w), o, fin, 1, 1, fin, 1, tot, ptr(tw[:, off:]), _s())
+            call("artsbir_cast", _hip.DT_F32, ptr(l.bias.detach()), _hip.DT_F32, ptr(bias[off:]), o, _s())
+            off += o
+        return fw, tw, bias
+
+    def _pack_all(self):
+        m = self.model
+        dev = m.conv1.weight.device
+        pk = {}
+        pk["stem"] = [self._pack_conv(m.conv1, ci_pad=8, need_dgrad=False),
+                      self._pack_conv(m.conv2), self._pack_conv(m.conv3)]
+        blocks = []
+        for blk in m.blocks():
+            d = {"conv1": self._pack_conv(blk.conv1), "conv2": self._pack_conv(blk.conv2),
+                 "conv3": self._pack_conv(blk.conv3)}
+            if blk.downsample is not None:
+                d["down"] = self._pack_conv(blk.downsample[1])
+            blocks.append(d)
+        pk["blocks"] = blocks
+        ap = m.attnpool
+        pk["kv"] = self._pack_linear_pair([ap.k_proj, ap.v_proj], dev)
+        pk["q"] = self._pack_linear_pair([ap.q_proj], dev)
+        pk["c"] = self._pack_linear_pair([ap.c_proj], dev)
+        return pk
+
+    # ------------------------------------------------------------- primitives
+    def _conv(self, a: Act, fw, cout, R, S, stride, pad, stats_buf=None):
+        B, H, W, C = a.shape
+        Ho = (H + 2 * pad - R) // stride + 1
+        Wo = (W + 2 * pad - S) // stride + 1
+        y = self._empty(B, Ho, Wo, cout, device=a.t.device)
+        d = self._desc(B, H, W, C, cout, R, S, stride, pad)
+        bn = a.bn
+        call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None,
+             ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None, a.relu,
+             ptr(stats_buf), _s())
+        return y
+
+    def _bn(self, bnmod, stats_buf, count, train):
+        C = bnmod.num_features
+        st = BNState(torch.empty(4, C, dtype=torch.float32, device=bnmod.weight.device), float(count))
+        call("artsbir_bn_finalize", ptr(stats_buf) if train else None, C, float(count),
+             ptr(bnmod.weight.detach()), ptr(bnmod.bias.detach()),
+             ptr(bnmod.running_mean), ptr(bnmod.running_var),
+             ptr(bnmod.num_batches_tracked) if train else None,
+             BN_MOMENTUM, BN_EPS, 1 if train else 0,
+             ptr(st.mean), ptr(st.istd), ptr(st.scale), ptr(st.shift), _s())
+        return st
+
+    def _conv_bn(self, a, conv, bnmod, fw, stride, pad, train, stats):
+        cout, _, R, S = conv.weight.shape
+        sb = stats.take(cout) if train else None
+        y = self._conv(a, fw, cout, R, S, stride, pad, sb)
+        B, Ho, Wo, _ = y.shape
+        return y, self._bn(bnmod, sb, B * Ho * Wo, train)
+
+    def _act_pool(self, x, bn, relu, pool):
+        B, H, W, C = x.shape
+        p = max(pool, 1)
+        out = self._empty(B, H // p, W // p, C, device=x.device)
+        call("artsbir_act_pool", self.dt, ptr(x), ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None,
+             relu, pool, B, H, W, C, ptr(out), _s())
+        return out
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x: torch.Tensor, train: bool, save: bool):
+        if not x.is_cuda:
+            raise RuntimeError("ModifiedResNet on libartsbir_hip runs on the GPU: move model and input to cuda")
+        m = self.model
+        pk = self.packed()
+        x = x.contiguous().float()
+        B, cin, R, R2 = x.shape
+        dev = x.device
+        nstat = 2 * NSLOT * m.total_bn_channels() if train else 0
+        stats = _Arena(torch.zeros(max(nstat, 1), dtype=torch.float32, device=dev), NSLOT * 2)
+        ctx = {"train": train, "B": B}
+
+        # stem (models.py:345-350)
+        x0 = self._empty(B, R, R2, 8, device=dev)
+        call("artsbir_pack_input", self.dt, ptr(x), B, cin, R, R2, ptr(x0), _s())
+        (fw1, _), (fw2, _), (fw3, _) = pk["stem"]
+        y1, b1 = self._conv_bn(Act(x0), m.conv1, m.bn1, fw1, 2, 1, train, stats)
+        y2, b2 = self._conv_bn(Act(y1, b1, 1), m.conv2, m.bn2, fw2, 1, 1, train, stats)
+        y3, b3 = self._conv_bn(Act(y2, b2, 1), m.conv3, m.bn3, fw3, 1, 1, train, stats)
+        h = self._act_pool(y3, b3, 1, 2)
+        if save:
+            ctx["stem"] = dict(x0=x0, y1=y1, y2=y2, y3=y3, b1=b1, b2=b2, b3=b3)
+
+        # residual stages (models.py:354-357)
+        bctx = []
+        for blk, bp in zip(m.blocks(), pk["blocks"]):
+            h, c = self._block_fwd(blk, bp, h, train, stats)
+            bctx.append(c if save else None)
+        ctx["blocks"] = bctx
+
+        # attention pool (models.py:249-272)
+        out, actx = self._attnpool_fwd(m.attnpool, pk, h)
+        if save:
+            ctx["attn"] = actx
+        return out, (ctx if save else None)
+
+    def _block_fwd(self, blk, bp, h, train, stats):
+        B, H, W, Cin = h.shape
+        s = blk.stride
+        y1, b1 = self._conv_bn(Act(h), blk.conv1, blk.bn1, bp["conv1"][0], 1, 0, train, stats)
+        y2, b2 = self._conv_bn(Act(y1, b1, 1), blk.conv2, blk.bn2, bp["conv2"][0], 1, 1, train, stats)
+        if s > 1:
+            p2 = self._act_pool(y2, b2, 1, s)
+            c3in = Act(p2)
+        else:
+            p2 = None
+            c3in = Act(y2, b2, 1)
+        y3, b3 = self._conv_bn(c3in, blk.conv3, blk.bn3, bp["conv3"][0], 1, 0, train, stats)
+        yd = bd = pd = None
+        if blk.downsample is not None:
+            if s > 1:
+                pd = self._act_pool(h, None, 0, s)
+                din = pd
+            else:
+                din = h
+            yd, bd = self._conv_bn(Act(din), blk.downsample[1], blk.downsample[2], bp["down"][0], 1, 0, train, stats)
+        out = torch.empty_like(y3)
+        rows = out.numel() // out.shape[-1]
+        call("artsbir_block_out", self.dt, ptr(y3), ptr(b3.scale), ptr(b3.shift),
+             ptr(yd), ptr(bd.scale) if bd else None, ptr(bd.shift) if bd else None,
+             None if yd is not None else ptr(h), rows, out.shape[-1], ptr(out), _s())
+        ctx = dict(h=h, y1=y1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, b1=b1, b2=b2, b3=b3, bd=bd)
+        return out, ctx
+
+    def _attnpool_fwd(self, ap, pk, h):
+        B, Hs, Ws, C = h.shape
+        P = Hs * Ws
+        Tk = P + 1
+        dev = h.device
+        heads = ap.num_heads
+        D = ap.c_proj.weight.shape[0]
+        tok = self._empty(B, Tk, C, device=dev)
+        call("artsbir_tokens_fwd", self.dt, ptr(h), ptr(ap.positional_embedding.detach()), B, P, C, ptr(tok), _s())
+        wkv, _, bkv = pk["kv"]
+        kv = self._empty(B * Tk, 2 * C, device=dev)
+        call("artsbir_gemm_nt", self.dt, B * Tk, 2 * C, C, ptr(tok), C, ptr(wkv), ptr(kv), 2 * C, 0, 0, ptr(bkv),
+             None, _s())
+        wq, _, bq = pk["q"]
+        q = torch.empty(B, C, dtype=torch.float32, device=dev)
+        call("artsbir_gemm_nt", self.dt, B, C, C, ptr(tok), Tk * C, ptr(wq), ptr(q), C, 1, 0, ptr(bq), None, _s())
+        pm = torch.empty(B, heads, Tk, dtype=torch.float32, device=dev)
+        o = self._empty(B, C, device=dev)
+        call("artsbir_attnpool_fwd", self.dt, ptr(q), ptr(kv), B, C, heads, Tk, ptr(pm), ptr(o), _s())
+        wc, _, bc = pk["c"]
+        out = torch.empty(B, D, dtype=torch.float32, device=dev)
+        call("artsbir_gemm_nt", self.dt, B, D, C, ptr(o), C, ptr(wc), ptr(out), D, 1, 0, ptr(bc), None, _s())
+        return out, dict(tok=tok, kv=kv, q=q, pm=pm, o=o, P=P, Tk=Tk, hw=(Hs, Ws))
+
+    # --------------------------------------------------------------- backward
+    def backward(self, ctx, dout: torch.Tensor):
+        if ctx is None:
+            raise RuntimeError("backward through a forward that did not save activations")
+        if not ctx["train"]:
+            raise NotImplementedError("backward is implemented for train-mode BatchNorm (as in train.py)")
+        m = self.model
+        pk = self.packed()
+        dev = dout.device
+        grads = GradBuffer(m, dev)
+        ws = _Arena(torch.zeros(max(2 * NSLOT * m.total_bn_channels() * 2, 1), dtype=torch.float32, device=dev),
+                    NSLOT * 2)
+        dh = self._attnpool_bwd(m.attnpool, pk, ctx["attn"], dout.contiguous().float(), grads)
+        for blk, bp, c in zip(reversed(m.blocks()), reversed(pk["blocks"]), reversed(ctx["blocks"])):
+            dh = self._block_bwd(blk, bp, c, dh, grads, ws)
+        self._stem_bwd(m, pk, ctx["stem"], dh, grads, ws)
+        return grads
+
+    def _attnpool_bwd(self, ap, pk, c, dout, grads):
+        tok, kv, q, pm, o = c["tok"], c["kv"], c["q"], c["pm"], c["o"]
+        B, Tk, C = tok.shape
+        P = c["P"]
+        heads = ap.num_heads
+        D = dout.shape[1]
+        dev = dout.device
+        call("artsbir_colsum", _hip.DT_F32, ptr(dout), B, D, D, ptr(grads[ap.c_proj.bias]), _s())
+        if self.dtype == torch.float32:
+            doutT = dout
+        else:
+            doutT = self._empty(B, D, device=dev)
+            call("artsbir_cast", _hip.DT_F32, ptr(dout), self.dt, ptr(doutT), B * D, _s())
+        call("artsbir_gemm_tn", self.dt, B, D, C, ptr(doutT), D, ptr(o), C, ptr(grads[ap.c_proj.weight]), _s())
+        _, wcT, _ = pk["c"]
+        do = torch.empty(B, C, dtype=torch.float32, device=dev)
+        call("artsbir_gemm_nt", self.dt, B, C, D, ptr(doutT), D, ptr(wcT), ptr(do), C, 1, 0, None, None, _s())
+        dq = self._empty(B, C, device=dev)
+        dkv = self._empty(B * Tk, 2 * C, device=dev)
+        call("artsbir_attnpool_bwd", self.dt, ptr(q), ptr(kv), ptr(pm), ptr(do), B, C, heads, Tk, ptr(dq), ptr(dkv),
+             _s())
+        call("artsbir_colsum", self.dt, ptr(dq), B, C, C, ptr(grads[ap.q_proj.bias]), _s())
+        call("artsbir_colsum", self.dt, ptr(dkv), B * Tk, 2 * C, 2 * C, ptr(grads[ap.k_proj.bias]), _s())
+        call("artsbir_gemm_tn", self.dt, B, C, C, ptr(dq), C, ptr(tok), Tk * C, ptr(grads[ap.q_proj.weight]), _s())
+        call("artsbir_gemm_tn", self.dt, B * Tk, 2 * C, C, ptr(dkv), 2 * C, ptr(tok), C,
+             ptr(grads[ap.k_proj.weight]), _s())
+        _, wkvT, _ = pk["kv"]
+        _, wqT, _ = pk["q"]
+        dtok = torch.empty(B, Tk, C, dtype=torch.float32, device=dev)
+        call("artsbir_gemm_nt", self.dt, B * Tk, C, 2 * C, ptr(dkv), 2 * C, ptr(wkvT), ptr(dtok), C, 1, 0, None, None,
+             _s())
+        call("artsbir_gemm_nt", self.dt, B, C, C, ptr(dq), C, ptr(wqT), ptr(dtok), Tk * C, 1, 1, None, None, _s())
+        call("artsbir_colsum", _hip.DT_F32, ptr(dtok), B, Tk * C, Tk * C, ptr(grads[ap.positional_embedding]), _s())
+        Hs, Ws = c["hw"]
+        dh = self._empty(B, Hs, Ws, C, device=dev)
+        call("artsbir_tokens_bwd", self.dt, ptr(dtok), B, P, C, ptr(dh), _s())
+        return dh
+
+    def _bn_bwd(self, kind, d, targets, bnmods, ws, grads, mask=None, mask_bn=None, pool=0, gout=None):
+        """targets: list of (y, BNState); returns list of dy tensors"""
+        y0 = targets[0][0]
+        B, H, W, C = y0.shape
+        desc = _hip.BnBwdDesc()
+        desc.dtype = self.dt
+        desc.kind = kind
+        desc.pool = pool
+        desc.d = ptr(d)
+        desc.mask = ptr(mask)
+        desc.mask_scale = ptr(mask_bn.scale) if mask_bn else None
+        desc.mask_shift = ptr(mask_bn.shift) if mask_bn else None
+        desc.ntarget = len(targets)
+        slots, coefs, dys = [], [], []
+        for i, (y, st) in enumerate(targets):
+            desc.y[i] = ptr(y)
+            desc.mean[i] = ptr(st.mean)
+            desc.istd[i] = ptr(st.istd)
+            sl = ws.take(C)
+            slots.append(sl)
+            desc.slots[i] = ptr(sl)
+        desc.B, desc.H, desc.W, desc.C = B, H, W, C
+        call("artsbir_bn_bwd_reduce", desc, _s())
+        for i, ((y, st), bnm) in enumerate(zip(targets, bnmods)):
+            coef = torch.empty(3, C, dtype=torch.float32, device=y.device)
+            call("artsbir_bn_bwd_finalize", ptr(slots[i]), C, float(B * H * W), ptr(bnm.weight.detach()),
+                 ptr(st.istd), ptr(grads[bnm.weight]), ptr(grads[bnm.bias]), ptr(coef), _s())
+            coefs.append(coef)
+            dy = torch.empty_like(y)
+            dys.append(dy)
+            desc.coef[i] = ptr(coef)
+            desc.dy[i] = ptr(dy)
+        desc.gout = ptr(gout)
+        call("artsbir_bn_bwd_apply", desc, _s())
+        return dys
+
+    def _wgrad(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):
+        B, H, W, C = a.shape
+        co, ci, R, S = conv.weight.shape
+        d = self._desc(B, H, W, C, co, R, S, stride, pad)
+        bn = a.bn
+        g = grads[conv.weight]
+        if R == 1 and S == 1 and C == ci:
+            target = g
+        else:
+            target = torch.zeros(co, R, S, C, dtype=torch.float32, device=dy.device)
+        call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), ptr(bn.scale) if bn else None,
+             ptr(bn.shift) if bn else None, a.relu, ptr(target), _s())
+        if target is not g:
+            call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
+
+    def _dgrad(self, dy, dw, conv, pad, out_shape, res=None, res_mode=0):
+        B, H, W, C = out_shape
+        co, _, R, S = conv.weight.shape
+        dx = self._empty(B, H, W, C, device=dy.device)
+        d = self._desc(B, H, W, C, co, R, S, 1, pad)
+        call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s())
+        return dx
+
+    def _block_bwd(self, blk, bp, c, dout, grads, ws):
+        h, y1, y2, p2, y3, yd, pd, out = (c[k] for k in ("h", "y1", "y2", "p2", "y3", "yd", "pd", "out"))
+        b1, b2, b3, bd = c["b1"], c["b2"], c["b3"], c["bd"]
+        s = blk.stride
+        has_ds = blk.downsample is not None
+        targets = [(y3, b3)] + ([(yd, bd)] if has_ds else [])
+        bnmods = [blk.bn3] + ([blk.downsample[2]] if has_ds else [])
+        gid = None if has_ds else torch.empty_like(dout)
+        dys = self._bn_bwd(0, dout, targets, bnmods, ws, grads, mask=out, gout=gid)
+        dy3 = dys[0]
+        c3in = Act(p2) if s > 1 else Act(y2, b2, 1)
+        self._wgrad(dy3, c3in, blk.conv3, 1, 0, grads)
+        dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3in.shape[:3] + (blk.conv3.weight.shape[1],))
+        dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
+        self._wgrad(dy2, Act(y1, b1, 1), blk.conv2, 1, 1, grads)
+        da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
+        dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
+        self._wgrad(dy1, Act(h), blk.conv1, 1, 0, grads)
+        if has_ds:
+            dyd = dys[1]
+            din = pd if s > 1 else h
+            dconv = blk.downsample[1]
+            self._wgrad(dyd, Act(din), dconv, 1, 0, grads)
+            dpd = self._dgrad(dyd, bp["down"][1], dconv, 0, din.shape)
+            return self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=dpd, res_mode=2 if s > 1 else 1)
+        return self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=gid, res_mode=1)
+
+    def _stem_bwd(self, m, pk, c, dh, grads, ws):
+        x0, y1, y2, y3, b1, b2, b3 = (c[k] for k in ("x0", "y1", "y2", "y3", "b1", "b2", "b3"))
+        (_, _), (_, dw2), (_, dw3) = pk["stem"]
+        dy3, = self._bn_bwd(1, dh, [(y3, b3)], [m.bn3], ws, grads, mask_bn=b3, pool=2)
+        self._wgrad(dy3, Act(y2, b2, 1), m.conv3, 1, 1, grads)
+        da2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape)
+        dy2, = self._bn_bwd(1, da2, [(y2, b2)], [m.bn2], ws, grads, mask_bn=b2)
+        self._wgrad(dy2, Act(y1, b1, 1), m.conv2, 1, 1, grads)
+        da1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape)
+        dy1, = self._bn_bwd(1, da1, [(y1, b1)], [m.bn1], ws, grads, mask_bn=b1)
+        self._wgrad(dy1, Act(x0), m.conv1, 2, 1, grads)
+
+
+class _Arena:
+    """Bump allocator of per-channel slot blocks out of one zeroed f32 buffer."""
+
+    def __init__(self, buf, per_channel):
+        self.buf, self.per, self.off = buf, per_channel, 0
+
+    def take(self, C):
+        n = self.per * C
+        v = self.buf[self.off:self.off + n]
+        self.off += n
+        if self.off > self.buf.numel():
+            raise RuntimeError("statistics arena overflow")
+        return v
+
+
+class GradBuffer:
+    """One zeroed f32 buffer holding the gradient of every parameter in the
+    reference layout.  k_proj/v_proj weights and biases are adjacent so the
+    fused K|V GEMMs write both at once."""
+
+    def __init__(self, model, device):
+        order = model.grad_order()
+        total = sum(p.numel() for p in order)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=device)
+        self.views = {}
+        off = 0
+        for p in order:
+            n = p.numel()
+            self.views[id(p)] = self.flat[off:off + n].view(p.shape)
+            off += n
+
+    def __getitem__(self, p):
+        return self.views[id(p)]

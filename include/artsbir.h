@@ -64,6 +64,87 @@ int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void* a, long lo
 int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void* dy, long long ldd,
                     const void* x, long long ldx, float* dw, void* stream);
 
+/* data gradient of a stride-1 'same' convolution: dx[m][ci] = sum dy * flipped w
+ * (wd = artsbir_pack_weight mode 1, [Cin][R][S][Cout]) (+ residual: res_mode 1 =
+ * res[m][ci], 2 = 0.25*res[img][oh/2][ow/2][ci], the AvgPool2d(2) backward).
+ * Replaces the input-gradient of nn.Conv2d.backward (+ the residual-branch add). */
+int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx,
+                         const void* res, int res_mode, void* stream);
+
+/* ---- layout / parameter packing ---------------------------------------- */
+/* x.type(weight dtype) + NCHW -> NHWC8 (models.py:352); x [B][Cin<=8][H][W] f32. */
+int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, void* out, void* stream);
+/* src [Co][Ci][R][S] f32 (state_dict layout) -> mode 0: [Co][R][S][ci_pad] (forward
+ * operand); mode 1: flipped [Ci][R][S] rows of stride ldo (data-gradient operand). */
+int artsbir_pack_weight(int dtype, const float* src, int Co, int Ci, int R, int S, int ci_pad, int mode,
+                        long long ldo, void* dst, void* stream);
+/* wgrad workspace [Co][R][S][Cp] f32 -> parameter-gradient layout [Co][Ci][R][S]. */
+int artsbir_unpack_wgrad(const float* src, int Co, int Ci, int R, int S, int Cp, float* dst, void* stream);
+int artsbir_cast(int src_dtype, const void* x, int dst_dtype, void* y, long long n, void* stream);
+
+/* ---- batch norm / activations (models.py BatchNorm2d, ReLU, AvgPool2d) -- */
+/* train: mean/var from stats slots, running stats updated (momentum, unbiased
+ * var), num_batches_tracked += 1; eval: from running stats.  Outputs per-channel
+ * mean, istd, scale = gamma*istd, shift = beta - mean*scale. */
+int artsbir_bn_finalize(const float* stats, int C, double count, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, long long* num_batches_tracked,
+                        float momentum, float eps, int train, float* mean, float* istd, float* scale,
+                        float* shift, void* stream);
+/* out = avgpool_pool( relu?(x*scale+shift) ) (scale == NULL: no affine). */
+int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* shift, int relu, int pool,
+                     int B, int H, int W, int C, void* out, void* stream);
+/* Bottleneck tail (models.py:234-235): out = relu(bn3(y3) + (bn_d(yd) | identity)). */
+int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
+                      const float* scd, const float* shd, const void* identity, long long rows, int C,
+                      void* out, void* stream);
+
+/* BatchNorm2d(train) backward, see elementwise.hip for the math. */
+typedef struct artsbir_bn_bwd_desc {
+  int dtype;
+  int kind;               /* 0: g = d*(mask>0) (block output); 1: g = up(d)*(y*mask_scale+mask_shift>0) */
+  int pool;               /* kind 1: d is at 1/pool resolution (AvgPool backward) */
+  const void* d;
+  const void* mask;
+  const float* mask_scale;
+  const float* mask_shift;
+  int ntarget;            /* 1 or 2 BN inputs sharing g */
+  const void* y[2];
+  const float* mean[2];
+  const float* istd[2];
+  float* slots[2];        /* reduce: [NSLOT][2][C] */
+  const float* coef[2];   /* apply: [3][C] from artsbir_bn_bwd_finalize */
+  void* dy[2];            /* apply outputs */
+  void* gout;             /* apply: optional copy of g */
+  int B, H, W, C;
+} artsbir_bn_bwd_desc;
+int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
+int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,
+                            float* dgamma, float* dbeta, float* coef, void* stream);
+int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream);
+/* out[c] += sum_r x[r*ld + c]  (bias / positional-embedding gradients). */
+int artsbir_colsum(int dtype, const void* x, long long rows, long long ld, long long C, float* out, void* stream);
+
+/* ---- attention pool (models.py:249-272) --------------------------------- */
+int artsbir_tokens_fwd(int dtype, const void* h, const float* pos, int B, int P, int C, void* tok, void* stream);
+int artsbir_tokens_bwd(int dtype, const float* dtok, int B, int P, int C, void* dh, void* stream);
+int artsbir_attnpool_fwd(int dtype, const float* q, const void* kv, int B, int C, int heads, int T,
+                         float* p, void* o, void* stream);
+int artsbir_attnpool_bwd(int dtype, const float* q, const void* kv, const float* p, const float* dout,
+                         int B, int C, int heads, int T, void* dq, void* dkv, void* stream);
+
+/* ---- loss and optimizer (train.py:158,169) ------------------------------ */
+int artsbir_triplet_fwd(const float* a, const float* p, const float* n, int B, int D, float margin, float eps,
+                        float* dist, float* loss, void* stream);
+int artsbir_triplet_bwd(const float* a, const float* p, const float* n, int B, int D, float margin, float eps,
+                        const float* dist, const float* grad_loss, float* da, float* dp, float* dn, void* stream);
+/* Adam over a device table of {param, grad, exp_avg, exp_avg_sq, numel} records
+ * (host helpers size and fill the per-block table). */
+long long artsbir_adam_table_blocks(const long long* numels, int ntensors, long long chunk);
+int artsbir_adam_fill_table(const long long* numels, int ntensors, long long chunk, long long* table);
+int artsbir_adam_step(const void* tensors, const long long* block_table, long long nblocks, long long chunk,
+                      float lr, float beta1, float beta2, float eps, float weight_decay, long long step,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

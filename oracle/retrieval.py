@@ -1,0 +1,116 @@
+"""Retrieval metrics on CPU in numpy (TEST ORACLE).
+
+Follows /root/reference/inference.py and utils.py:
+  get_ranking_position  inference.py:30-57 (name parsing, first matching gallery
+                        path, distance, full sort, position of the positive)
+  get_topk_images       inference.py:60-69
+  process_inference     inference.py:94-136 (rank+1, MRR, topk_acc[rank:] += 1,
+                        pandas describe() of ranks)
+  find_image_index      utils.py:22-25
+  euclidean_distance    utils.py:42  nn.PairwiseDistance(p=2, eps=1e-6): ||x1-x2+eps||
+  cosine_distance       utils.py:31-40  1 - cos(x1,x2) (CosineSimilarity eps=1e-8)
+  InferenceDataset      data_preparation.py:24-41 (dedup, then sort the gallery paths)
+
+"Exact" distances here are evaluated in float64 from float32 inputs and the
+sort is stable on (distance, gallery index): this is the total order the HIP
+retrieval path must reproduce bit-exactly (torch.topk leaves the order of
+equal distances unspecified, so a tie rule has to be fixed somewhere).
+"""
+from __future__ import annotations
+
+import re
+from pathlib import Path
+
+import numpy as np
+
+EPS = 1e-6
+
+
+def l2_distances(q: np.ndarray, g: np.ndarray) -> np.ndarray:
+    """||q - g_i + eps||_2 for every gallery row, float64.  q [D], g [N, D]."""
+    d = (q.astype(np.float64)[None, :] - g.astype(np.float64)) + EPS
+    return np.sqrt(np.einsum("nd,nd->n", d, d))
+
+
+def cosine_distances(q: np.ndarray, g: np.ndarray, eps: float = 1e-8) -> np.ndarray:
+    q64, g64 = q.astype(np.float64), g.astype(np.float64)
+    num = g64 @ q64
+    den = np.maximum(np.linalg.norm(g64, axis=1) * np.linalg.norm(q64), eps)
+    return 1.0 - num / den
+
+
+def order(dist: np.ndarray) -> np.ndarray:
+    """Ascending order with ties broken by lower index (stable sort)."""
+    return np.argsort(dist, kind="stable")
+
+
+def topk(dist: np.ndarray, k: int):
+    idx = order(dist)[:k]
+    return idx, dist[idx]
+
+
+def rank_of(dist: np.ndarray, pos: int) -> int:
+    """0-based position of gallery item `pos` in the stable ascending order."""
+    d = dist[pos]
+    return int(np.count_nonzero(dist < d) + np.count_nonzero(dist[:pos] == d))
+
+
+def find_image_index(image_paths, name: str) -> int:
+    """utils.py:22-25 — first path whose stem equals `name`, else -1."""
+    for i, p in enumerate(image_paths):
+        if Path(p).stem == name:
+            return i
+    return -1
+
+
+def positive_name(sketch_path, image_paths) -> str:
+    """inference.py:33-37 sketch-name parsing."""
+    stem = Path(sketch_path).stem
+    parts = re.split('-', stem)
+    if len(parts) <= 2:
+        return stem if "artworks" in str(image_paths[0]) else parts[0]
+    if len(parts) == 3:
+        return parts[1]
+    return parts  # the reference leaves a list here; it never matches a stem
+
+
+def inference_dataset_paths(paths):
+    """data_preparation.py:30-31 — dedup keeping first occurrence, then sort."""
+    return sorted(dict.fromkeys(paths))
+
+
+def describe(ranks) -> dict:
+    """pandas DataFrame.describe() of the 1-based ranks (ddof=1 std, linear quantiles)."""
+    r = np.asarray(ranks, np.float64)
+    out = {"count": float(len(r)), "mean": float(r.mean())}
+    out["std"] = float(r.std(ddof=1)) if len(r) > 1 else float("nan")
+    out["min"] = float(r.min())
+    for q, key in ((0.25, "25%"), (0.5, "50%"), (0.75, "75%")):
+        out[key] = float(np.quantile(r, q))
+    out["max"] = float(r.max())
+    return out
+
+
+def metrics(ranks0, k: int = 10) -> dict:
+    """inference.py:116-134 from 0-based ranks; adds mAP@k (one relevant item per
+    query => mean of 1/rank over queries whose rank <= k)."""
+    ranks1 = [r + 1 for r in ranks0]
+    mrr = float(np.mean([1.0 / r for r in ranks1]))
+    acc = np.zeros(k)
+    for r in ranks0:
+        if r < k:
+            acc[r:] += 1
+    acc /= len(ranks0)
+    out = {"mean_reciprocal_rank": mrr}
+    out.update(describe(ranks1))
+    out["topk_acc"] = [float(a) for a in acc]
+    out[f"map@{k}"] = float(np.mean([1.0 / r if r <= k else 0.0 for r in ranks1]))
+    return out
+
+
+def synthetic_gallery(n: int, d: int, q: int, seed_g: int = 7, seed_q: int = 8, noise: float = 0.5):
+    """G ~ N(0,1) [n,d]; query i = G[p_i] + noise*N(0,1), p_i = (i*7919) mod n."""
+    g = np.random.Generator(np.random.PCG64(seed_g)).standard_normal((n, d), dtype=np.float32)
+    pos = (np.arange(q, dtype=np.int64) * 7919) % n
+    qs = g[pos] + noise * np.random.Generator(np.random.PCG64(seed_q)).standard_normal((q, d), dtype=np.float32)
+    return g, qs.astype(np.float32), pos

@@ -1,0 +1,115 @@
+"""Encoder forward / triplet step on libartsbir_hip vs the CPU oracle (f32 parity mode)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import encoder as oenc
+from oracle import steps as osteps
+
+pytestmark = pytest.mark.gpu
+
+TINY = dict(layers=(1, 1, 1, 1), output_dim=32, heads=8, res=64, width=16)
+SMALL = dict(layers=(2, 2, 2, 2), output_dim=128, heads=8, res=64, width=16)
+
+
+def _pair(cfg, dev, dtype=torch.float32, seed=1234):
+    import models
+    ref = osteps.build(cfg["layers"], cfg["output_dim"], cfg["heads"], cfg["res"], cfg["width"], seed=seed)
+    mine = models.ModifiedResNet(cfg["layers"], cfg["output_dim"], heads=cfg["heads"],
+                                 input_resolution=cfg["res"], width=cfg["width"])
+    mine.load_state_dict(ref.state_dict(), strict=True)
+    mine.compute_dtype = dtype
+    return ref, mine.to(dev)
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / (b.abs().max() + 1e-12))
+
+
+@pytest.mark.parametrize("cfg", [TINY, SMALL], ids=["tiny", "small"])
+def test_forward_train_and_eval_f32(cfg, dev):
+    ref, mine = _pair(cfg, dev)
+    s, p, n = oenc.synthetic_triplet(4, cfg["res"])
+    ref.train(); mine.train()
+    with torch.no_grad():
+        for x in (s, p, n):
+            e_ref = ref(x)
+            e = mine(x.to(dev)).cpu()
+            assert torch.allclose(e, e_ref, atol=1e-3, rtol=1e-3), _rel(e, e_ref)
+    # running statistics after three train-mode forwards
+    sd_ref, sd = ref.state_dict(), mine.state_dict()
+    for k in sd_ref:
+        if "running" in k or "num_batches" in k:
+            assert torch.allclose(sd[k].cpu().double(), sd_ref[k].double(), atol=1e-4, rtol=1e-4), k
+    ref.eval(); mine.eval()
+    with torch.no_grad():
+        e_ref = ref(s)
+        e = mine(s.to(dev)).cpu()
+    assert torch.allclose(e, e_ref, atol=1e-3, rtol=1e-3), _rel(e, e_ref)
+
+
+@pytest.mark.parametrize("cfg", [TINY, SMALL], ids=["tiny", "small"])
+def test_triplet_step_f32(cfg, dev):
+    import losses
+    import optim
+    ref, mine = _pair(cfg, dev)
+    elements = oenc.synthetic_triplet(4, cfg["res"], seed=3)
+    opt_ref = osteps.make_optimizer(ref, lr=1e-3, weight_decay=0.002)
+    loss_ref, emb_ref = osteps.train_step(ref, opt_ref, osteps.make_loss(0.2), list(elements))
+
+    opt = optim.Adam(mine.parameters(), lr=1e-3, weight_decay=0.002)
+    mine.train()
+    loss_fn = losses.TripletMarginLoss(margin=0.2)
+    outs = [mine(e.to(dev)) for e in elements]
+    loss = loss_fn(*outs)
+    opt.zero_grad()
+    loss.backward()
+    grads = {k: p.grad.detach().cpu().clone() for k, p in mine.named_parameters()}
+    before = {k: p.detach().cpu().clone() for k, p in mine.named_parameters()}
+    opt.step()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref.item()) < 1e-4 * max(1.0, abs(loss_ref.item()))
+    # gradients: the triplet loss at batch 4 is ill-conditioned (the oracle's own
+    # f32 gradients differ from its f64 gradients by up to a few 1e-2 relative), so
+    # the bar is "as accurate as the reference's f32 path": error vs the f64 oracle
+    # within max(2e-3, 4 x the f32 oracle's own error).
+    def ref_grads(dtype):
+        r = osteps.build(cfg["layers"], cfg["output_dim"], cfg["heads"], cfg["res"], cfg["width"]).to(dtype)
+        r.train()
+        l, _ = osteps.get_loss(osteps.make_loss(0.2), r, [e.to(dtype) for e in elements])
+        l.backward()
+        return {k: q.grad.double() for k, q in r.named_parameters()}
+    g64, g32 = ref_grads(torch.float64), ref_grads(torch.float32)
+    floor = 1e-4 * max(g.abs().max().item() for g in g64.values())
+    for k, g_ref in g64.items():
+        scale = max(g_ref.abs().max().item(), floor)
+        e_ref = (g32[k] - g_ref).abs().max().item() / scale
+        e_mine = (grads[k].double() - g_ref).abs().max().item() / scale
+        assert e_mine <= max(2e-3, 4 * e_ref), (k, e_mine, e_ref)
+    # parameters after one Adam step: the HIP Adam vs the float64 restatement of
+    # torch.optim.Adam applied to the same gradients (first-step Adam is ~lr*sign(g),
+    # so comparing against the reference parameters would test sign noise of ~0 grads)
+    from oracle import numpy_ref
+    for k, p in mine.named_parameters():
+        z = np.zeros(p.shape)
+        want, _, _ = numpy_ref.adam_step(before[k].double().numpy(), grads[k].double().numpy(), z, z, 1,
+                                         lr=1e-3, wd=0.002)
+        assert np.allclose(p.detach().cpu().double().numpy(), want, atol=1e-6, rtol=1e-5), k
+    # and the BN running statistics of the three train-mode forwards
+    sd_ref = ref.state_dict()
+    for k, v in mine.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            assert torch.allclose(v.cpu().double(), sd_ref[k].double(), atol=1e-4, rtol=1e-4), k
+
+
+def test_forward_bf16_close(dev):
+    ref, mine = _pair(SMALL, dev, dtype=torch.bfloat16)
+    s, _, _ = oenc.synthetic_triplet(8, SMALL["res"])
+    ref.train(); mine.train()
+    with torch.no_grad():
+        e_ref = ref(s)
+        e = mine(s.to(dev)).cpu()
+    cos = torch.nn.functional.cosine_similarity(e, e_ref, dim=1)
+    assert cos.min() > 0.98, cos  # bf16 activations through 8 blocks of batch-8 BN
