@@ -102,12 +102,37 @@ class HipError(RuntimeError):
     pass
 
 
-def call(name: str, *args) -> None:
+# Optional live per-launch timing (bench.py): when PROFILE is a list, every call
+# that declares its algorithmic work is bracketed by two timing events on the
+# current stream and (kernel, flops, bytes, start, end) is appended.
+PROFILE = None
+
+
+def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes: float = 0.0) -> None:
     """Invoke a status-returning entry point; map a non-zero status to HipError."""
-    rc = getattr(lib(), name)(*args)
+    prof = PROFILE
+    if prof is not None and kernel is not None:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = getattr(lib(), name)(*args)
+        e1.record()
+        prof.append((kernel, flops, nbytes, e0, e1))
+    else:
+        rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().artsbir_last_error().decode(errors="replace")
         raise HipError(f"{name} failed ({rc}): {msg}")
+
+
+def conv_kernel_name(dtype_code: int, cout: int) -> str:
+    """kernel template artsbir_conv2d_fwd / _dgrad / gemm_nt launch for this width"""
+    t = "bf16" if dtype_code == DT_BF16 else "f32"
+    return f"conv_gemm_kernel<{t},128,{64 if cout <= 64 else 128}>"
+
+
+def wgrad_kernel_name(dtype_code: int) -> str:
+    return f"wgrad_kernel<{'bf16' if dtype_code == DT_BF16 else 'f32'},128,128>"
 
 
 def ptr(t) -> int | None:

@@ -311,8 +311,8 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ slots, int C, d
     s1 += slots[(long long)k * 2 * C + c];
     s2 += slots[(long long)k * 2 * C + C + c];
   }
-  if (dbeta) dbeta[c] = (float)s1;
-  if (dgamma) dgamma[c] = (float)s2;
+  if (dbeta) dbeta[c] += (float)s1;   // parameter gradients accumulate
+  if (dgamma) dgamma[c] += (float)s2;
   coef[c] = gamma[c] * istd[c];
   coef[C + c] = (float)(s1 / count);
   coef[2 * C + c] = (float)(s2 / count);
@@ -373,7 +373,7 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, int Co, int Ci
   }
 }
 
-// wgrad workspace [Co][R][S][Cp] f32 -> parameter-gradient layout [Co][Ci][R][S]
+// wgrad workspace [Co][R][S][Cp] f32 -> += parameter-gradient layout [Co][Ci][R][S]
 __global__ void unpack_wgrad_kernel(const float* __restrict__ src, int Co, int Ci, int R, int S, int Cp,
                                     float* __restrict__ dst) {
   const long long n = (long long)Co * Ci * R * S;
@@ -383,7 +383,7 @@ __global__ void unpack_wgrad_kernel(const float* __restrict__ src, int Co, int C
     int r = (int)(t % R); t /= R;
     int ci = (int)(t % Ci);
     int co = (int)(t / Ci);
-    dst[i] = src[(((long long)co * R + r) * S + s) * Cp + ci];
+    dst[i] += src[(((long long)co * R + r) * S + s) * Cp + ci];  // accumulate
   }
 }
 

@@ -167,6 +167,14 @@ class Engine:
         return pk
 
     # ------------------------------------------------------------- primitives
+    def _gemm_nt(self, M, N, K, a, lda, b, c, ldc, out_f32, acc, bias):
+        call("artsbir_gemm_nt", self.dt, M, N, K, ptr(a), lda, ptr(b), ptr(c), ldc, out_f32, acc, ptr(bias), None,
+             _s(), kernel=_hip.conv_kernel_name(self.dt, N), flops=2.0 * M * N * K)
+
+    def _gemm_tn(self, M, N, K, dy, ldd, x, ldx, dw):
+        call("artsbir_gemm_tn", self.dt, M, N, K, ptr(dy), ldd, ptr(x), ldx, ptr(dw), _s(),
+             kernel=_hip.wgrad_kernel_name(self.dt), flops=2.0 * M * N * K)
+
     def _conv(self, a: Act, fw, cout, R, S, stride, pad, stats_buf=None):
         B, H, W, C = a.shape
         Ho = (H + 2 * pad - R) // stride + 1
@@ -176,7 +184,8 @@ class Engine:
         bn = a.bn
         call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None,
              ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None, a.relu,
-             ptr(stats_buf), _s())
+             ptr(stats_buf), _s(), kernel=_hip.conv_kernel_name(self.dt, cout),
+             flops=2.0 * B * Ho * Wo * cout * R * S * C)
         return y
 
     def _bn(self, bnmod, stats_buf, count, train):
@@ -281,20 +290,26 @@ class Engine:
         call("artsbir_tokens_fwd", self.dt, ptr(h), ptr(ap.positional_embedding.detach()), B, P, C, ptr(tok), _s())
         wkv, _, bkv = pk["kv"]
         kv = self._empty(B * Tk, 2 * C, device=dev)
-        call("artsbir_gemm_nt", self.dt, B * Tk, 2 * C, C, ptr(tok), C, ptr(wkv), ptr(kv), 2 * C, 0, 0, ptr(bkv),
-             None, _s())
+        self._gemm_nt(B * Tk, 2 * C, C, tok, C, wkv, kv, 2 * C, 0, 0, bkv)
         wq, _, bq = pk["q"]
         q = torch.empty(B, C, dtype=torch.float32, device=dev)
-        call("artsbir_gemm_nt", self.dt, B, C, C, ptr(tok), Tk * C, ptr(wq), ptr(q), C, 1, 0, ptr(bq), None, _s())
+        self._gemm_nt(B, C, C, tok, Tk * C, wq, q, C, 1, 0, bq)
         pm = torch.empty(B, heads, Tk, dtype=torch.float32, device=dev)
         o = self._empty(B, C, device=dev)
         call("artsbir_attnpool_fwd", self.dt, ptr(q), ptr(kv), B, C, heads, Tk, ptr(pm), ptr(o), _s())
         wc, _, bc = pk["c"]
         out = torch.empty(B, D, dtype=torch.float32, device=dev)
-        call("artsbir_gemm_nt", self.dt, B, D, C, ptr(o), C, ptr(wc), ptr(out), D, 1, 0, ptr(bc), None, _s())
+        self._gemm_nt(B, D, C, o, C, wc, out, D, 1, 0, bc)
         return out, dict(tok=tok, kv=kv, q=q, pm=pm, o=o, P=P, Tk=Tk, hw=(Hs, Ws))
 
     # --------------------------------------------------------------- backward
+    def grad_buffer(self, device):
+        gb = getattr(self, "_grads", None)
+        if gb is None or gb.flat.device != device or gb.flat.numel() != sum(p.numel() for p in self.model.parameters()):
+            gb = self._grads = GradBuffer(self.model, device)
+        gb.attach()
+        return gb
+
     def backward(self, ctx, dout: torch.Tensor):
         if ctx is None:
             raise RuntimeError("backward through a forward that did not save activations")
@@ -303,7 +318,7 @@ class Engine:
         m = self.model
         pk = self.packed()
         dev = dout.device
-        grads = GradBuffer(m, dev)
+        grads = self.grad_buffer(dev)
         ws = _Arena(torch.zeros(max(2 * NSLOT * m.total_bn_channels() * 2, 1), dtype=torch.float32, device=dev),
                     NSLOT * 2)
         dh = self._attnpool_bwd(m.attnpool, pk, ctx["attn"], dout.contiguous().float(), grads)
@@ -325,25 +340,23 @@ class Engine:
         else:
             doutT = self._empty(B, D, device=dev)
             call("artsbir_cast", _hip.DT_F32, ptr(dout), self.dt, ptr(doutT), B * D, _s())
-        call("artsbir_gemm_tn", self.dt, B, D, C, ptr(doutT), D, ptr(o), C, ptr(grads[ap.c_proj.weight]), _s())
+        self._gemm_tn(B, D, C, doutT, D, o, C, grads[ap.c_proj.weight])
         _, wcT, _ = pk["c"]
         do = torch.empty(B, C, dtype=torch.float32, device=dev)
-        call("artsbir_gemm_nt", self.dt, B, C, D, ptr(doutT), D, ptr(wcT), ptr(do), C, 1, 0, None, None, _s())
+        self._gemm_nt(B, C, D, doutT, D, wcT, do, C, 1, 0, None)
         dq = self._empty(B, C, device=dev)
         dkv = self._empty(B * Tk, 2 * C, device=dev)
         call("artsbir_attnpool_bwd", self.dt, ptr(q), ptr(kv), ptr(pm), ptr(do), B, C, heads, Tk, ptr(dq), ptr(dkv),
              _s())
         call("artsbir_colsum", self.dt, ptr(dq), B, C, C, ptr(grads[ap.q_proj.bias]), _s())
         call("artsbir_colsum", self.dt, ptr(dkv), B * Tk, 2 * C, 2 * C, ptr(grads[ap.k_proj.bias]), _s())
-        call("artsbir_gemm_tn", self.dt, B, C, C, ptr(dq), C, ptr(tok), Tk * C, ptr(grads[ap.q_proj.weight]), _s())
-        call("artsbir_gemm_tn", self.dt, B * Tk, 2 * C, C, ptr(dkv), 2 * C, ptr(tok), C,
-             ptr(grads[ap.k_proj.weight]), _s())
+        self._gemm_tn(B, C, C, dq, C, tok, Tk * C, grads[ap.q_proj.weight])
+        self._gemm_tn(B * Tk, 2 * C, C, dkv, 2 * C, tok, C, grads[ap.k_proj.weight])
         _, wkvT, _ = pk["kv"]
         _, wqT, _ = pk["q"]
         dtok = torch.empty(B, Tk, C, dtype=torch.float32, device=dev)
-        call("artsbir_gemm_nt", self.dt, B * Tk, C, 2 * C, ptr(dkv), 2 * C, ptr(wkvT), ptr(dtok), C, 1, 0, None, None,
-             _s())
-        call("artsbir_gemm_nt", self.dt, B, C, C, ptr(dq), C, ptr(wqT), ptr(dtok), Tk * C, 1, 1, None, None, _s())
+        self._gemm_nt(B * Tk, C, 2 * C, dkv, 2 * C, wkvT, dtok, C, 1, 0, None)
+        self._gemm_nt(B, C, C, dq, C, wqT, dtok, Tk * C, 1, 1, None)
         call("artsbir_colsum", _hip.DT_F32, ptr(dtok), B, Tk * C, Tk * C, ptr(grads[ap.positional_embedding]), _s())
         Hs, Ws = c["hw"]
         dh = self._empty(B, Hs, Ws, C, device=dev)
@@ -396,8 +409,10 @@ class Engine:
             target = g
         else:
             target = torch.zeros(co, R, S, C, dtype=torch.float32, device=dy.device)
+        Ho, Wo = dy.shape[1], dy.shape[2]
         call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), ptr(bn.scale) if bn else None,
-             ptr(bn.shift) if bn else None, a.relu, ptr(target), _s())
+             ptr(bn.shift) if bn else None, a.relu, ptr(target), _s(), kernel=_hip.wgrad_kernel_name(self.dt),
+             flops=2.0 * B * Ho * Wo * co * R * S * C)
         if target is not g:
             call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
 
@@ -406,7 +421,8 @@ class Engine:
         co, _, R, S = conv.weight.shape
         dx = self._empty(B, H, W, C, device=dy.device)
         d = self._desc(B, H, W, C, co, R, S, 1, pad)
-        call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s())
+        call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
+             kernel=_hip.conv_kernel_name(self.dt, C), flops=2.0 * B * H * W * C * R * S * co)
         return dx
 
     def _block_bwd(self, blk, bp, c, dout, grads, ws):
@@ -465,20 +481,37 @@ class _Arena:
 
 
 class GradBuffer:
-    """One zeroed f32 buffer holding the gradient of every parameter in the
-    reference layout.  k_proj/v_proj weights and biases are adjacent so the
-    fused K|V GEMMs write both at once."""
+    """One persistent f32 buffer holding the gradient of every parameter in the
+    reference layout; ``param.grad`` are views into it.  Every backward kernel
+    ACCUMULATES into it, so the three branch backwards of a triplet step sum
+    in place (no autograd AccumulateGrad traffic), the optimizer sees stable
+    pointers, and data-parallel training all-reduces one contiguous buffer.
+    k_proj/v_proj weights and biases are adjacent so the fused K|V GEMMs write
+    both at once."""
 
     def __init__(self, model, device):
-        order = model.grad_order()
-        total = sum(p.numel() for p in order)
+        self.order = model.grad_order()
+        total = sum(p.numel() for p in self.order)
         self.flat = torch.zeros(total, dtype=torch.float32, device=device)
         self.views = {}
         off = 0
-        for p in order:
+        for p in self.order:
             n = p.numel()
             self.views[id(p)] = self.flat[off:off + n].view(p.shape)
             off += n
 
     def __getitem__(self, p):
         return self.views[id(p)]
+
+    def attach(self):
+        """Make every param.grad a view of the buffer.  If any .grad was reset
+        (optimizer.zero_grad(set_to_none=True)) or replaced, start from zero and
+        carry over gradients that exist."""
+        if all(p.grad is not None and p.grad.data_ptr() == self.views[id(p)].data_ptr() for p in self.order):
+            return
+        self.flat.zero_()
+        for p in self.order:
+            v = self.views[id(p)]
+            if p.grad is not None:
+                v.copy_(p.grad)
+            p.grad = v

@@ -112,16 +112,18 @@ class _EncoderFunction(torch.autograd.Function):
         eng = model._hip_engine
         eng.dtype = model.compute_dtype
         out, state = eng.forward(x, model.training, save=True)
-        ctx.state, ctx.model, ctx.dtype = state, model, model.compute_dtype
+        ctx.state, ctx.model, ctx.dtype, ctx.nparams = state, model, model.compute_dtype, len(params)
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        # parameter gradients are accumulated in place into param.grad (views of
+        # the engine's flat gradient buffer) by the HIP kernels themselves
         eng = ctx.model._hip_engine
         eng.dtype = ctx.dtype
-        grads = eng.backward(ctx.state, dout)
+        eng.backward(ctx.state, dout)
         ctx.state = None
-        return (None, None) + tuple(grads[p] for p in ctx.model.parameters())
+        return (None, None) + (None,) * ctx.nparams
 
 
 class ModifiedResNet(nn.Module):

@@ -78,7 +78,7 @@ int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, 
  * operand); mode 1: flipped [Ci][R][S] rows of stride ldo (data-gradient operand). */
 int artsbir_pack_weight(int dtype, const float* src, int Co, int Ci, int R, int S, int ci_pad, int mode,
                         long long ldo, void* dst, void* stream);
-/* wgrad workspace [Co][R][S][Cp] f32 -> parameter-gradient layout [Co][Ci][R][S]. */
+/* wgrad workspace [Co][R][S][Cp] f32 -> dst[Co][Ci][R][S] += (parameter-gradient layout). */
 int artsbir_unpack_wgrad(const float* src, int Co, int Ci, int R, int S, int Cp, float* dst, void* stream);
 int artsbir_cast(int src_dtype, const void* x, int dst_dtype, void* y, long long n, void* stream);
 
@@ -118,6 +118,7 @@ typedef struct artsbir_bn_bwd_desc {
   int B, H, W, C;
 } artsbir_bn_bwd_desc;
 int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
+/* dgamma += sum g*xhat, dbeta += sum g; coef = [gamma*istd, sum g/cnt, sum g*xhat/cnt]. */
 int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,
                             float* dgamma, float* dbeta, float* coef, void* stream);
 int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream);
