@@ -21,14 +21,33 @@
 //         with one ds_read_b128 and issues 4 MFMAs, element e in step e.  The
 //         k order inside the MFMA is a permutation applied identically to A
 //         and B, so the sum is unchanged.
+//
+// Global loads are raw buffer loads: an out-of-range byte offset returns zero,
+// which implements both the convolution zero padding and every M/N/K tail
+// without a branch.  Per thread, the A rows it stages are decoded once
+// (pixel offset + one validity bit per filter tap); per K-step only the tap
+// (r, s, ci) changes, and when C is a multiple of the K-step it is uniform
+// across the workgroup (scalar arithmetic).
 #include "common.h"
 
 namespace artsbir {
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+#define OOB_OFFSET 0x80000000u
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, long long bytes) {
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  if (bytes < 0) bytes = 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 template <typename T> struct MM;
 template <> struct MM<bf16> {
   static constexpr int EPC = 8;  // elements per 16-B chunk
-  typedef bf16x8 frag;
   __device__ __forceinline__ static void mma(f32x4& acc, const uint4& a, const uint4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&a),
                                                   *reinterpret_cast<const bf16x8*>(&b), acc, 0, 0, 0);
@@ -44,6 +63,38 @@ template <> struct MM<float> {
   }
 };
 
+// affine(+relu) of one 16-B chunk of T for channels sc/sh[0..EPC)
+__device__ __forceinline__ uint4 affine_chunk(uint4 v, const float* sc, const float* sh, int relu, bf16) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float lo = __uint_as_float(w[i] << 16), hi = __uint_as_float(w[i] & 0xffff0000u);
+    lo = lo * sc[2 * i] + sh[2 * i];
+    hi = hi * sc[2 * i + 1] + sh[2 * i + 1];
+    if (relu) { lo = fmaxf(lo, 0.f); hi = fmaxf(hi, 0.f); }
+    bf16 blo = (bf16)lo, bhi = (bf16)hi;
+    w[i] = (uint32_t)__builtin_bit_cast(unsigned short, blo) | ((uint32_t)__builtin_bit_cast(unsigned short, bhi) << 16);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint4 affine_chunk(uint4 v, const float* sc, const float* sh, int relu, float) {
+  float f[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[i] = f[i] * sc[i] + sh[i];
+    if (relu) f[i] = fmaxf(f[i], 0.f);
+  }
+  return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+}
+
+// bijective XCD-aware block remap: blocks that share an XCD (bid % 8) get
+// consecutive logical ids, so neighbouring tiles (same A panel) share an L2.
+__device__ __forceinline__ long long xcd_remap(long long bid, long long nwg) {
+  if (nwg < 8) return bid;
+  const long long q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
 // ---------------------------------------------------------------------------
 // Forward / data-gradient implicit GEMM:  Y[m][n] = sum_k Xcol[m][k] * W[n][k]
 //   Xcol[m=(img,oh,ow)][k=(r,s,ci)] = act(X[img][oh*st-pad+r][ow*st-pad+s][ci])
@@ -51,6 +102,7 @@ template <> struct MM<float> {
 // ---------------------------------------------------------------------------
 struct ConvArgs {
   const void* x;
+  long long x_elems;     // extent of x (elements) for the bounds check
   long long sN, sH, sW;  // element strides of x (channel stride 1)
   int H, W, C;
   int R, S, stride, pad;
@@ -66,104 +118,130 @@ struct ConvArgs {
   int out_f32;
   int accumulate;
   const float* bias;
-  float* stats;  // [NSLOT][2][Cout]
+  float* stats;     // [NSLOT][2][Cout]
   const void* res;  // epilogue residual (T): mode 1 same index, mode 2 2x2 average-unpool
   int res_mode;
 };
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool UNIFORM_TAP, bool AFFINE>
 __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
   constexpr int EPC = MM<T>::EPC;
+  constexpr int ES = sizeof(T);
   constexpr int BK = 8 * EPC;  // 8 chunks per K-step (128 bytes of k per row)
   constexpr int A_BYTES = 8 * (BM + 1) * 16;
   constexpr int B_BYTES = 8 * (BN + 1) * 16;
   constexpr int ARows = BM / 32;  // rows per thread in the A loader
   constexpr int BRows = BN / 32;
-  constexpr int WTM = BM / 2, WTN = BN / 2;  // 2x2 waves
+  constexpr int WN = BN >= 128 ? 2 : 1;  // waves along N
+  constexpr int WM = 4 / WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  constexpr int MAIN_BYTES = 2 * (A_BYTES + B_BYTES);
+  constexpr int EPI_LD = BN + 4;  // f32 staging row stride
+  constexpr int EPI_BYTES = BM * EPI_LD * 4;
+  constexpr int SMEM = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
 
-  // block -> tile; consecutive blocks walk N first so the A panel is reused from L2
   const int ntn = (a.Cout + BN - 1) / BN;
-  const long long bid = blockIdx.x;
-  const long long bm = (bid / ntn) * BM;
-  const int bn = (int)(bid % ntn) * BN;
+  const long long ntm = (a.M + BM - 1) / BM;
+  const long long lid = xcd_remap(blockIdx.x, ntm * ntn);
+  const long long bm = (lid / ntn) * BM;
+  const int bn = (int)(lid % ntn) * BN;
 
-  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
-  const T* __restrict__ Wt = reinterpret_cast<const T*>(a.w);
-
-  const int lc = tid & 7;    // chunk handled by this thread
-  const int lr = tid >> 3;   // first row handled by this thread
-  // per-row decode of the A rows this thread loads
-  long long abase[ARows];
-  int aih[ARows], aiw[ARows];
-  bool avalid[ARows];
   const int HoWo = a.Ho * a.Wo;
+  const long long img0 = bm / HoWo;
+  const __amdgpu_buffer_rsrc_t xr =
+      make_rsrc(reinterpret_cast<const T*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * ES);
+  const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, (long long)a.Cout * a.K * ES);
+
+  const int lc = tid & 7;   // chunk handled by this thread
+  const int lr = tid >> 3;  // first row handled by this thread
+  int rowoff[ARows];
+  unsigned rmask[ARows];
 #pragma unroll
   for (int i = 0; i < ARows; ++i) {
-    long long gm = bm + lr + 32 * i;
-    avalid[i] = gm < a.M;
-    long long gmc = avalid[i] ? gm : 0;
-    long long img = gmc / HoWo;
-    int rem = (int)(gmc - img * HoWo);
-    int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-    abase[i] = img * a.sN;
-    aih[i] = oh * a.stride - a.pad;
-    aiw[i] = ow * a.stride - a.pad;
+    const long long gm = bm + lr + 32 * i;
+    const bool valid = gm < a.M;
+    const long long gmc = valid ? gm : bm;
+    const long long img = gmc / HoWo;
+    const int rem = (int)(gmc - img * HoWo);
+    const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    rowoff[i] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * ES);
+    unsigned msk = 0;
+    for (int r = 0; r < a.R; ++r)
+      for (int s = 0; s < a.S; ++s) {
+        const bool ok = valid && ih0 + r >= 0 && ih0 + r < a.H && iw0 + s >= 0 && iw0 + s < a.W;
+        msk |= (ok ? 1u : 0u) << (r * a.S + s);
+      }
+    rmask[i] = msk;
+  }
+  int boff[BRows];
+#pragma unroll
+  for (int i = 0; i < BRows; ++i) {
+    const int n = bn + lr + 32 * i;
+    boff[i] = n < a.Cout ? n * a.K * ES + lc * 16 : (int)OOB_OFFSET;
   }
 
-  Vec16<T> ra[ARows], rb[BRows];
+  uint4 ra[ARows], rb[BRows];
 
+  // uniform taps: (ci, s, r) of the K-step advance incrementally (no division)
+  int u_ci = 0, u_s = 0, u_r = 0;
   auto load_tiles = [&](int kt) {
-    const int k = kt * BK + lc * EPC;
-    const bool kval = k < a.K;
-    int rs = kval ? k / a.C : 0;
-    int ci = k - rs * a.C;
-    int r = rs / a.S, s = rs - (rs / a.S) * a.S;
-    float sc[EPC], sh[EPC];
-    const bool aff = a.in_scale != nullptr;
-    if (aff && kval) {
-#pragma unroll
-      for (int e = 0; e < EPC; ++e) { sc[e] = a.in_scale[ci + e]; sh[e] = a.in_shift[ci + e]; }
+    const int k0 = kt * BK;
+    int rs, ci, r, s;
+    if constexpr (UNIFORM_TAP) {
+      ci = u_ci; s = u_s; r = u_r;
+      rs = r * a.S + s;
+      u_ci += BK;
+      if (u_ci == a.C) {
+        u_ci = 0;
+        if (++u_s == a.S) { u_s = 0; ++u_r; }
+      }
+    } else {
+      const int kq = k0 + lc * EPC;  // first k of this thread's chunk
+      rs = kq / a.C;
+      ci = kq - rs * a.C;
+      r = rs / a.S;
+      s = rs - r * a.S;
     }
+    const bool kval = UNIFORM_TAP ? true : (k0 + lc * EPC < a.K);
+    const int tapoff = (r * (int)a.sH + s * (int)a.sW + ci) * ES + (UNIFORM_TAP ? lc * 16 : 0);
 #pragma unroll
     for (int i = 0; i < ARows; ++i) {
-      int ih = aih[i] + r, iw = aiw[i] + s;
-      bool ok = kval && avalid[i] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      if (ok) {
-        ra[i] = ld16<T>(X + abase[i] + ih * a.sH + iw * a.sW + ci);
-        if (aff) {
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) {
-            float v = to_f(ra[i].v[e]) * sc[e] + sh[e];
-            if (a.in_relu) v = fmaxf(v, 0.f);
-            ra[i].v[e] = from_f<T>(v);
-          }
-        }
-      } else {
-        ra[i] = zero16<T>();
-      }
+      const bool ok = kval && ((rmask[i] >> rs) & 1u);
+      ra[i] = bload(xr, ok ? (unsigned)(rowoff[i] + tapoff) : OOB_OFFSET);
     }
+    const bool bok = (k0 + lc * EPC) < a.K;
 #pragma unroll
-    for (int i = 0; i < BRows; ++i) {
-      int n = bn + lr + 32 * i;
-      if (kval && n < a.Cout) rb[i] = ld16<T>(Wt + (long long)n * a.K + k);
-      else rb[i] = zero16<T>();
+    for (int i = 0; i < BRows; ++i) rb[i] = bload(wr, bok ? (unsigned)(boff[i] + k0 * ES) : OOB_OFFSET);
+    if constexpr (AFFINE) {
+      const int cch = UNIFORM_TAP ? ci + lc * EPC : ci;
+      float sc[EPC], sh[EPC];
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        sc[e] = kval ? a.in_scale[cch + e] : 0.f;
+        sh[e] = kval ? a.in_shift[cch + e] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < ARows; ++i) {
+        const bool ok = kval && ((rmask[i] >> rs) & 1u);
+        const uint4 v = affine_chunk(ra[i], sc, sh, a.in_relu, T());
+        ra[i] = ok ? v : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto store_tiles = [&](int buf) {
     char* As = smem + buf * (A_BYTES + B_BYTES);
     char* Bs = As + A_BYTES;
 #pragma unroll
-    for (int i = 0; i < ARows; ++i)
-      *reinterpret_cast<uint4*>(As + (lc * (BM + 1) + lr + 32 * i) * 16) = *reinterpret_cast<uint4*>(&ra[i]);
+    for (int i = 0; i < ARows; ++i) *reinterpret_cast<uint4*>(As + (lc * (BM + 1) + lr + 32 * i) * 16) = ra[i];
 #pragma unroll
-    for (int i = 0; i < BRows; ++i)
-      *reinterpret_cast<uint4*>(Bs + (lc * (BN + 1) + lr + 32 * i) * 16) = *reinterpret_cast<uint4*>(&rb[i]);
+    for (int i = 0; i < BRows; ++i) *reinterpret_cast<uint4*>(Bs + (lc * (BN + 1) + lr + 32 * i) * 16) = rb[i];
   };
 
   f32x4 acc[MT][NT];
@@ -201,50 +279,102 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // epilogue
-  const int slot = (int)(bid % ARTSBIR_NSLOT);
+  // ---- epilogue 1: batch-norm statistics straight from the accumulators
+  if (a.stats) {
+    const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int gn = bn + wn * WTN + j * 16 + fr;
-    const bool nval = gn < a.Cout;
-    const float bval = (a.bias && nval) ? a.bias[gn] : 0.f;
-    float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < NT; ++j) {
+      const int gn = bn + wn * WTN + j * 16 + fr;
+      const float bval = (a.bias && gn < a.Cout) ? a.bias[gn] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const long long gm = bm + wm * WTM + i * 16 + fq * 4 + r;
-        if (nval && gm < a.M) {
-          float v = acc[i][j][r] + bval;
-          s1 += v;
-          s2 += v * v;
-          if (a.res_mode == 1) {
-            v += to_f(reinterpret_cast<const T*>(a.res)[gm * a.ldy + gn]);
-          } else if (a.res_mode == 2) {
-            const long long img = gm / HoWo;
-            const int rem = (int)(gm - img * HoWo);
-            const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-            const long long ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
-            v += 0.25f * to_f(reinterpret_cast<const T*>(a.res)[ri * a.ldy + gn]);
-          }
-          if (a.out_f32) {
-            float* yp = reinterpret_cast<float*>(a.y) + gm * a.ldy + gn;
-            if (a.accumulate) v += *yp;
-            *yp = v;
-          } else {
-            reinterpret_cast<T*>(a.y)[gm * a.ldy + gn] = from_f<T>(v);
-          }
+        for (int r = 0; r < 4; ++r) {
+          const long long gm = bm + wm * WTM + i * 16 + fq * 4 + r;
+          const float v = acc[i][j][r] + bval;
+          if (gm < a.M) { s1 += v; s2 += v * v; }
         }
-      }
-    }
-    if (a.stats) {
       s1 += __shfl_xor(s1, 16, 64);
       s1 += __shfl_xor(s1, 32, 64);
       s2 += __shfl_xor(s2, 16, 64);
       s2 += __shfl_xor(s2, 32, 64);
-      if (fq == 0 && nval) {
+      if (fq == 0 && gn < a.Cout) {
         atomicAdd(a.stats + (long long)slot * 2 * a.Cout + gn, s1);
         atomicAdd(a.stats + (long long)slot * 2 * a.Cout + a.Cout + gn, s2);
+      }
+    }
+  }
+  // ---- epilogue 2: stage the f32 tile row-major in LDS, then 16-B coalesced rows
+  float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        st[(wm * WTM + i * 16 + fq * 4 + r) * EPI_LD + wn * WTN + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-column chunks per row
+  for (int u = tid; u < BM * CPR; u += 256) {
+    const int row = u / CPR, cc = u - (u / CPR) * CPR;
+    const long long gm = bm + row;
+    const int gn = bn + cc * 8;
+    if (gm >= a.M || gn >= a.Cout) continue;
+    float v[8];
+    *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(st + row * EPI_LD + cc * 8);
+    *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(st + row * EPI_LD + cc * 8 + 4);
+    const int nv = a.Cout - gn < 8 ? a.Cout - gn : 8;
+    if (a.bias) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += e < nv ? a.bias[gn + e] : 0.f;
+    }
+    if (a.res_mode) {
+      long long ri;
+      float scale = 1.f;
+      if (a.res_mode == 1) {
+        ri = gm;
+      } else {
+        const long long img = gm / HoWo;
+        const int rem = (int)(gm - img * HoWo);
+        const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+        ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+        scale = 0.25f;
+      }
+      const T* rp = reinterpret_cast<const T*>(a.res) + ri * a.ldy + gn;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += e < nv ? scale * to_f(rp[e]) : 0.f;
+    }
+    if (a.out_f32) {
+      float* yp = reinterpret_cast<float*>(a.y) + gm * a.ldy + gn;
+      if (nv == 8 && (a.ldy % 4) == 0) {
+        if (a.accumulate) {
+          const float4 p0 = *reinterpret_cast<const float4*>(yp), p1 = *reinterpret_cast<const float4*>(yp + 4);
+          v[0] += p0.x; v[1] += p0.y; v[2] += p0.z; v[3] += p0.w;
+          v[4] += p1.x; v[5] += p1.y; v[6] += p1.z; v[7] += p1.w;
+        }
+        *reinterpret_cast<float4*>(yp) = make_float4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<float4*>(yp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        for (int e = 0; e < nv; ++e) yp[e] = a.accumulate ? yp[e] + v[e] : v[e];
+      }
+    } else {
+      T* yp = reinterpret_cast<T*>(a.y) + gm * a.ldy + gn;
+      if (nv == 8 && (a.ldy % 8) == 0) {
+        Vec16<T> o0;
+        if constexpr (EPC == 8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o0.v[e] = from_f<T>(v[e]);
+          st16<T>(yp, o0);
+        } else {
+          Vec16<T> o1;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { o0.v[e] = from_f<T>(v[e]); o1.v[e] = from_f<T>(v[e + 4]); }
+          st16<T>(yp, o0);
+          st16<T>(yp + 4, o1);
+        }
+      } else {
+        for (int e = 0; e < nv; ++e) yp[e] = from_f<T>(v[e]);
       }
     }
   }
@@ -256,12 +386,16 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
 // EPC x EPC block (EPC rows m, EPC consecutive co / ci) with 16-B coalesced
 // loads and transposes it in registers (v_perm_b32 for bf16) into EPC chunks
 // of the common LDS image.  The reduction over m is split across workgroups
-// and combined with f32 atomics into dW.
+// and combined with f32 atomics into dW.  The (r, s, ci) of every Xcol unit is
+// loop-invariant per thread (the K-loop runs over m), so its affine
+// coefficients and tap offsets are loaded/decoded once.
 // ---------------------------------------------------------------------------
 struct WgradArgs {
   const void* dy;
+  long long dy_elems;
   long long ldd;  // row stride of dY
   const void* x;
+  long long x_elems;
   long long sN, sH, sW;
   int H, W, C;
   int R, S, stride, pad;
@@ -277,31 +411,32 @@ struct WgradArgs {
   float* dw;               // [Cout][K] f32
 };
 
-__device__ __forceinline__ void transpose_unit(const Vec16<bf16> (&in)[8], Vec16<bf16> (&out)[8]) {
-  const uint32_t* d[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) d[e] = reinterpret_cast<const uint32_t*>(&in[e]);
+__device__ __forceinline__ void transpose_unit(const uint4 (&in)[8], uint4 (&out)[8], bf16) {
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    uint32_t* o0 = reinterpret_cast<uint32_t*>(&out[2 * p]);
-    uint32_t* o1 = reinterpret_cast<uint32_t*>(&out[2 * p + 1]);
+    uint32_t o0[4], o1[4];
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      o0[w] = __builtin_amdgcn_perm(d[2 * w + 1][p], d[2 * w][p], 0x05040100u);
-      o1[w] = __builtin_amdgcn_perm(d[2 * w + 1][p], d[2 * w][p], 0x07060302u);
+      const uint32_t a0 = reinterpret_cast<const uint32_t*>(&in[2 * w])[p];
+      const uint32_t a1 = reinterpret_cast<const uint32_t*>(&in[2 * w + 1])[p];
+      o0[w] = __builtin_amdgcn_perm(a1, a0, 0x05040100u);
+      o1[w] = __builtin_amdgcn_perm(a1, a0, 0x07060302u);
     }
+    out[2 * p] = make_uint4(o0[0], o0[1], o0[2], o0[3]);
+    out[2 * p + 1] = make_uint4(o1[0], o1[1], o1[2], o1[3]);
   }
 }
-__device__ __forceinline__ void transpose_unit(const Vec16<float> (&in)[4], Vec16<float> (&out)[4]) {
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) out[c].v[e] = in[e].v[c];
+__device__ __forceinline__ void transpose_unit(const uint4 (&in)[4], uint4 (&out)[4], float) {
+  out[0] = make_uint4(in[0].x, in[1].x, in[2].x, in[3].x);
+  out[1] = make_uint4(in[0].y, in[1].y, in[2].y, in[3].y);
+  out[2] = make_uint4(in[0].z, in[1].z, in[2].z, in[3].z);
+  out[3] = make_uint4(in[0].w, in[1].w, in[2].w, in[3].w);
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, bool AFFINE>
 __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
   constexpr int EPC = MM<T>::EPC;
+  constexpr int ES = sizeof(T);
   constexpr int BK = 8 * EPC;
   constexpr int A_BYTES = 8 * (BM + 1) * 16;
   constexpr int B_BYTES = 8 * (BN + 1) * 16;
@@ -309,89 +444,117 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
   constexpr int BU = 8 * (BN / EPC);
   constexpr int UT = (AU + BU + 255) / 256;
   static_assert(AU % 64 == 0, "A units must be wave aligned");
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int WN = BM >= 128 ? 2 : 4;  // waves along N (k')
+  constexpr int WM = 4 / WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int MT = WTM / 16, NT = WTN / 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WN, wn = wid % WN;
   const int ntn = (a.K + BN - 1) / BN;
   const int ntm = (a.Cout + BM - 1) / BM;
   const int tile = blockIdx.x % (ntm * ntn);
   const int split = blockIdx.x / (ntm * ntn);
-  const int bm = (tile / ntn) * BM;   // co
-  const int bn = (tile % ntn) * BN;   // k
+  const int bm = (tile / ntn) * BM;  // co
+  const int bn = (tile % ntn) * BN;  // k
   const long long m_begin = (long long)split * a.m_per_split;
   long long m_end = m_begin + a.m_per_split;
   if (m_end > a.M) m_end = a.M;
   if (m_begin >= m_end) return;
   const int nk = (int)((m_end - m_begin + BK - 1) / BK);
 
-  const T* __restrict__ DY = reinterpret_cast<const T*>(a.dy);
-  const T* __restrict__ X = reinterpret_cast<const T*>(a.x);
   const int HoWo = a.Ho * a.Wo;
+  const long long img0 = a.dense ? 0 : m_begin / HoWo;
+  const long long xbase = a.dense ? m_begin * a.ldx : img0 * a.sN;
+  const __amdgpu_buffer_rsrc_t dyr = make_rsrc(reinterpret_cast<const T*>(a.dy) + m_begin * a.ldd,
+                                               (a.dy_elems - m_begin * a.ldd) * ES);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc(reinterpret_cast<const T*>(a.x) + xbase, (a.x_elems - xbase) * ES);
 
-  // loader units: [0, AU) are dY^T units, [AU, AU+BU) are Xcol^T units
-  Vec16<T> tu[UT][EPC];
+  // per-unit loop invariants
+  int u_mc[UT], u_cc[UT];
+  bool u_isA[UT], u_act[UT];
+  int b_r[UT], b_s[UT], b_ci[UT];
+  bool b_kval[UT];
+  float b_sc[UT][AFFINE ? EPC : 1], b_sh[UT][AFFINE ? EPC : 1];
+#pragma unroll
+  for (int t = 0; t < UT; ++t) {
+    const int uu = tid + 256 * t;
+    u_act[t] = uu < AU + BU;
+    u_isA[t] = uu < AU;
+    const int u = u_isA[t] ? uu : uu - AU;
+    u_mc[t] = u & 7;
+    u_cc[t] = u >> 3;
+    const int k = bn + u_cc[t] * EPC;
+    b_kval[t] = !u_isA[t] && k < a.K;
+    const int rs = b_kval[t] ? k / a.C : 0;
+    b_ci[t] = b_kval[t] ? k - rs * a.C : 0;
+    b_r[t] = rs / a.S;
+    b_s[t] = rs - (rs / a.S) * a.S;
+    if constexpr (AFFINE) {
+#pragma unroll
+      for (int e = 0; e < EPC; ++e) {
+        b_sc[t][e] = b_kval[t] ? a.in_scale[b_ci[t] + e] : 0.f;
+        b_sh[t][e] = b_kval[t] ? a.in_shift[b_ci[t] + e] : 0.f;
+      }
+    }
+  }
+
+  uint4 tu[UT][EPC];
+  // 32-bit, block-relative pixel walk: m = m_begin + rel, pos = rem0 + rel is the
+  // pixel index counted from the start of image img0 (pos < 2^24 by construction)
+  const int mlen = (int)(m_end - m_begin);
+  const int rem0 = a.dense ? 0 : (int)(m_begin - img0 * HoWo);
+  const float inv_howo = 1.f / (float)HoWo, inv_wo = 1.f / (float)a.Wo;
+  const int sN = (int)a.sN, sH = (int)a.sH, sW = (int)a.sW, ldd = (int)a.ldd, ldx = (int)a.ldx;
 
   auto load_tiles = [&](int kt) {
-    const long long m0 = m_begin + (long long)kt * BK;
+    const int m0 = kt * BK;  // relative to m_begin
 #pragma unroll
     for (int t = 0; t < UT; ++t) {
-      const int uu = tid + 256 * t;
-      if (uu < AU) {
-        const int mc = uu & 7, cc = uu >> 3;
-        const int co = bm + cc * EPC;
+      if (!u_act[t]) continue;
+      const int mb = m0 + u_mc[t] * EPC;
+      if (u_isA[t]) {
+        const int co = bm + u_cc[t] * EPC;
+        const bool cval = co < a.Cout;
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
-          const long long m = m0 + mc * EPC + e;
-          if (m < m_end && co < a.Cout) tu[t][e] = ld16<T>(DY + m * a.ldd + co);
-          else tu[t][e] = zero16<T>();
+          const bool ok = cval && mb + e < mlen;
+          tu[t][e] = bload(dyr, ok ? (unsigned)(((mb + e) * ldd + co) * ES) : OOB_OFFSET);
         }
-      } else if (uu < AU + BU) {
-        const int u = uu - AU;
-        const int mc = u & 7, cc = u >> 3;
-        const int k = bn + cc * EPC;
-        const bool kval = k < a.K;
-        int rs = kval ? k / a.C : 0;
-        int ci = k - rs * a.C;
-        int r = rs / a.S, s = rs - (rs / a.S) * a.S;
-        float sc[EPC], sh[EPC];
-        const bool aff = a.in_scale != nullptr;
-        if (aff && kval) {
-#pragma unroll
-          for (int e = 0; e < EPC; ++e) { sc[e] = a.in_scale[ci + e]; sh[e] = a.in_shift[ci + e]; }
-        }
+      } else if (a.dense) {
 #pragma unroll
         for (int e = 0; e < EPC; ++e) {
-          const long long m = m0 + mc * EPC + e;
-          bool ok = kval && m < m_end;
-          long long off = 0;
-          if (ok) {
-            if (a.dense) {
-              off = m * a.ldx + k;
-            } else {
-              long long img = m / HoWo;
-              int rem = (int)(m - img * HoWo);
-              int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-              int ih = oh * a.stride - a.pad + r, iw = ow * a.stride - a.pad + s;
-              ok = ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-              off = img * a.sN + ih * a.sH + iw * a.sW + ci;
-            }
+          const bool ok = b_kval[t] && mb + e < mlen;
+          tu[t][e] = bload(xr, ok ? (unsigned)(((mb + e) * ldx + bn + u_cc[t] * EPC) * ES) : OOB_OFFSET);
+        }
+      } else {
+        // decode the first m of the unit, then walk along the output row
+        const int pos = rem0 + mb;
+        int q = (int)((float)pos * inv_howo);
+        int p = pos - q * HoWo;
+        if (p < 0) { --q; p += HoWo; } else if (p >= HoWo) { ++q; p -= HoWo; }
+        int oh = (int)((float)p * inv_wo);
+        int ow = p - oh * a.Wo;
+        if (ow < 0) { --oh; ow += a.Wo; } else if (ow >= a.Wo) { ++oh; ow -= a.Wo; }
+        int ih = oh * a.stride - a.pad + b_r[t], iw = ow * a.stride - a.pad + b_s[t];
+        int base = q * sN + b_ci[t];
+#pragma unroll
+        for (int e = 0; e < EPC; ++e) {
+          const bool ok = b_kval[t] && mb + e < mlen && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+          tu[t][e] = bload(xr, ok ? (unsigned)((base + ih * sH + iw * sW) * ES) : OOB_OFFSET);
+          if constexpr (AFFINE) {
+            const uint4 v = affine_chunk(tu[t][e], b_sc[t], b_sh[t], a.in_relu, T());
+            tu[t][e] = ok ? v : make_uint4(0, 0, 0, 0);
           }
-          if (ok) {
-            tu[t][e] = ld16<T>(X + off);
-            if (aff) {
-#pragma unroll
-              for (int q = 0; q < EPC; ++q) {
-                float v = to_f(tu[t][e].v[q]) * sc[q] + sh[q];
-                if (a.in_relu) v = fmaxf(v, 0.f);
-                tu[t][e].v[q] = from_f<T>(v);
-              }
-            }
-          } else {
-            tu[t][e] = zero16<T>();
+          ++ow;
+          iw += a.stride;
+          if (ow == a.Wo) {
+            ow = 0;
+            iw = b_s[t] - a.pad;
+            ih += a.stride;
+            if (++oh == a.Ho) { oh = 0; ih = b_r[t] - a.pad; base += sN; }
           }
         }
       }
@@ -402,17 +565,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
     char* Bs = As + A_BYTES;
 #pragma unroll
     for (int t = 0; t < UT; ++t) {
-      const int uu = tid + 256 * t;
-      if (uu < AU + BU) {
-        const bool isA = uu < AU;
-        const int u = isA ? uu : uu - AU;
-        const int mc = u & 7, cc = u >> 3;
-        char* base = isA ? As + (mc * (BM + 1) + cc * EPC) * 16 : Bs + (mc * (BN + 1) + cc * EPC) * 16;
-        Vec16<T> o[EPC];
-        transpose_unit(tu[t], o);
+      if (!u_act[t]) continue;
+      char* base = u_isA[t] ? As + (u_mc[t] * (BM + 1) + u_cc[t] * EPC) * 16
+                            : Bs + (u_mc[t] * (BN + 1) + u_cc[t] * EPC) * 16;
+      uint4 o[EPC];
+      transpose_unit(tu[t], o, T());
 #pragma unroll
-        for (int c = 0; c < EPC; ++c) *reinterpret_cast<uint4*>(base + c * 16) = *reinterpret_cast<uint4*>(&o[c]);
-      }
+      for (int c = 0; c < EPC; ++c) *reinterpret_cast<uint4*>(base + c * 16) = o[c];
     }
   };
 
@@ -476,6 +635,7 @@ static int check_conv(const artsbir_conv_desc* d) {
   if (d->C % 8 != 0) { set_error("conv: C=%d must be a multiple of 8", d->C); return -1; }
   if (d->Cout <= 0 || d->N <= 0) { set_error("conv: empty shape"); return -1; }
   if (d->R <= 0 || d->S <= 0 || d->stride <= 0 || d->pad < 0) { set_error("conv: bad geometry"); return -1; }
+  if (d->R * d->S > 32) { set_error("conv: at most 32 filter taps"); return -1; }
   return 0;
 }
 
@@ -484,16 +644,23 @@ static void fill_geom(const artsbir_conv_desc* d, int& Ho, int& Wo) {
   Wo = (d->W + 2 * d->pad - d->S) / d->stride + 1;
 }
 
+template <typename T, int BM, int BN>
+static void launch_conv_tile(const ConvArgs& a, hipStream_t st) {
+  constexpr int BK = 8 * MM<T>::EPC;
+  const long long tiles = ((a.M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
+  const bool uni = (a.C % BK) == 0;
+  const bool aff = a.in_scale != nullptr;
+  if (uni && aff) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, true, true>), dim3((unsigned)tiles), dim3(256), 0, st, a);
+  else if (uni) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, true, false>), dim3((unsigned)tiles), dim3(256), 0, st, a);
+  else if (aff) hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false, true>), dim3((unsigned)tiles), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, false, false>), dim3((unsigned)tiles), dim3(256), 0, st, a);
+}
+
 template <typename T>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
-  const bool narrow = a.Cout <= 64;
-  if (narrow) {
-    long long tiles = ((a.M + 127) / 128) * ((a.Cout + 63) / 64);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, 128, 64>), dim3((unsigned)tiles), dim3(256), 0, st, a);
-  } else {
-    long long tiles = ((a.M + 127) / 128) * ((a.Cout + 127) / 128);
-    hipLaunchKernelGGL((conv_gemm_kernel<T, 128, 128>), dim3((unsigned)tiles), dim3(256), 0, st, a);
-  }
+  if ((long long)a.Cout * a.K * sizeof(T) > 0x7fffffffLL) { set_error("conv: weight tensor too large"); return -1; }
+  if (a.Cout <= 64) launch_conv_tile<T, 128, 64>(a, st);
+  else launch_conv_tile<T, 128, 128>(a, st);
   ARTSBIR_CHECK_LAUNCH("conv_gemm");
   return 0;
 }
@@ -511,6 +678,7 @@ extern "C" int artsbir_conv2d_fwd(const artsbir_conv_desc* d, const void* x, con
   a.sW = d->C;
   a.sH = (long long)d->W * d->C;
   a.sN = (long long)d->H * d->W * d->C;
+  a.x_elems = (long long)d->N * a.sN;
   a.H = d->H; a.W = d->W; a.C = d->C;
   a.R = d->R; a.S = d->S; a.stride = d->stride; a.pad = d->pad;
   a.Ho = Ho; a.Wo = Wo;
@@ -528,6 +696,7 @@ extern "C" int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, 
                                     const void* res, int res_mode, void* stream) {
   // data gradient of a stride-1 convolution: a convolution of dy [N][H][W][Cout]
   // with the flipped, transposed weights wd [Cin][R][S][Cout] and padding R-1-pad.
+  if (check_conv(d)) return -1;
   if (d->stride != 1) { set_error("conv2d_dgrad: only stride 1 (got %d)", d->stride); return -1; }
   if (d->Cout % 8 || d->C % 8) { set_error("conv2d_dgrad: channels must be multiples of 8"); return -1; }
   if (res_mode < 0 || res_mode > 2 || (res_mode && !res)) { set_error("conv2d_dgrad: bad residual"); return -1; }
@@ -536,6 +705,7 @@ extern "C" int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, 
   const int pad = d->R - 1 - d->pad;
   a.x = dy;
   a.sW = d->Cout; a.sH = (long long)d->W * d->Cout; a.sN = (long long)d->H * d->W * d->Cout;
+  a.x_elems = (long long)d->N * a.sN;
   a.H = d->H; a.W = d->W; a.C = d->Cout;
   a.R = d->R; a.S = d->S; a.stride = 1; a.pad = pad;
   a.Ho = d->H + 2 * pad - d->R + 1; a.Wo = d->W + 2 * pad - d->S + 1;
@@ -556,11 +726,13 @@ extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void*
   if (K % 8 != 0 || lda % 8 != 0) { set_error("gemm_nt: K=%d and lda=%lld must be multiples of 8", K, lda); return -1; }
   if (accumulate && !out_f32) { set_error("gemm_nt: accumulate requires f32 output"); return -1; }
   if (M <= 0 || N <= 0) return 0;
-  ConvArgs p;
-  p.x = a; p.sN = 0; p.sH = lda; p.sW = 0;
-  p.H = (int)M; p.W = 1; p.C = K;
   if (M > 0x7fffffffLL) { set_error("gemm_nt: M too large"); return -1; }
-  p.R = 1; p.S = 1; p.stride = 1; p.pad = 0; p.Ho = (int)M; p.Wo = 1;
+  // dense rows as "images" of one pixel: row offsets stay relative to the tile
+  ConvArgs p;
+  p.x = a; p.sN = lda; p.sH = 0; p.sW = 0;
+  p.x_elems = (M - 1) * lda + K;
+  p.H = 1; p.W = 1; p.C = K;
+  p.R = 1; p.S = 1; p.stride = 1; p.pad = 0; p.Ho = 1; p.Wo = 1;
   p.in_scale = nullptr; p.in_shift = nullptr; p.in_relu = 0;
   p.w = b; p.Cout = N; p.K = K; p.M = M;
   p.y = c; p.ldy = ldc > 0 ? ldc : N;
@@ -570,21 +742,41 @@ extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void*
   return dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
 }
 
-template <typename T>
-static int launch_wgrad(WgradArgs& a, hipStream_t st) {
-  constexpr int BM = 128, BN = 128;
+template <typename T, int BM, int BN>
+static void launch_wgrad_tile(WgradArgs& a, hipStream_t st) {
   constexpr int BK = 8 * MM<T>::EPC;
   const int tiles = ((a.Cout + BM - 1) / BM) * ((a.K + BN - 1) / BN);
-  // enough workgroups to fill 256 CUs ~4 deep, but >= 8 K-steps per workgroup
+  // ~4 workgroups per CU in total, but >= 8 K-steps per workgroup
   long long ksteps = (a.M + BK - 1) / BK;
   long long splits = (1024 + tiles - 1) / tiles;
   long long max_splits = (ksteps + 7) / 8;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   long long per = (ksteps + splits - 1) / splits;
+  // keep every block-relative byte offset and pixel index in 31 / 24 bits
+  const long long ld = a.dense ? (a.ldx > a.ldd ? a.ldx : a.ldd) : a.ldd;
+  long long cap = (1LL << 22) / BK;
+  const long long cap2 = ((1LL << 30) / ((ld + 1) * (long long)sizeof(T))) / BK;
+  if (cap2 < cap) cap = cap2;
+  if (!a.dense) {  // images spanned by one block's pixel range
+    const long long imgs = (1LL << 30) / (a.sN * (long long)sizeof(T)) - 2;
+    const long long cap3 = imgs > 0 ? imgs * a.Ho * a.Wo / BK : 1;
+    if (cap3 < cap) cap = cap3;
+  }
+  if (cap < 1) cap = 1;
+  if (per > cap) per = cap;
   a.m_per_split = per * BK;
   splits = (ksteps + per - 1) / per;
-  hipLaunchKernelGGL((wgrad_kernel<T, BM, BN>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, a);
+  if (a.in_scale)
+    hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, true>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, false>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, a);
+}
+
+template <typename T>
+static int launch_wgrad(WgradArgs& a, hipStream_t st) {
+  if (a.Cout <= 64) launch_wgrad_tile<T, 64, 128>(a, st);
+  else launch_wgrad_tile<T, 128, 128>(a, st);
   ARTSBIR_CHECK_LAUNCH("wgrad");
   return 0;
 }
@@ -598,16 +790,18 @@ extern "C" int artsbir_conv2d_wgrad(const artsbir_conv_desc* d, const void* dy, 
   fill_geom(d, Ho, Wo);
   WgradArgs a;
   a.dy = dy; a.ldd = d->Cout;
+  a.M = (long long)d->N * Ho * Wo;
+  a.dy_elems = a.M * d->Cout;
   a.x = x;
   a.sW = d->C; a.sH = (long long)d->W * d->C; a.sN = (long long)d->H * d->W * d->C;
+  a.x_elems = (long long)d->N * a.sN;
   a.H = d->H; a.W = d->W; a.C = d->C;
   a.R = d->R; a.S = d->S; a.stride = d->stride; a.pad = d->pad;
   a.Ho = Ho; a.Wo = Wo;
-  a.dense = (d->R == 1 && d->S == 1 && d->stride == 1 && d->pad == 0) ? 1 : 0;
+  a.dense = (d->R == 1 && d->S == 1 && d->stride == 1 && d->pad == 0 && !in_scale) ? 1 : 0;
   a.ldx = d->C;
   a.in_scale = in_scale; a.in_shift = in_shift; a.in_relu = in_relu;
   a.Cout = d->Cout; a.K = d->R * d->S * d->C;
-  a.M = (long long)d->N * Ho * Wo;
   a.dw = dw;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_wgrad<bf16>(a, st) : launch_wgrad<float>(a, st);
@@ -622,7 +816,8 @@ extern "C" int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void*
   }
   if (M <= 0) return 0;
   WgradArgs a;
-  a.dy = dy; a.ldd = ldd; a.x = x;
+  a.dy = dy; a.ldd = ldd; a.dy_elems = (M - 1) * ldd + N;
+  a.x = x; a.x_elems = (M - 1) * ldx + K;
   a.sN = 0; a.sH = 0; a.sW = 0; a.H = 1; a.W = 1; a.C = K;
   a.R = 1; a.S = 1; a.stride = 1; a.pad = 0; a.Ho = 1; a.Wo = 1;
   a.dense = 1; a.ldx = ldx;

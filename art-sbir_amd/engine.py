@@ -232,11 +232,13 @@ class Engine:
         call("artsbir_pack_input", self.dt, ptr(x), B, cin, R, R2, ptr(x0), _s())
         (fw1, _), (fw2, _), (fw3, _) = pk["stem"]
         y1, b1 = self._conv_bn(Act(x0), m.conv1, m.bn1, fw1, 2, 1, train, stats)
-        y2, b2 = self._conv_bn(Act(y1, b1, 1), m.conv2, m.bn2, fw2, 1, 1, train, stats)
-        y3, b3 = self._conv_bn(Act(y2, b2, 1), m.conv3, m.bn3, fw3, 1, 1, train, stats)
+        a1 = self._act_pool(y1, b1, 1, 0)
+        y2, b2 = self._conv_bn(Act(a1), m.conv2, m.bn2, fw2, 1, 1, train, stats)
+        a2 = self._act_pool(y2, b2, 1, 0)
+        y3, b3 = self._conv_bn(Act(a2), m.conv3, m.bn3, fw3, 1, 1, train, stats)
         h = self._act_pool(y3, b3, 1, 2)
         if save:
-            ctx["stem"] = dict(x0=x0, y1=y1, y2=y2, y3=y3, b1=b1, b2=b2, b3=b3)
+            ctx["stem"] = dict(x0=x0, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, b1=b1, b2=b2, b3=b3)
 
         # residual stages (models.py:354-357)
         bctx = []
@@ -254,14 +256,13 @@ class Engine:
     def _block_fwd(self, blk, bp, h, train, stats):
         B, H, W, Cin = h.shape
         s = blk.stride
+        # BN+ReLU outputs are materialised once (bf16): cheaper than re-applying
+        # them in every GEMM tile that reads them (9 taps x N-tiles for 3x3)
         y1, b1 = self._conv_bn(Act(h), blk.conv1, blk.bn1, bp["conv1"][0], 1, 0, train, stats)
-        y2, b2 = self._conv_bn(Act(y1, b1, 1), blk.conv2, blk.bn2, bp["conv2"][0], 1, 1, train, stats)
-        if s > 1:
-            p2 = self._act_pool(y2, b2, 1, s)
-            c3in = Act(p2)
-        else:
-            p2 = None
-            c3in = Act(y2, b2, 1)
+        a1 = self._act_pool(y1, b1, 1, 0)
+        y2, b2 = self._conv_bn(Act(a1), blk.conv2, blk.bn2, bp["conv2"][0], 1, 1, train, stats)
+        p2 = self._act_pool(y2, b2, 1, s if s > 1 else 0)
+        c3in = Act(p2)
         y3, b3 = self._conv_bn(c3in, blk.conv3, blk.bn3, bp["conv3"][0], 1, 0, train, stats)
         yd = bd = pd = None
         if blk.downsample is not None:
@@ -276,7 +277,7 @@ class Engine:
         call("artsbir_block_out", self.dt, ptr(y3), ptr(b3.scale), ptr(b3.shift),
              ptr(yd), ptr(bd.scale) if bd else None, ptr(bd.shift) if bd else None,
              None if yd is not None else ptr(h), rows, out.shape[-1], ptr(out), _s())
-        ctx = dict(h=h, y1=y1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, b1=b1, b2=b2, b3=b3, bd=bd)
+        ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, b1=b1, b2=b2, b3=b3, bd=bd)
         return out, ctx
 
     def _attnpool_fwd(self, ap, pk, h):
@@ -435,11 +436,11 @@ class Engine:
         gid = None if has_ds else torch.empty_like(dout)
         dys = self._bn_bwd(0, dout, targets, bnmods, ws, grads, mask=out, gout=gid)
         dy3 = dys[0]
-        c3in = Act(p2) if s > 1 else Act(y2, b2, 1)
+        c3in = Act(p2)
         self._wgrad(dy3, c3in, blk.conv3, 1, 0, grads)
         dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3in.shape[:3] + (blk.conv3.weight.shape[1],))
         dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
-        self._wgrad(dy2, Act(y1, b1, 1), blk.conv2, 1, 1, grads)
+        self._wgrad(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
         da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
         dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
         self._wgrad(dy1, Act(h), blk.conv1, 1, 0, grads)
@@ -456,10 +457,10 @@ class Engine:
         x0, y1, y2, y3, b1, b2, b3 = (c[k] for k in ("x0", "y1", "y2", "y3", "b1", "b2", "b3"))
         (_, _), (_, dw2), (_, dw3) = pk["stem"]
         dy3, = self._bn_bwd(1, dh, [(y3, b3)], [m.bn3], ws, grads, mask_bn=b3, pool=2)
-        self._wgrad(dy3, Act(y2, b2, 1), m.conv3, 1, 1, grads)
+        self._wgrad(dy3, Act(c["a2"]), m.conv3, 1, 1, grads)
         da2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape)
         dy2, = self._bn_bwd(1, da2, [(y2, b2)], [m.bn2], ws, grads, mask_bn=b2)
-        self._wgrad(dy2, Act(y1, b1, 1), m.conv2, 1, 1, grads)
+        self._wgrad(dy2, Act(c["a1"]), m.conv2, 1, 1, grads)
         da1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape)
         dy1, = self._bn_bwd(1, da1, [(y1, b1)], [m.bn1], ws, grads, mask_bn=b1)
         self._wgrad(dy1, Act(x0), m.conv1, 2, 1, grads)
