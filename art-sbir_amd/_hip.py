@@ -75,8 +75,29 @@ SIGNATURES = {
     "artsbir_adam_table_blocks": [_vp, _c_int, _c_ll],
     "artsbir_adam_fill_table": [_vp, _c_int, _c_ll, _vp],
     "artsbir_adam_step": [_vp, _vp, _c_ll, _c_ll, _c_float, _c_float, _c_float, _c_float, _c_float, _c_ll, _vp],
+    "artsbir_pairwise_l2": [_vp, _c_ll, _vp, _c_ll, _c_int, _c_float, _vp, _vp],
+    "artsbir_rows_prep": [_c_int, _vp, _c_int, _c_int, _vp, _vp, _c_int, _vp],
+    "artsbir_knn_band": [_vp, _vp, _vp, _c_ll, _c_ll, _vp, _c_float, _c_int, _c_int, _c_float, _vp, _vp, _vp, _vp],
+    "artsbir_knn_band_from_dpos": [_vp, _vp, _c_float, _c_int, _c_float, _vp, _vp, _vp],
+    "artsbir_knn_candidates_per_query": [_c_int, _c_int],
+    "artsbir_knn_scan": [_c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int,
+                         _vp, _vp, _vp],
+    "artsbir_knn_merge": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_float, _c_float, _c_ll, _c_int, _vp,
+                          _vp, _vp, _vp],
+    "artsbir_knn_uncertain": [_vp, _vp, _c_int, _vp, _c_int, _vp, _vp, _c_ll, _vp, _vp],
+    "artsbir_knn_exact_all": [_vp, _vp, _c_int, _c_int, _vp, _vp],
+    "artsbir_pairwise_l2_bwd": [_vp, _c_ll, _vp, _c_ll, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_linear_fwd": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_linear_bwd": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "artsbir_cross_entropy_fwd": [_vp, _vp, _c_int, _c_int, _c_ll, _vp, _vp, _vp],
+    "artsbir_cross_entropy_bwd": [_vp, _vp, _c_int, _c_int, _c_ll, _vp, _vp, _vp, _vp],
+    "artsbir_cosine_fwd": [_vp, _c_ll, _vp, _c_ll, _c_int, _c_float, _vp, _vp, _vp],
+    "artsbir_cosine_bwd": [_vp, _c_ll, _vp, _c_ll, _c_int, _vp, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_hinge_fwd": [_vp, _vp, _c_int, _c_float, _vp, _vp],
+    "artsbir_hinge_bwd": [_vp, _vp, _c_int, _c_float, _vp, _vp, _vp, _vp],
 }
-_RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll}
+_RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll,
+             "artsbir_knn_candidates_per_query": _c_int}
 
 _lib = None
 

@@ -185,43 +185,57 @@ struct BnBwdArgs {
   int B, H, W, C;            // geometry of y (full resolution)
 };
 
-template <typename T>
-__device__ __forceinline__ void bnb_g(const BnBwdArgs& a, long long b, int h, int w, int cg, long long off, float (&g)[8]) {
-  if (a.kind == 0) {
-    float m[8];
-    load8<T>(reinterpret_cast<const T*>(a.d) + off, g);
-    load8<T>(reinterpret_cast<const T*>(a.mask) + off, m);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = m[e] > 0.f ? g[e] : 0.f;
+// A "unit" is one pixel, or one 2x2 (pool x pool) quad when the forward pooled
+// after the ReLU: the quad's pooled gradient d is read once and spread over its
+// four pixels.  Each thread owns one 8-channel group for the whole kernel, so
+// per-channel parameters are loaded once; no per-element index division.
+template <typename T, int KIND, int POOL>
+__device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, long long (&offs)[POOL * POOL],
+                                          float (&g)[POOL * POOL][8], const float (&ms)[8], const float (&mh)[8]) {
+  if constexpr (POOL == 1) {
+    offs[0] = (long long)u * a.C + cg * 8;
   } else {
-    if (a.pool > 1) {
-      const int Hp = a.H / a.pool, Wp = a.W / a.pool;
-      load8<T>(reinterpret_cast<const T*>(a.d) + (((b * Hp + h / a.pool) * Wp + w / a.pool) * a.C + cg * 8), g);
-      const float inv = 1.f / (a.pool * a.pool);
+    const int Wp = a.W / POOL, Hp = a.H / POOL;
+    const int wp = u % Wp;
+    const int t = u / Wp;
+    const int hp = t % Hp;
+    const int b = t / Hp;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[e] *= inv;
-    } else {
-      load8<T>(reinterpret_cast<const T*>(a.d) + off, g);
+    for (int dy = 0; dy < POOL; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < POOL; ++dx)
+        offs[dy * POOL + dx] = ((long long)(b * a.H + hp * POOL + dy) * a.W + wp * POOL + dx) * a.C + cg * 8;
+  }
+  if constexpr (KIND == 0) {
+    float m[8];
+    load8<T>(reinterpret_cast<const T*>(a.d) + offs[0], g[0]);
+    load8<T>(reinterpret_cast<const T*>(a.mask) + offs[0], m);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[0][e] = m[e] > 0.f ? g[0][e] : 0.f;
+  } else {
+    float dv[8];
+    load8<T>(reinterpret_cast<const T*>(a.d) + (long long)u * a.C + cg * 8, dv);
+    constexpr float inv = 1.f / (POOL * POOL);
+#pragma unroll
+    for (int q = 0; q < POOL * POOL; ++q) {
+      float y[8];
+      load8<T>(reinterpret_cast<const T*>(a.y[0]) + offs[q], y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) g[q][e] = (y[e] * ms[e] + mh[e]) > 0.f ? dv[e] * inv : 0.f;
     }
-    float y[8], s[8], sh[8];
-    load8<T>(reinterpret_cast<const T*>(a.y[0]) + off, y);
-    loadf8(a.msc + cg * 8, s);
-    loadf8(a.msh + cg * 8, sh);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = (y[e] * s[e] + sh[e]) > 0.f ? g[e] : 0.f;
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, long long rows_per_block) {
+template <typename T, int KIND, int POOL>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int units_per_block) {
+  constexpr int NQ = POOL * POOL;
   const int CG = a.C / 8;
-  const int RL = 256 / CG;  // row lanes
+  const int RL = 256 / CG;  // unit lanes
   const int tid = threadIdx.x;
   const int cg = tid % CG, rl = tid / CG;
-  const long long rows = (long long)a.B * a.H * a.W;
-  const long long r0 = blockIdx.x * rows_per_block;
-  long long r1 = r0 + rows_per_block;
-  if (r1 > rows) r1 = rows;
+  const int units = a.B * (a.H / POOL) * (a.W / POOL);
+  const int u0 = blockIdx.x * units_per_block;
+  const int u1 = min(u0 + units_per_block, units);
   float acc[2][2][8];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -229,29 +243,31 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, long lo
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[t][q][e] = 0.f;
-  float mn[2][8], is[2][8];
   if (rl < RL) {
+    float mn[2][8], is[2][8], ms[8], mh[8];
     for (int t = 0; t < a.ntarget; ++t) { loadf8(a.mean[t] + cg * 8, mn[t]); loadf8(a.istd[t] + cg * 8, is[t]); }
-    for (long long r = r0 + rl; r < r1; r += RL) {
-      int w = (int)(r % a.W);
-      long long q = r / a.W;
-      int h = (int)(q % a.H);
-      long long b = q / a.H;
-      const long long off = r * a.C + cg * 8;
-      float g[8];
-      bnb_g<T>(a, b, h, w, cg, off, g);
-      for (int t = 0; t < a.ntarget; ++t) {
-        float y[8];
-        load8<T>(reinterpret_cast<const T*>(a.y[t]) + off, y);
+    if constexpr (KIND == 1) { loadf8(a.msc + cg * 8, ms); loadf8(a.msh + cg * 8, mh); }
+    for (int u = u0 + rl; u < u1; u += RL) {
+      long long offs[NQ];
+      float g[NQ][8];
+      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, ms, mh);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          acc[t][0][e] += g[e];
-          acc[t][1][e] += g[e] * (y[e] - mn[t][e]) * is[t][e];
+      for (int t = 0; t < 2; ++t) {
+        if (t >= a.ntarget) break;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          float y[8];
+          load8<T>(reinterpret_cast<const T*>(a.y[t]) + offs[q], y);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            acc[t][0][e] += g[q][e];
+            acc[t][1][e] += g[q][e] * ((y[e] - mn[t][e]) * is[t][e]);
+          }
         }
       }
     }
   }
-  // reduce over row lanes in LDS, then one atomic per channel per block
+  // reduce over unit lanes in LDS, then one atomic per channel per block
   __shared__ float red[256 * 8];
   const int slot = blockIdx.x % ARTSBIR_NSLOT;
   for (int t = 0; t < a.ntarget; ++t)
@@ -260,42 +276,62 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, long lo
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[tid * 8 + e] = (rl < RL) ? acc[t][q][e] : 0.f;
       __syncthreads();
-      if (tid < CG) {
-        for (int e = 0; e < 8; ++e) {
-          float s = 0.f;
-          for (int l = 0; l < RL; ++l) s += red[(l * CG + tid) * 8 + e];
-          atomicAdd(a.slots[t] + (long long)slot * 2 * a.C + q * a.C + tid * 8 + e, s);
+      if (tid < a.C) {  // one channel per thread
+        const int c = tid, cgi = c / 8, e = c % 8;
+        float sum = 0.f;
+        for (int l = 0; l < RL; ++l) sum += red[(l * CG + cgi) * 8 + e];
+        atomicAdd(a.slots[t] + (long long)slot * 2 * a.C + q * a.C + c, sum);
+      }
+      if (a.C > 256) {  // C up to 2048: remaining channels
+        for (int c = tid + 256; c < a.C; c += 256) {
+          const int cgi = c / 8, e = c % 8;
+          float sum = 0.f;
+          for (int l = 0; l < RL; ++l) sum += red[(l * CG + cgi) * 8 + e];
+          atomicAdd(a.slots[t] + (long long)slot * 2 * a.C + q * a.C + c, sum);
         }
       }
     }
 }
 
-template <typename T>
-__global__ void bn_bwd_apply_kernel(BnBwdArgs a) {
+template <typename T, int KIND, int POOL>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int units_per_block) {
+  constexpr int NQ = POOL * POOL;
   const int CG = a.C / 8;
-  const long long n = (long long)a.B * a.H * a.W * CG;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    const int cg = (int)(i % CG);
-    const long long r = i / CG;
-    int w = (int)(r % a.W);
-    long long q = r / a.W;
-    int h = (int)(q % a.H);
-    long long b = q / a.H;
-    const long long off = r * a.C + cg * 8;
-    float g[8];
-    bnb_g<T>(a, b, h, w, cg, off, g);
-    if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + off, g);
-    for (int t = 0; t < a.ntarget; ++t) {
-      float y[8], mn[8], is[8], c1[8], c2[8], c3[8], o[8];
-      load8<T>(reinterpret_cast<const T*>(a.y[t]) + off, y);
-      loadf8(a.mean[t] + cg * 8, mn);
-      loadf8(a.istd[t] + cg * 8, is);
-      loadf8(a.coef[t] + cg * 8, c1);
-      loadf8(a.coef[t] + a.C + cg * 8, c2);
-      loadf8(a.coef[t] + 2 * a.C + cg * 8, c3);
+  const int RL = 256 / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, rl = tid / CG;
+  if (rl >= RL) return;
+  const int units = a.B * (a.H / POOL) * (a.W / POOL);
+  const int u0 = blockIdx.x * units_per_block;
+  const int u1 = min(u0 + units_per_block, units);
+  float mn[2][8], is[2][8], c1[2][8], c2[2][8], c3[2][8], ms[8], mh[8];
+  for (int t = 0; t < a.ntarget; ++t) {
+    loadf8(a.mean[t] + cg * 8, mn[t]);
+    loadf8(a.istd[t] + cg * 8, is[t]);
+    loadf8(a.coef[t] + cg * 8, c1[t]);
+    loadf8(a.coef[t] + a.C + cg * 8, c2[t]);
+    loadf8(a.coef[t] + 2 * a.C + cg * 8, c3[t]);
+  }
+  if constexpr (KIND == 1) { loadf8(a.msc + cg * 8, ms); loadf8(a.msh + cg * 8, mh); }
+  for (int u = u0 + rl; u < u1; u += RL) {
+    long long offs[NQ];
+    float g[NQ][8];
+    bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, ms, mh);
+    if (a.gout) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = c1[e] * (g[e] - c2[e] - (y[e] - mn[e]) * is[e] * c3[e]);
-      store8<T>(reinterpret_cast<T*>(a.dy[t]) + off, o);
+      for (int q = 0; q < NQ; ++q) store8<T>(reinterpret_cast<T*>(a.gout) + offs[q], g[q]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t >= a.ntarget) break;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float y[8], o[8];
+        load8<T>(reinterpret_cast<const T*>(a.y[t]) + offs[q], y);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = c1[t][e] * (g[q][e] - c2[t][e] - (y[e] - mn[t][e]) * is[t][e] * c3[t][e]);
+        store8<T>(reinterpret_cast<T*>(a.dy[t]) + offs[q], o);
+      }
     }
   }
 }
@@ -505,6 +541,10 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
     return -1;
   }
   if (d->ntarget < 1 || d->ntarget > 2) { set_error("bn_bwd: ntarget must be 1 or 2"); return -1; }
+  if (d->kind == 1 && d->pool > 2) { set_error("bn_bwd: pool must be <= 2"); return -1; }
+  if (d->kind == 1 && d->pool == 2 && (d->H % 2 || d->W % 2)) { set_error("bn_bwd: odd H/W with pool"); return -1; }
+  if (d->kind == 0 && d->pool > 1) { set_error("bn_bwd: pool only with kind 1"); return -1; }
+  if ((long long)d->B * d->H * d->W >= (1LL << 31)) { set_error("bn_bwd: too many pixels"); return -1; }
   a.kind = d->kind; a.pool = d->pool; a.d = d->d; a.mask = d->mask; a.msc = d->mask_scale; a.msh = d->mask_shift;
   a.ntarget = d->ntarget;
   for (int t = 0; t < 2; ++t) {
@@ -516,14 +556,30 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
   return 0;
 }
 
+template <typename T>
+static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
+  const int P = (a.kind == 1 && a.pool > 1) ? a.pool : 1;
+  const int units = a.B * (a.H / P) * (a.W / P);
+  const int RL = 256 / (a.C / 8);
+  // ~2048 workgroups, each walking a contiguous range of units
+  int upb = (units + 2047) / 2048;
+  if (upb < RL) upb = RL;
+  const unsigned grid = (unsigned)((units + upb - 1) / upb);
+#define BNB_LAUNCH(K, PP)                                                                                     \
+  do {                                                                                                       \
+    if (reduce) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K, PP>), dim3(grid), dim3(256), 0, st, a, upb);  \
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP>), dim3(grid), dim3(256), 0, st, a, upb);          \
+  } while (0)
+  if (a.kind == 0) BNB_LAUNCH(0, 1);
+  else if (P == 2) BNB_LAUNCH(1, 2);
+  else BNB_LAUNCH(1, 1);
+#undef BNB_LAUNCH
+}
+
 extern "C" int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream) {
   BnBwdArgs a;
   if (fill_bnb(a, d)) return -1;
-  const long long rows = (long long)d->B * d->H * d->W;
-  long long rpb = (rows + 2047) / 2048;
-  if (rpb < 32) rpb = 32;
-  const unsigned grid = (unsigned)((rows + rpb - 1) / rpb);
-  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_reduce_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a, rpb));
+  DISPATCH_T(d->dtype, launch_bnb<T>(a, true, (hipStream_t)stream));
   ARTSBIR_CHECK_LAUNCH("bn_bwd_reduce");
   return 0;
 }
@@ -531,8 +587,7 @@ extern "C" int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream)
 extern "C" int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream) {
   BnBwdArgs a;
   if (fill_bnb(a, d)) return -1;
-  const long long n = (long long)d->B * d->H * d->W * (d->C / 8);
-  DISPATCH_T(d->dtype, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, a));
+  DISPATCH_T(d->dtype, launch_bnb<T>(a, false, (hipStream_t)stream));
   ARTSBIR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }

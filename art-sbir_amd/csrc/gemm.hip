@@ -202,6 +202,15 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
         u_ci = 0;
         if (++u_s == a.S) { u_s = 0; ++u_r; }
       }
+    } else if (a.C < BK && BK % a.C == 0) {
+      // C divides the K-step (stem: C = 8 or 32): BK/C taps per step, each
+      // thread's chunk sits at a fixed (sub-tap, channel) inside the step
+      const int cpt = a.C / EPC;  // chunks per tap
+      const int sub = lc / cpt;
+      ci = (lc - sub * cpt) * EPC;
+      rs = kt * (BK / a.C) + sub;
+      r = rs / a.S;
+      s = rs - r * a.S;
     } else {
       const int kq = k0 + lc * EPC;  // first k of this thread's chunk
       rs = kq / a.C;

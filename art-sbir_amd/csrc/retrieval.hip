@@ -1,0 +1,582 @@
+// All-pairs L2 retrieval: top-k gallery items and the rank of the positive.
+//
+// Reference (inference.py:30-69, utils.py:42): per query,
+//   d_i = || q - g_i + 1e-6 ||_2   (nn.PairwiseDistance(p=2, eps=1e-6))
+//   topk(N, largest=False) -> position of the positive; topk(k) -> top-k list.
+// Here all queries are processed at once and the order is made total and
+// exact: distances are EVALUATED in f64 from the f32 features and sorted by
+// (distance, gallery index) — the oracle's definition (oracle/retrieval.py).
+//
+//  1. knn_scan_kernel (MFMA): for a (query tile x gallery chunk) workgroup,
+//     stream gallery tiles, compute approximate squared distances
+//     |q|^2 + |g|^2 - 2 q.g with bf16 (or exact-f32) MFMA and
+//       * keep, per query, the T smallest approximate values of the chunk
+//         (threshold filter -> rare insertions into a per-query register list),
+//       * count items certainly closer than the positive (approx < lo_q) and
+//         queue the uncertain ones (lo_q <= approx <= hi_q) for exact checks,
+//     where [lo_q, hi_q] = d_pos^2 -/+ eps_q and eps_q bounds the approximation
+//     error of the squared distance;
+//  2. knn_merge_kernel: exact f64 distances of the S*T candidates of a query,
+//     top-k by (distance, index), plus a verification flag if a chunk list
+//     could have dropped a true top-k item (then the host reruns that query
+//     with an exhaustive exact scan);
+//  3. knn_uncertain_kernel: exact checks of the queued uncertain items.
+#include "common.h"
+#include "../../include/artsbir.h"
+
+namespace artsbir {
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4r;
+#define ROOB 0x80000000u
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rrsrc(const void* base, long long bytes) {
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 rload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  u32x4r v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+template <typename T> struct RM;
+template <> struct RM<bf16> {
+  static constexpr int EPC = 8;
+  __device__ __forceinline__ static void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&a),
+                                                  *reinterpret_cast<const bf16x8*>(&b), acc, 0, 0, 0);
+  }
+};
+template <> struct RM<float> {
+  static constexpr int EPC = 4;
+  __device__ __forceinline__ static void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    const float* fa = reinterpret_cast<const float*>(&a);
+    const float* fb = reinterpret_cast<const float*>(&b);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[e], fb[e], acc, 0, 0, 0);
+  }
+};
+
+// ---------------------------------------------------------------- helpers
+// squared norm of each f32 row, and the compute-dtype copy of the row
+template <typename T>
+__global__ void rows_prep_kernel(const float* __restrict__ x, int n, int D, float* __restrict__ sq, T* __restrict__ xc,
+                                 int ldc) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* r = x + (long long)row * D;
+  float s = 0.f;
+  for (int d = lane; d < ldc; d += 64) {  // the compute copy is zero-padded to ldc columns
+    const float v = d < D ? r[d] : 0.f;
+    s += v * v;
+    if (xc) xc[(long long)row * ldc + d] = from_f<T>(v);
+  }
+  s = warp_sum(s);
+  if (lane == 0) sq[row] = s;
+}
+
+// exact ||q - g + eps|| in f64 (one wave)
+__device__ __forceinline__ double exact_l2(const float* q, const float* g, int D, int lane) {
+  double s = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const double t = ((double)q[d] - (double)g[d]) + 1e-6;
+    s += t * t;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return sqrt(s);
+}
+
+// d_pos^2 (exact, f64) and the uncertainty band of every query
+__global__ void knn_band_kernel(const float* __restrict__ q, const float* __restrict__ g, const long long* __restrict__ pos,
+                                long long g_base, long long n_g, const float* __restrict__ qsq, float gsq_max, int nq, int D,
+                                float rel, double* __restrict__ dpos, float* __restrict__ lo, float* __restrict__ hi) {
+  const int lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (qi >= nq) return;
+  const long long p = pos[qi];
+  const double eps = rel * (2.0 * sqrt((double)qsq[qi] * gsq_max) + qsq[qi] + gsq_max) + 1e-3;
+  if (p < g_base || p >= g_base + n_g) {
+    // positive not in this shard: the caller provides dpos from its owner
+    if (lane == 0) {
+      const double d = dpos[qi];
+      lo[qi] = d >= 0 ? (float)(d * d - eps) : -1.f;
+      hi[qi] = d >= 0 ? (float)(d * d + eps) : -1.f;
+    }
+    return;
+  }
+  const double d = exact_l2(q + (long long)qi * D, g + (p - g_base) * D, D, lane);
+  if (lane == 0) {
+    dpos[qi] = d;
+    lo[qi] = (float)(d * d - eps);
+    hi[qi] = (float)(d * d + eps);
+  }
+}
+
+__global__ void knn_band_from_dpos_kernel(const double* __restrict__ dpos, const float* __restrict__ qsq, float gsq_max,
+                                          int nq, float rel, float* __restrict__ lo, float* __restrict__ hi) {
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi >= nq) return;
+  const double eps = rel * (2.0 * sqrt((double)qsq[qi] * gsq_max) + qsq[qi] + gsq_max) + 1e-3;
+  const double d = dpos[qi];
+  lo[qi] = d >= 0 ? (float)(d * d - eps) : -1.f;
+  hi[qi] = d >= 0 ? (float)(d * d + eps) : -1.f;
+}
+
+// ------------------------------------------------------------ fused scan
+struct KnnScanArgs {
+  const void* q;  // [Nq][D] compute dtype
+  const void* g;  // [Ng][D] compute dtype
+  const float* qsq;
+  const float* gsq;
+  int Nq, Ng, D;
+  int tiles_per_chunk;
+  int nchunks;
+  const float* lo;  // rank band (nullptr: no rank)
+  const float* hi;
+  int* cnt;         // [Nq] items certainly closer than the positive
+  int* unc;         // [unc_cap][2] (query, local gallery index); unc_n = unc + 2*unc_cap
+  int unc_cap;
+  float* cand_d;    // [Nq][nchunks][KT]
+  int* cand_i;
+};
+
+constexpr int KT = 16;  // per (query, chunk) candidate list length
+
+template <typename T>
+__global__ void __launch_bounds__(256) knn_scan_kernel(KnnScanArgs a) {
+  constexpr int EPC = RM<T>::EPC;
+  constexpr int ES = sizeof(T);
+  constexpr int BM = 128, BN = 128, BK = 8 * EPC;
+  constexpr int A_BYTES = 8 * (BM + 1) * 16, B_BYTES = 8 * (BN + 1) * 16;
+  constexpr int MAIN = 2 * (A_BYTES + B_BYTES);
+  constexpr int LD = BN + 4;
+  constexpr int EPI = BM * LD * 4;
+  constexpr int SMEM = (MAIN > EPI ? MAIN : EPI);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  __shared__ float s_gsq[BN];
+  __shared__ float s_thr[BM];
+  __shared__ int s_qn[BM];              // queued insertions per row this tile
+  __shared__ float s_qd[BM][8];
+  __shared__ int s_qi[BM][8];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int ntq = (a.Nq + BM - 1) / BM;
+  const int chunk = blockIdx.x / ntq;
+  const int qt = blockIdx.x % ntq;
+  const int bm = qt * BM;
+  const int tile0 = chunk * a.tiles_per_chunk;
+  int ntiles = (a.Ng + BN - 1) / BN - tile0;
+  if (ntiles > a.tiles_per_chunk) ntiles = a.tiles_per_chunk;
+  if (ntiles <= 0) return;
+
+  const __amdgpu_buffer_rsrc_t qr = rrsrc(reinterpret_cast<const T*>(a.q) + (long long)bm * a.D,
+                                          (long long)(a.Nq - bm) * a.D * ES);
+  // chunk-relative gallery descriptor keeps byte offsets in 31 bits for any N
+  const long long g0 = (long long)tile0 * BN;
+  const __amdgpu_buffer_rsrc_t gr = rrsrc(reinterpret_cast<const T*>(a.g) + g0 * a.D, (long long)(a.Ng - g0) * a.D * ES);
+  const int lc = tid & 7, lr = tid >> 3;
+  const int nk = a.D / BK;
+
+  // the row owner (2 threads per row: t = 2r, 2r+1 scan one half each; 2r owns the list)
+  const int my_row = tid >> 1, my_half = tid & 1;
+  const bool owner = my_half == 0;
+  const bool row_ok = bm + my_row < a.Nq;
+  float lst_d[KT];
+  int lst_i[KT];
+#pragma unroll
+  for (int i = 0; i < KT; ++i) { lst_d[i] = INFINITY; lst_i[i] = -1; }
+  int closer = 0;
+  const float lo = (a.lo && row_ok) ? a.lo[bm + my_row] : -1.f;
+  const float hi = (a.lo && row_ok) ? a.hi[bm + my_row] : -1.f;
+  const float qsq = row_ok ? a.qsq[bm + my_row] : 0.f;
+  if (tid < BM) s_thr[tid] = INFINITY;
+
+  uint4 ra[4], rb[4];
+  for (int t = 0; t < ntiles; ++t) {
+    const int bn = (tile0 + t) * BN;
+    auto load_tiles = [&](int kt) {
+      const int k0 = kt * BK;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = lr + 32 * i;
+        ra[i] = rload(qr, (unsigned)((row * a.D + k0 + lc * EPC) * ES));
+        const int gi = bn + row;
+        rb[i] = rload(gr, gi < a.Ng ? (unsigned)(((gi - (int)g0) * a.D + k0 + lc * EPC) * ES) : ROOB);
+      }
+    };
+    auto store_tiles = [&](int buf) {
+      char* As = smem + buf * (A_BYTES + B_BYTES);
+      char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        *reinterpret_cast<uint4*>(As + (lc * (BM + 1) + lr + 32 * i) * 16) = ra[i];
+        *reinterpret_cast<uint4*>(Bs + (lc * (BN + 1) + lr + 32 * i) * 16) = rb[i];
+      }
+    };
+    f32x4 acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (tid < BN) s_gsq[tid] = (bn + tid < a.Ng) ? a.gsq[bn + tid] : INFINITY;
+    load_tiles(0);
+    store_tiles(0);
+    __syncthreads();
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) load_tiles(kt + 1);
+      const char* As = smem + cur * (A_BYTES + B_BYTES);
+      const char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int gq = kk * 4 + fq;
+        uint4 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const uint4*>(As + (gq * (BM + 1) + wm * 64 + i * 16 + fr) * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs + (gq * (BN + 1) + wn * 64 + j * 16 + fr) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) RM<T>::mma(acc[i][j], af[i], bfr[j]);
+      }
+      if (kt + 1 < nk) store_tiles(cur ^ 1);
+      __syncthreads();
+    }
+    // stage q.g as f32, then each row is scanned by two threads (64 columns each)
+    float* st = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st[(wm * 64 + i * 16 + fq * 4 + r) * LD + wn * 64 + j * 16 + fr] = acc[i][j][r];
+    if (tid < BM) s_qn[tid] = 0;
+    __syncthreads();
+    if (row_ok) {
+      const float thr = s_thr[my_row];  // INF on the first tile: the owner rescans instead
+      const float* srow = st + my_row * LD + my_half * 64;
+      for (int c4 = 0; c4 < 64; c4 += 4) {
+        const float4 s4 = *reinterpret_cast<const float4*>(srow + c4);
+        const float sv[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = my_half * 64 + c4 + e;
+          const float d2 = qsq + s_gsq[c] - 2.f * sv[e];
+          if (d2 < thr && thr != INFINITY) {
+            const int slot = atomicAdd(&s_qn[my_row], 1);
+            if (slot < 8) { s_qd[my_row][slot] = d2; s_qi[my_row][slot] = bn + c; }
+          }
+          if (hi >= 0.f && bn + c < a.Ng) {
+            if (d2 < lo) {
+              ++closer;
+            } else if (d2 <= hi) {
+              const int k = atomicAdd(a.unc + 2 * a.unc_cap, 1);
+              if (k < a.unc_cap) { a.unc[2 * k] = bm + my_row; a.unc[2 * k + 1] = bn + c; }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // the owner merges the queued values into its sorted register list; if the
+    // list was not yet full (first tile) or the queue overflowed, it rescans the
+    // whole staged row instead
+    if (owner && row_ok) {
+      const int nq = s_qn[my_row];
+      auto insert = [&](float x, int xi) {
+#pragma unroll
+        for (int i = 0; i < KT; ++i) {  // compare-swap down the sorted list
+          const bool sw = x < lst_d[i] || (x == lst_d[i] && xi < lst_i[i] && lst_i[i] >= 0);
+          const float td = lst_d[i];
+          const int ti = lst_i[i];
+          lst_d[i] = sw ? x : td;
+          lst_i[i] = sw ? xi : ti;
+          x = sw ? td : x;
+          xi = sw ? ti : xi;
+        }
+      };
+      if (nq > 8 || s_thr[my_row] == INFINITY) {
+        const float* srow = st + my_row * LD;
+        const float thr0 = s_thr[my_row];
+        for (int c = 0; c < BN; ++c) {
+          const float d2 = qsq + s_gsq[c] - 2.f * srow[c];
+          if (d2 < thr0 && bn + c < a.Ng) insert(d2, bn + c);
+        }
+      } else {
+        for (int k = 0; k < nq; ++k) insert(s_qd[my_row][k], s_qi[my_row][k]);
+      }
+      s_thr[my_row] = lst_d[KT - 1];
+    }
+    __syncthreads();
+  }
+  if (row_ok) {
+    if (closer) atomicAdd(a.cnt + bm + my_row, closer);
+    if (owner) {
+      const long long o = ((long long)(bm + my_row) * a.nchunks + chunk) * KT;
+#pragma unroll
+      for (int i = 0; i < KT; ++i) {
+        a.cand_d[o + i] = lst_d[i];
+        a.cand_i[o + i] = lst_i[i];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------ exact merge
+// one workgroup per query: exact f64 distances of every candidate, top-k by
+// (distance, global index), verification of the chunk lists.
+__global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict__ q, const float* __restrict__ g, int D,
+                                                        int nchunks, const float* __restrict__ cand_d,
+                                                        const int* __restrict__ cand_i, const float* __restrict__ qsq,
+                                                        float gsq_max, float rel, long long g_base, int k,
+                                                        long long* __restrict__ out_i, double* __restrict__ out_d,
+                                                        int* __restrict__ flag) {
+  extern __shared__ char sm[];
+  const int nc = nchunks * KT;
+  double* ed = reinterpret_cast<double*>(sm);           // [nc]
+  int* ei = reinterpret_cast<int*>(ed + nc);            // [nc]
+  const int qi = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float* qr = q + (long long)qi * D;
+  const float* cd = cand_d + (long long)qi * nc;
+  const int* ci = cand_i + (long long)qi * nc;
+  const double eps = rel * (2.0 * sqrt((double)qsq[qi] * gsq_max) + qsq[qi] + gsq_max) + 1e-3;
+  __shared__ double rd[4];
+  __shared__ int ri[4], rslot[4];
+  // (1) a_k = k-th smallest approximate value: the k items with approx <= a_k have
+  //     exact d^2 <= a_k + eps, so every true top-k item has approx <= a_k + 2 eps
+  for (int c = threadIdx.x; c < nc; c += blockDim.x) { ed[c] = ci[c] >= 0 ? (double)cd[c] : INFINITY; ei[c] = c; }
+  __syncthreads();
+  double ak = INFINITY;
+  for (int r = 0; r < k; ++r) {
+    double bd = INFINITY;
+    int bs = -1;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x)
+      if (ei[c] >= 0 && ed[c] < bd) { bd = ed[c]; bs = c; }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, 64);
+      const int os = __shfl_xor(bs, o, 64);
+      if (od < bd) { bd = od; bs = os; }
+    }
+    if (lane == 0) { rd[wid] = bd; rslot[wid] = bs; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double b = rd[0];
+      int s2 = rslot[0];
+      for (int w = 1; w < (int)blockDim.x / 64; ++w)
+        if (rd[w] < b) { b = rd[w]; s2 = rslot[w]; }
+      if (s2 >= 0) ei[s2] = -1;
+      rd[0] = b;
+    }
+    __syncthreads();
+    ak = rd[0];
+    __syncthreads();
+  }
+  const double cut = ak + 2.0 * eps;
+  // (2) exact f64 distances only for candidates that can still be in the top-k
+  for (int c = wid; c < nc; c += blockDim.x / 64) {
+    const int gi = ci[c];
+    double d = INFINITY;
+    const bool live = gi >= 0 && (double)cd[c] <= cut;
+    if (live) d = exact_l2(qr, g + (long long)gi * D, D, lane);
+    if (lane == 0) { ed[c] = d; ei[c] = live ? gi : -1; }
+  }
+  __syncthreads();
+  // (3) k rounds of a block-wide argmin on (exact distance, index)
+  double kth = INFINITY;
+  for (int r = 0; r < k; ++r) {
+    double bd = INFINITY;
+    int bi = 0x7fffffff, bs = -1;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+      const double d = ed[c];
+      const int i = ei[c];
+      if (i >= 0 && (d < bd || (d == bd && i < bi))) { bd = d; bi = i; bs = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, 64);
+      const int oi = __shfl_xor(bi, o, 64), os = __shfl_xor(bs, o, 64);
+      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; bs = os; }
+    }
+    if (lane == 0) { rd[wid] = bd; ri[wid] = bi; rslot[wid] = bs; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double b = rd[0];
+      int bi2 = ri[0], bs2 = rslot[0];
+      for (int w = 1; w < (int)blockDim.x / 64; ++w)
+        if (rd[w] < b || (rd[w] == b && ri[w] < bi2)) { b = rd[w]; bi2 = ri[w]; bs2 = rslot[w]; }
+      out_i[(long long)qi * k + r] = bs2 >= 0 ? g_base + bi2 : -1;
+      out_d[(long long)qi * k + r] = b;
+      if (bs2 >= 0) ei[bs2] = -1;  // remove
+      rd[0] = b;
+    }
+    __syncthreads();
+    kth = rd[0];
+    __syncthreads();
+  }
+  // verification: a full chunk list whose last approximate value is within the
+  // error band of the k-th exact distance may have dropped a true top-k item
+  if (threadIdx.x == 0) {
+    int bad = 0;
+    for (int c = 0; c < nchunks; ++c) {
+      const float last = cd[c * KT + KT - 1];
+      if (ci[c * KT + KT - 1] >= 0 && (double)last - eps <= kth * kth) bad = 1;
+    }
+    flag[qi] = bad;
+  }
+}
+
+// exact checks of the uncertain items of the rank count
+__global__ void knn_uncertain_kernel(const float* __restrict__ q, const float* __restrict__ g, int D,
+                                     const int* __restrict__ unc, int unc_cap, const double* __restrict__ dpos,
+                                     const long long* __restrict__ pos, long long g_base, int* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int n = min(unc[2 * unc_cap], unc_cap);
+  for (int e = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); e < n; e += gridDim.x * (blockDim.x / 64)) {
+    const int qi = unc[2 * e], gi = unc[2 * e + 1];
+    const double d = exact_l2(q + (long long)qi * D, g + (long long)gi * D, D, lane);
+    const double dp = dpos[qi];
+    const long long ggi = g_base + gi;
+    if (lane == 0 && (d < dp || (d == dp && ggi < pos[qi]))) atomicAdd(cnt + qi, 1);
+  }
+}
+
+// exhaustive exact scan of one query (fallback for flagged queries, and the
+// small-gallery path): writes all exact distances
+__global__ void knn_exact_all_kernel(const float* __restrict__ q, const float* __restrict__ g, int D, int n,
+                                     double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  for (int i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += gridDim.x * (blockDim.x / 64)) {
+    const double d = exact_l2(q, g + (long long)i * D, D, lane);
+    if (lane == 0) out[i] = d;
+  }
+}
+
+// nn.PairwiseDistance(p=2, eps=1e-6) with broadcasting of a one-row operand,
+// f32 arithmetic as torch does it (utils.euclidean_distance)
+__global__ void pairwise_l2_kernel(const float* __restrict__ x1, long long n1, const float* __restrict__ x2, long long n2,
+                                   int D, float eps, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const long long n = n1 > n2 ? n1 : n2;
+  for (long long i = blockIdx.x * (long long)(blockDim.x / 64) + (threadIdx.x >> 6); i < n;
+       i += (long long)gridDim.x * (blockDim.x / 64)) {
+    const float* a = x1 + (n1 == 1 ? 0 : i) * D;
+    const float* b = x2 + (n2 == 1 ? 0 : i) * D;
+    float s = 0.f;
+    for (int d = lane; d < D; d += 64) {
+      const float t = a[d] - b[d] + eps;
+      s += t * t;
+    }
+    s = warp_sum(s);
+    if (lane == 0) out[i] = sqrtf(s);
+  }
+}
+
+}  // namespace artsbir
+
+using namespace artsbir;
+
+extern "C" int artsbir_pairwise_l2(const float* x1, long long n1, const float* x2, long long n2, int D, float eps,
+                                   float* out, void* stream) {
+  if (!(n1 == n2 || n1 == 1 || n2 == 1)) { set_error("pairwise_l2: shapes %lld vs %lld", n1, n2); return -1; }
+  const long long n = n1 > n2 ? n1 : n2;
+  long long grid = (n + 3) / 4;
+  if (grid > 65536) grid = 65536;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(pairwise_l2_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, x1, n1, x2, n2, D, eps, out);
+  ARTSBIR_CHECK_LAUNCH("pairwise_l2");
+  return 0;
+}
+
+extern "C" int artsbir_rows_prep(int dtype, const float* x, int n, int D, float* sq, void* xc, int ldc, void* stream) {
+  const unsigned grid = (unsigned)((n + 3) / 4);
+  if (n <= 0) return 0;
+  if (ldc < D) ldc = D;
+  if (dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL(rows_prep_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, D, sq, (bf16*)xc, ldc);
+  else
+    hipLaunchKernelGGL(rows_prep_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, D, sq, (float*)xc, ldc);
+  ARTSBIR_CHECK_LAUNCH("rows_prep");
+  return 0;
+}
+
+extern "C" int artsbir_knn_band(const float* q, const float* g, const long long* pos, long long g_base, long long n_g,
+                                const float* qsq, float gsq_max, int nq, int D, float rel, double* dpos, float* lo,
+                                float* hi, void* stream) {
+  if (nq <= 0) return 0;
+  hipLaunchKernelGGL(knn_band_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, (hipStream_t)stream, q, g, pos, g_base,
+                     n_g, qsq, gsq_max, nq, D, rel, dpos, lo, hi);
+  ARTSBIR_CHECK_LAUNCH("knn_band");
+  return 0;
+}
+
+extern "C" int artsbir_knn_band_from_dpos(const double* dpos, const float* qsq, float gsq_max, int nq, float rel,
+                                          float* lo, float* hi, void* stream) {
+  if (nq <= 0) return 0;
+  hipLaunchKernelGGL(knn_band_from_dpos_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     dpos, qsq, gsq_max, nq, rel, lo, hi);
+  ARTSBIR_CHECK_LAUNCH("knn_band_from_dpos");
+  return 0;
+}
+
+extern "C" int artsbir_knn_candidates_per_query(int ng, int tiles_per_chunk) {
+  const int tiles = (ng + 127) / 128;
+  const int nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
+  return nchunks * KT;
+}
+
+extern "C" int artsbir_knn_scan(int dtype, const void* qc, const void* gc, const float* qsq, const float* gsq, int nq,
+                                int ng, int D, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc,
+                                int unc_cap, float* cand_d, int* cand_i, void* stream) {
+  const int EPC = dtype == ARTSBIR_DT_BF16 ? 8 : 4;
+  if (D % (8 * EPC)) { set_error("knn_scan: D=%d must be a multiple of %d", D, 8 * EPC); return -1; }
+  if (nq <= 0 || ng <= 0) return 0;
+  KnnScanArgs a;
+  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.Nq = nq; a.Ng = ng; a.D = D;
+  a.tiles_per_chunk = tiles_per_chunk;
+  const int tiles = (ng + 127) / 128;
+  a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
+  a.lo = lo; a.hi = hi; a.cnt = cnt; a.unc = unc; a.unc_cap = unc_cap; a.cand_d = cand_d; a.cand_i = cand_i;
+  const unsigned grid = (unsigned)(a.nchunks * ((nq + 127) / 128));
+  if (dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL(knn_scan_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(knn_scan_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
+  ARTSBIR_CHECK_LAUNCH("knn_scan");
+  return 0;
+}
+
+extern "C" int artsbir_knn_merge(const float* q, const float* g, int D, int nq, int nchunks, const float* cand_d,
+                                 const int* cand_i, const float* qsq, float gsq_max, float rel, long long g_base, int k,
+                                 long long* out_i, double* out_d, int* flag, void* stream) {
+  if (nq <= 0) return 0;
+  if (k > nchunks * KT) { set_error("knn_merge: k=%d exceeds candidates %d", k, nchunks * KT); return -1; }
+  const size_t sh = (size_t)nchunks * KT * (sizeof(double) + sizeof(int));
+  if (sh > 60000) { set_error("knn_merge: too many candidates (%d chunks)", nchunks); return -1; }
+  hipLaunchKernelGGL(knn_merge_kernel, dim3(nq), dim3(256), sh, (hipStream_t)stream, q, g, D, nchunks, cand_d, cand_i,
+                     qsq, gsq_max, rel, g_base, k, out_i, out_d, flag);
+  ARTSBIR_CHECK_LAUNCH("knn_merge");
+  return 0;
+}
+
+extern "C" int artsbir_knn_uncertain(const float* q, const float* g, int D, const int* unc, int unc_cap,
+                                     const double* dpos, const long long* pos, long long g_base, int* cnt, void* stream) {
+  hipLaunchKernelGGL(knn_uncertain_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, q, g, D, unc, unc_cap, dpos,
+                     pos, g_base, cnt);
+  ARTSBIR_CHECK_LAUNCH("knn_uncertain");
+  return 0;
+}
+
+extern "C" int artsbir_knn_exact_all(const float* q, const float* g, int D, int n, double* out, void* stream) {
+  if (n <= 0) return 0;
+  unsigned grid = (unsigned)((n + 3) / 4);
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(knn_exact_all_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, q, g, D, n, out);
+  ARTSBIR_CHECK_LAUNCH("knn_exact_all");
+  return 0;
+}

@@ -1,0 +1,118 @@
+"""Datasets feeding the hot path (/root/reference/data_preparation.py, hot-path parts).
+
+  InferenceDataset      data_preparation.py:24-41 — gallery paths de-duplicated
+                        (first occurrence kept) and SORTED; this order defines the
+                        gallery index used by retrieval ranks.
+  SyntheticTripletDataset  stands in for the Sketchy/Kaggle datasets (no data and
+                        no network here): same interface as RetrievalDataset
+                        (sketch_paths, photo_paths, __getitem__ -> (sketch, pos,
+                        neg) with the negative drawn by random.choice after
+                        random.seed(seed), state_dict), sketch names
+                        "<photo-stem>-<n>.png" so inference.py's name parsing and
+                        utils.find_image_index work unchanged.  Images are
+                        generated deterministically from the path (PCG64 seeded
+                        by crc32(path)): photos uniform [0,1), sketches 90 % white
+                        / 10 % black strokes correlated with their photo, both
+                        through the CLIP normalize of models.py:294.
+  get_datasets          data_preparation.py:796-848 factory ("Synthetic*").
+"""
+from __future__ import annotations
+
+import random
+import zlib
+from pathlib import Path
+from typing import Dict, List
+
+import numpy as np
+import torch
+from torch.utils.data import Dataset
+
+MEAN = np.array((0.48145466, 0.4578275, 0.40821073), np.float32)[:, None, None]
+STD = np.array((0.26862954, 0.26130258, 0.27577711), np.float32)[:, None, None]
+
+
+def _rng(path) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64(zlib.crc32(str(path).encode())))
+
+
+def synthetic_photo(path, res: int) -> torch.Tensor:
+    img = _rng(path).random((3, res, res), dtype=np.float32)
+    return torch.from_numpy((img - MEAN) / STD)
+
+
+def synthetic_sketch(path, photo_path, res: int) -> torch.Tensor:
+    # strokes where the photo's luminance is low, plus 5 % noise: a learnable pairing
+    photo = _rng(photo_path).random((3, res, res), dtype=np.float32).mean(0)
+    noise = _rng(path).random((res, res), dtype=np.float32)
+    stroke = (photo < 0.3) ^ (noise < 0.05)
+    img = np.where(stroke, 0.0, 1.0).astype(np.float32)[None].repeat(3, axis=0)
+    return torch.from_numpy((img - MEAN) / STD)
+
+
+class InferenceDataset(Dataset):
+    def __init__(self, image_paths: List[Path], transform=None, resolution: int = 224):
+        super().__init__()
+        self.transform = transform
+        self.resolution = resolution
+        self.image_paths = list(dict.fromkeys(image_paths))
+        self.image_paths.sort()
+
+    def __len__(self) -> int:
+        return len(self.image_paths)
+
+    def __getitem__(self, idx: int) -> torch.Tensor:
+        p = self.image_paths[idx]
+        if Path(p).is_file() and self.transform is not None:
+            from PIL import Image
+            return self.transform(Image.open(p))
+        return synthetic_photo(p, self.resolution)
+
+
+class SyntheticTripletDataset(Dataset):
+    def __init__(self, n: int = 256, resolution: int = 224, mode: str = "train", split_ratio: float = 0.1,
+                 size: float = 1.0, seed: int = 42, transform=None, dups: int = 1):
+        super().__init__()
+        if mode not in ("train", "test"):
+            raise ValueError("invalid mode: [train, test]")
+        random.seed(seed)
+        self.mode, self.size, self.seed, self.split_ratio = mode, size, seed, split_ratio
+        self.resolution, self.transform = resolution, transform
+        total = max(2, int(n * size))
+        n_test = max(1, int(round(total * split_ratio)))
+        ids = list(range(total))
+        ids = ids[n_test:] if mode == "train" else ids[:n_test]
+        root = Path("data/synthetic")
+        # several sketches per photo (Sketchy has ~5): "<stem>-<k>.png"
+        self.photo_paths = [root / "photos" / f"img{i:07d}.jpg" for i in ids for _ in range(dups)]
+        self.sketch_paths = [root / "sketches" / f"img{i:07d}-{k + 1}.png" for i in ids for k in range(dups)]
+
+    def __len__(self) -> int:
+        return len(self.sketch_paths)
+
+    def load_image_sketch_tuple(self, idx):
+        neg = random.choice(self.photo_paths)  # may pick the positive, as the reference does
+        return self.sketch_paths[idx], self.photo_paths[idx], neg
+
+    def __getitem__(self, idx):
+        s, p, n = self.load_image_sketch_tuple(idx)
+        r = self.resolution
+        return synthetic_sketch(s, p, r), synthetic_photo(p, r), synthetic_photo(n, r)
+
+    def sketch(self, idx):
+        return synthetic_sketch(self.sketch_paths[idx], self.photo_paths[idx], self.resolution)
+
+    @property
+    def state_dict(self) -> Dict:
+        return {"dataset": f"{self.__class__.__name__}", "size": self.size, "img_number": len(self),
+                "img_type": "synthetic", "img_format": "jpg", "sketch_format": "png", "seed": self.seed,
+                "split_ratio": self.split_ratio, "mode": self.mode, "transform": str(self.transform)}
+
+
+def get_datasets(dataset: str = "Synthetic", size: float = 1.0, sketch_format: str = 'png', img_format: str = 'jpg',
+                 sketch_type: str = 'placeholder', img_type: str = 'photos', split_ratio: float = 0.1, seed: int = 42,
+                 transform=None, n: int = 256, resolution: int = 224, **kw):
+    if dataset.startswith("Synthetic"):
+        tr = SyntheticTripletDataset(n, resolution, "train", split_ratio, size, seed, transform)
+        te = SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform)
+        return tr, te
+    raise Exception(f"{dataset} is not available (no datasets ship with this build; use Synthetic)")

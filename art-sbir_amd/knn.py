@@ -1,0 +1,169 @@
+"""Batched exact L2 retrieval on libartsbir_hip (single GPU and gallery-sharded).
+
+Replaces the per-query loop of inference.py:104-121 (model(sketch) ->
+utils.euclidean_distance(q[1,D], G[N,D]) -> distances.topk(N) -> position of
+the positive; get_topk_images topk(k)).  All queries are scored at once by the
+fused MFMA scan (retrieval.hip); the final order is exact: f64 distances of
+the f32 features, ties broken by the lower gallery index (oracle/retrieval.py).
+
+Sharding: every rank holds rows [g_base, g_base + n) of the
+gallery, computes its local exact top-k and its count of items closer than the
+positive; one all_gather of (k indices, k distances) per query and one
+all_reduce of the counts give the global answer.
+"""
+from __future__ import annotations
+
+import torch
+
+import _hip
+from _hip import call, ptr
+
+# relative bound on the error of the approximate squared distance
+# |q|^2+|g|^2-2q.g (bf16 operands + f32 accumulation, or exact f32 MFMA)
+REL = {_hip.DT_BF16: 2.0 ** -6, _hip.DT_F32: 2.0 ** -14}
+TILES_PER_CHUNK = 64
+UNC_CAP = 1 << 20
+
+
+def _s():
+    return _hip.stream()
+
+
+def knn(queries: torch.Tensor, gallery: torch.Tensor, k: int = 10, positives: torch.Tensor | None = None,
+        compute: str = "bf16", g_base: int = 0, dpos: torch.Tensor | None = None,
+        tiles_per_chunk: int = TILES_PER_CHUNK):
+    """Exact top-k and rank of the positive.
+
+    queries [Q, D], gallery [N, D] (float, CUDA).  positives: int64 [Q] global
+    gallery index of each query's positive (-1: none) or None.  Returns
+    (idx int64 [Q, k] global indices, dist float64 [Q, k], rank int64 [Q] or None,
+    dpos float64 [Q] or None).  With g_base/dpos this is one shard of a larger
+    gallery: dpos must then hold the exact positive distance (or -1) for rows
+    whose positive lives in another shard.
+    """
+    if not (queries.is_cuda and gallery.is_cuda):
+        raise RuntimeError("knn on libartsbir_hip needs CUDA tensors")
+    q = queries.detach().contiguous().float()
+    g = gallery.detach().contiguous().float()
+    Q, D = q.shape
+    N = g.shape[0]
+    dev = q.device
+    dt = _hip.DT_BF16 if compute == "bf16" else _hip.DT_F32
+    tdt = torch.bfloat16 if dt == _hip.DT_BF16 else torch.float32
+    rel = REL[dt]
+    if k > N:
+        raise ValueError(f"k={k} > gallery size {N}")
+    if k > _hip.lib().artsbir_knn_candidates_per_query(N, tiles_per_chunk):
+        tiles_per_chunk = 1  # more chunks -> more candidates per query (k <= 16 * chunks)
+        if k > _hip.lib().artsbir_knn_candidates_per_query(N, 1):
+            raise ValueError(f"k={k} exceeds the candidate capacity for a gallery of {N}")
+    qsq = torch.empty(Q, dtype=torch.float32, device=dev)
+    gsq = torch.empty(N, dtype=torch.float32, device=dev)
+    step = 64 if dt == _hip.DT_BF16 else 32
+    Dp = (D + step - 1) // step * step  # MFMA scan: zero-padded compute copies
+    qc = torch.empty(Q, Dp, dtype=tdt, device=dev)
+    gc = torch.empty(N, Dp, dtype=tdt, device=dev)
+    call("artsbir_rows_prep", dt, ptr(q), Q, D, ptr(qsq), ptr(qc), Dp, _s())
+    call("artsbir_rows_prep", dt, ptr(g), N, D, ptr(gsq), ptr(gc), Dp, _s())
+    gsq_max = float(gsq.max().item()) if N else 0.0
+
+    lo = hi = pos = None
+    if positives is not None:
+        pos = positives.to(dev, torch.int64).contiguous()
+        if dpos is None:
+            dpos = torch.full((Q,), -1.0, dtype=torch.float64, device=dev)
+        else:
+            dpos = dpos.to(dev, torch.float64).contiguous().clone()
+        lo = torch.empty(Q, dtype=torch.float32, device=dev)
+        hi = torch.empty(Q, dtype=torch.float32, device=dev)
+        call("artsbir_knn_band", ptr(q), ptr(g), ptr(pos), g_base, N, ptr(qsq), gsq_max, Q, D, rel, ptr(dpos),
+             ptr(lo), ptr(hi), _s())
+    cnt = torch.zeros(Q, dtype=torch.int32, device=dev)
+    unc = torch.zeros(2 * UNC_CAP + 1, dtype=torch.int32, device=dev)
+    ncand = _hip.lib().artsbir_knn_candidates_per_query(N, tiles_per_chunk)
+    nchunks = ncand // 16
+    cand_d = torch.empty(Q, ncand, dtype=torch.float32, device=dev)
+    cand_i = torch.empty(Q, ncand, dtype=torch.int32, device=dev)
+    call("artsbir_knn_scan", dt, ptr(qc), ptr(gc), ptr(qsq), ptr(gsq), Q, N, Dp, tiles_per_chunk, ptr(lo), ptr(hi),
+         ptr(cnt), ptr(unc), UNC_CAP, ptr(cand_d), ptr(cand_i), _s(), kernel="knn_scan_kernel",
+         flops=2.0 * Q * N * D)
+    out_i = torch.empty(Q, k, dtype=torch.int64, device=dev)
+    out_d = torch.empty(Q, k, dtype=torch.float64, device=dev)
+    flag = torch.empty(Q, dtype=torch.int32, device=dev)
+    call("artsbir_knn_merge", ptr(q), ptr(g), D, Q, nchunks, ptr(cand_d), ptr(cand_i), ptr(qsq), gsq_max, rel,
+         g_base, k, ptr(out_i), ptr(out_d), ptr(flag), _s())
+    rank = None
+    if positives is not None:
+        call("artsbir_knn_uncertain", ptr(q), ptr(g), D, ptr(unc), UNC_CAP, ptr(dpos), ptr(pos), g_base, ptr(cnt),
+             _s())
+        if int(unc[2 * UNC_CAP].item()) > UNC_CAP:
+            cnt = _exact_counts(q, g, pos, dpos, g_base)
+        rank = cnt.to(torch.int64)
+    # rare: a chunk list could have hidden a true top-k item -> exhaustive exact pass
+    bad = torch.nonzero(flag).flatten().tolist()
+    for qi in bad:
+        d = torch.empty(N, dtype=torch.float64, device=dev)
+        call("artsbir_knn_exact_all", ptr(q[qi]), ptr(g), D, N, ptr(d), _s())
+        order = _stable_order(d)[:k]
+        out_i[qi] = order + g_base
+        out_d[qi] = d[order]
+    return out_i, out_d, rank, dpos
+
+
+def _stable_order(d: torch.Tensor) -> torch.Tensor:
+    return torch.sort(d, stable=True).indices
+
+
+def _exact_counts(q, g, pos, dpos, g_base):
+    """exhaustive exact rank counts (uncertain-queue overflow fallback)."""
+    Q, D = q.shape
+    N = g.shape[0]
+    cnt = torch.zeros(Q, dtype=torch.int32, device=q.device)
+    d = torch.empty(N, dtype=torch.float64, device=q.device)
+    idx = torch.arange(N, device=q.device) + g_base
+    for qi in range(Q):
+        if dpos[qi].item() < 0:
+            continue
+        call("artsbir_knn_exact_all", ptr(q[qi]), ptr(g), D, N, ptr(d), _s())
+        dp = dpos[qi]
+        cnt[qi] = int(((d < dp) | ((d == dp) & (idx < pos[qi]))).sum().item())
+    return cnt
+
+
+def knn_sharded(queries, gallery_shard, g_base: int, k: int = 10, positives=None, compute="bf16"):
+    """Gallery sharded over the ranks of the default process group (RCCL):
+    every rank passes ITS shard [g_base, g_base + n) and the same queries."""
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    Q = queries.shape[0]
+    dpos = None
+    if positives is not None:
+        # exact positive distance from the owning shard, then shared (max of -1s)
+        pos = positives.to(queries.device, torch.int64)
+        n = gallery_shard.shape[0]
+        own = (pos >= g_base) & (pos < g_base + n)
+        dpos = torch.full((Q,), -1.0, dtype=torch.float64, device=queries.device)
+        if bool(own.any()):
+            qi = torch.nonzero(own).flatten()
+            sub = queries[qi].contiguous().float()
+            d = torch.empty(len(qi), dtype=torch.float64, device=queries.device)
+            gsub = gallery_shard.float()[pos[qi] - g_base].contiguous()
+            for j in range(len(qi)):
+                call("artsbir_knn_exact_all", ptr(sub[j]), ptr(gsub[j]), sub.shape[1], 1, ptr(d[j:j + 1]), _s())
+            dpos[qi] = d
+        dist.all_reduce(dpos, op=dist.ReduceOp.MAX)
+    idx, dd, rank, _ = knn(queries, gallery_shard, k, positives, compute, g_base=g_base, dpos=dpos)
+    all_i = [torch.empty_like(idx) for _ in range(world)]
+    all_d = [torch.empty_like(dd) for _ in range(world)]
+    dist.all_gather(all_i, idx)
+    dist.all_gather(all_d, dd)
+    ci = torch.cat(all_i, 1)
+    cd = torch.cat(all_d, 1)
+    # order by (distance, global index): stable sort by index, then by distance
+    o1 = torch.sort(ci, dim=1, stable=True).indices
+    ci, cd = torch.gather(ci, 1, o1), torch.gather(cd, 1, o1)
+    o2 = torch.sort(cd, dim=1, stable=True).indices[:, :k]
+    out_i, out_d = torch.gather(ci, 1, o2), torch.gather(cd, 1, o2)
+    if rank is not None:
+        dist.all_reduce(rank, op=dist.ReduceOp.SUM)
+    return out_i, out_d, rank

@@ -1,0 +1,203 @@
+"""Drop-in for /root/reference/train.py on MI355X (same CLI flags, same outputs).
+
+  get_loss        train.py:27-37  three separate encoder forwards (-> per-branch
+                                  BatchNorm statistics), dispatch on the output arity
+  triplet_train   train.py:39-98  epochs / iteration-level losses / timing dict
+  CLI             train.py:103-195
+Differences, all opt-in or documented:
+  * the model, loss and optimizer run on libartsbir_hip (models.ModifiedResNet,
+    losses.*, optim.Adam); ``--dtype bf16`` selects the MFMA bf16 throughput mode
+    (default f32 = the reference's arithmetic);
+  * get_loss dispatches on the output TYPE, not ``len(output) > 3`` (the
+    reference misfires for a plain model at batch size <= 3);
+  * the reference evaluates its test loss on the stale last TRAIN batch
+    (train.py:80,89); here the test batches are used unless ``--stale_eval``;
+  * data: the Sketchy/Kaggle files are not available offline — ``-d Synthetic``
+    (default) generates the triplets (data_preparation.SyntheticTripletDataset);
+  * one process per GPU when launched by torch.distributed.run: minibatches
+    are sharded and gradients all-reduced over RCCL (ddp.py).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+from timeit import default_timer as timer
+
+import torch
+from torch.utils.data import DataLoader
+
+import data_preparation
+import ddp
+import inference
+import losses
+import models
+import optim
+import utils
+
+device = "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def get_loss(loss_fn, model, elements):
+    s = model(elements[0])
+    p = model(elements[1])
+    n = model(elements[2])
+    if isinstance(s, torch.Tensor):
+        return loss_fn(s, p, n)
+    if len(s) == 2:
+        return loss_fn(s[0], p[0], n[0], s[1], p[1], elements[3])
+    return loss_fn(s[0], p[0], n[0], s[1], p[1], s[2], p[2], elements[3], elements[4])
+
+
+def triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
+                  stale_eval=False):
+    start_time = timer()
+    train_losses, test_losses, itrain_losses, itest_losses = [], [], [], []
+    iteration_loss_frequency = 10000 // train_dataloader.batch_size if epochs <= 6 else 0
+    itest_size = max(1000 // test_dataloader.batch_size, 1)
+    for epoch in range(epochs):
+        train_loss = torch.zeros((), device=device)
+        itrain_loss = 0.0
+        model.train()
+        elements = None
+        for batch, tup in enumerate(train_dataloader):
+            elements = [e.to(device) for e in tup]
+            loss = get_loss(loss_fn, model, elements)
+            optimizer.zero_grad()
+            loss.backward()
+            ddp.allreduce_gradients(model)
+            optimizer.step()
+            train_loss += loss.detach()
+            if iteration_loss_frequency and batch and batch % iteration_loss_frequency == 0:
+                itrain_losses.append((train_loss.item() - itrain_loss) / iteration_loss_frequency)
+                itrain_loss = train_loss.item()
+                itest_losses.append(_evaluate(model, loss_fn, test_dataloader, elements if stale_eval else None,
+                                              itest_size) / itest_size)
+                model.train()
+        test_loss = _evaluate(model, loss_fn, test_dataloader, elements if stale_eval else None, None)
+        train_losses.append(train_loss.item() / max(len(train_dataloader), 1))
+        test_losses.append(test_loss / max(len(test_dataloader), 1))
+        print(f"Epoch {epoch+1} - Train loss: {train_losses[epoch]:.5f} | Test loss: {test_losses[epoch]:.5f}",
+              flush=True)
+    return {"train_losses": train_losses, "test_losses": test_losses, "itrain_losses": itrain_losses,
+            "itest_losses": itest_losses, "iteration_loss_frequency": iteration_loss_frequency,
+            "iteration_test_size": itest_size, "training_time": timer() - start_time}
+
+
+@torch.no_grad()
+def _evaluate(model, loss_fn, loader, stale, limit):
+    """eval-mode loss over the test batches (or over the stale train batch, as the reference)."""
+    model.eval()
+    total = 0.0
+    for b, tup in enumerate(loader):
+        el = stale if stale is not None else [e.to(device) for e in tup]
+        total += float(get_loss(loss_fn, model, el).item())
+        if limit is not None and b >= limit:
+            break
+    return total
+
+
+def make_loss(loss_type, with_classification, dataset_name, margin):
+    if loss_type == 'euclidean':
+        if with_classification:
+            if 'Sketchy' in dataset_name:
+                return utils.TripletMarginLoss_with_classification(margin=margin)
+            if 'Mixed' in dataset_name:
+                return utils.TripletMarginLoss_with_classification(margin=margin, classification_weight=0.01)
+            if 'Kaggle' in dataset_name:
+                return utils.TripletMarginLoss_with_classification2(margin=margin, classification_weight=0,
+                                                                    classification_weight2=0.2)
+        return losses.TripletMarginLoss(margin=margin)
+    if loss_type == 'cosine':
+        if with_classification:
+            if 'Kaggle' in dataset_name:
+                return utils.TripletMarginLoss_with_classification2(margin=margin, distance_f=utils.cosine_distance)
+            return utils.TripletMarginLoss_with_classification(margin=margin, distance_f=utils.cosine_distance)
+        return losses.TripletMarginWithDistanceLoss(margin=margin, distance_function=utils.cosine_distance)
+    raise Exception(f"loss type not correct {loss_type}")
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="Starts training a model")
+    p.add_argument("-e", "--epochs", type=int, default=1)
+    p.add_argument("-b", "--batch_size", type=int, default=32)
+    p.add_argument("-l", "--learning_rate", type=float, default=0.00001)
+    p.add_argument("-m", "--model", type=str, default='openResNet50m.pth')
+    p.add_argument('--model_type', type=str, default='ModifiedResNet',
+                   choices=['ModifiedResNet', 'ModifiedResNet_with_classification'])
+    p.add_argument("-d", "--dataset", type=str, default='Synthetic')
+    p.add_argument("-s", "--dsize", type=float, default=1.0)
+    p.add_argument("--inference", action="store_true")
+    p.add_argument('--feature_folder', default=None)
+    p.add_argument("--no_training", action='store_true')
+    p.add_argument("-w", "--weight_decay", type=float, default=0.002)
+    p.add_argument('--img_type', type=str, default='photos')
+    p.add_argument('--sketch_type', default='sketches_png')
+    p.add_argument('--sketch_format', default='png', choices=['png', 'jpg'])
+    p.add_argument('--loss_type', default='euclidean', choices=['euclidean', 'cosine'])
+    p.add_argument('--loss_margin', type=float, default=0.2)
+    # additions
+    p.add_argument('--dtype', default='f32', choices=['f32', 'bf16'], help="encoder compute dtype")
+    p.add_argument('--layers', default='3,4,6,3', help="ModifiedResNet layers (reference: 3,4,6,3)")
+    p.add_argument('--output_dim', type=int, default=1024)
+    p.add_argument('--resolution', type=int, default=224)
+    p.add_argument('--width', type=int, default=64)
+    p.add_argument('--synthetic_n', type=int, default=256, help="triplets in the synthetic dataset")
+    p.add_argument('--stale_eval', action='store_true', help="reproduce the reference's stale-batch test loss")
+    p.add_argument('--no_save', action='store_true')
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    utils.MARGIN = args.loss_margin
+    layers = tuple(int(v) for v in args.layers.split(","))
+    model = utils.build_model(args.dataset, args.model_type, layers=layers, output_dim=args.output_dim,
+                              input_resolution=args.resolution, width=args.width, heads=args.width * 32 // 64)
+    if os.path.isfile(os.path.join("models", args.model)):
+        model = utils.load_model(args.model, dataset=args.dataset, model_type=args.model_type)
+    model.freeze_layers()
+    model.compute_dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    model.to(device)
+    ddp.broadcast_parameters(model)
+    train_dataset, test_dataset = data_preparation.get_datasets(dataset=args.dataset, size=args.dsize,
+                                                                transform=model.transform, n=args.synthetic_n,
+                                                                resolution=args.resolution)
+    sampler = None
+    if world > 1:
+        sampler = torch.utils.data.distributed.DistributedSampler(train_dataset, shuffle=True)
+    train_loader = DataLoader(train_dataset, batch_size=args.batch_size, num_workers=min(4, os.cpu_count()),
+                              shuffle=sampler is None, sampler=sampler)
+    test_loader = DataLoader(test_dataset, batch_size=args.batch_size, num_workers=min(4, os.cpu_count()),
+                             shuffle=False)
+    optimizer = optim.Adam(model.parameters(), lr=args.learning_rate, weight_decay=args.weight_decay)
+    with_classification = 'with_classification' in type(model).__name__ and 'V2' in train_dataset.state_dict['dataset']
+    loss_fn = make_loss(args.loss_type, with_classification, train_dataset.state_dict['dataset'], utils.MARGIN)
+    param_dict = {"model": args.model, "trained_layers": model.trained_layers, "dataset": args.dataset,
+                  "epochs": args.epochs, "batch_size": args.batch_size, "learning_rate": args.learning_rate,
+                  "weight_decay": args.weight_decay, "optimizer": type(optimizer).__name__,
+                  "loss_fn": type(loss_fn).__name__, "loss_margin": loss_fn.margin, "loss_type": args.loss_type,
+                  "dtype": args.dtype}
+    data_dict = train_dataset.state_dict
+    print(param_dict, flush=True)
+    print(data_dict, flush=True)
+    training_dict, inference_dict = {}, {}
+    if not args.no_training:
+        training_dict = triplet_train(model, args.epochs, train_loader, test_loader, loss_fn, optimizer,
+                                      with_classification, stale_eval=args.stale_eval)
+    rank0 = int(os.environ.get("RANK", "0")) == 0
+    if args.inference and rank0:
+        inference_dict = inference.run_inference(model, test_dataset, args.feature_folder, args.loss_type)
+        print({k: v for k, v in inference_dict.items() if k != "retrieval_samples"}, flush=True)
+    if rank0 and not args.no_save:
+        utils.save_model(model, data_dict, training_dict, param_dict, inference_dict)
+    return training_dict, inference_dict
+
+
+if __name__ == "__main__":
+    main()

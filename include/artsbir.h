@@ -146,6 +146,65 @@ int artsbir_adam_step(const void* tensors, const long long* block_table, long lo
                       float lr, float beta1, float beta2, float eps, float weight_decay, long long step,
                       void* stream);
 
+/* ---- retrieval (inference.py:30-69,94-136; utils.py:42) ---------------- */
+/* nn.PairwiseDistance(p=2, eps): out[i] = ||x1[i] - x2[i] + eps||_2 (f32), a one-row
+ * operand broadcasts.  Replaces utils.euclidean_distance. */
+int artsbir_pairwise_l2(const float* x1, long long n1, const float* x2, long long n2, int D, float eps,
+                        float* out, void* stream);
+/* sq[i] = ||x[i]||^2 (f32) and, if xc != NULL, the compute-dtype copy of x with
+ * rows zero-padded to ldc columns (the MFMA scan needs D % 64 == 0). */
+int artsbir_rows_prep(int dtype, const float* x, int n, int D, float* sq, void* xc, int ldc, void* stream);
+/* exact f64 distance to the positive (rows whose positive lies in [g_base, g_base+n_g)),
+ * else dpos taken as given (<0: no positive); rank band lo/hi = dpos^2 -/+ eps(rel). */
+int artsbir_knn_band(const float* q, const float* g, const long long* pos, long long g_base, long long n_g,
+                     const float* qsq, float gsq_max, int nq, int D, float rel, double* dpos, float* lo,
+                     float* hi, void* stream);
+int artsbir_knn_band_from_dpos(const double* dpos, const float* qsq, float gsq_max, int nq, float rel,
+                               float* lo, float* hi, void* stream);
+/* candidates per query of artsbir_knn_scan for a gallery of ng rows. */
+int artsbir_knn_candidates_per_query(int ng, int tiles_per_chunk);
+/* fused MFMA scan: per (query, gallery chunk) the 16 smallest approximate squared
+ * distances; counts of items certainly closer than the positive; queue of
+ * uncertain items (unc: [unc_cap][2] int pairs followed by one int counter). */
+int artsbir_knn_scan(int dtype, const void* qc, const void* gc, const float* qsq, const float* gsq, int nq,
+                     int ng, int D, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc,
+                     int unc_cap, float* cand_d, int* cand_i, void* stream);
+/* exact f64 top-k by (distance, index) from the candidates; flag[q] = 1 when a
+ * chunk list could have dropped a true top-k item (caller re-runs exhaustively). */
+int artsbir_knn_merge(const float* q, const float* g, int D, int nq, int nchunks, const float* cand_d,
+                      const int* cand_i, const float* qsq, float gsq_max, float rel, long long g_base, int k,
+                      long long* out_i, double* out_d, int* flag, void* stream);
+/* cnt[q] += #{uncertain g : d < dpos or (d == dpos and g_base+g < pos)} (exact f64). */
+int artsbir_knn_uncertain(const float* q, const float* g, int D, const int* unc, int unc_cap,
+                          const double* dpos, const long long* pos, long long g_base, int* cnt, void* stream);
+/* out[i] = exact f64 ||q - g_i + 1e-6|| for all i (fallback / tiny galleries). */
+int artsbir_knn_exact_all(const float* q, const float* g, int D, int n, double* out, void* stream);
+
+/* backward of artsbir_pairwise_l2 (one-row operands accumulate with atomics). */
+int artsbir_pairwise_l2_bwd(const float* x1, long long n1, const float* x2, long long n2, int D, float eps,
+                            const float* dist, const float* gout, float* d1, float* d2, void* stream);
+
+/* ---- heads and composite losses (models.py:363-379, utils.py:31-75) ---- */
+/* y = x W^T + bias (nn.Linear of the classification heads, f32). */
+int artsbir_linear_fwd(const float* x, const float* W, const float* bias, int B, int D, int C, float* y, void* stream);
+/* dx = dy W; dW += dy^T x; db += colsum(dy). */
+int artsbir_linear_bwd(const float* dy, const float* x, const float* W, int B, int D, int C, float* dx, float* dW,
+                       float* db, void* stream);
+/* nn.CrossEntropyLoss(reduction='mean', ignore_index): loss2 = {loss, #counted}; prob saved. */
+int artsbir_cross_entropy_fwd(const float* logits, const long long* labels, int B, int C, long long ignore_index,
+                              float* prob, float* loss2, void* stream);
+int artsbir_cross_entropy_bwd(const float* prob, const long long* labels, int B, int C, long long ignore_index,
+                              const float* gout, const float* loss2, float* dlogits, void* stream);
+/* nn.CosineSimilarity(dim=1, eps) of row pairs (broadcasting one-row operands). */
+int artsbir_cosine_fwd(const float* x1, long long n1, const float* x2, long long n2, int D, float eps, float* cosv,
+                       float* norms, void* stream);
+int artsbir_cosine_bwd(const float* x1, long long n1, const float* x2, long long n2, int D, const float* cosv,
+                       const float* norms, const float* gcos, float* d1, float* d2, void* stream);
+/* TripletMarginWithDistanceLoss hinge: loss = mean(max(0, margin + dp - dn)). */
+int artsbir_hinge_fwd(const float* dp, const float* dn, int B, float margin, float* loss, void* stream);
+int artsbir_hinge_bwd(const float* dp, const float* dn, int B, float margin, const float* gout, float* gdp, float* gdn,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif
