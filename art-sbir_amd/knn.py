@@ -157,13 +157,20 @@ def knn_sharded(queries, gallery_shard, g_base: int, k: int = 10, positives=None
     all_d = [torch.empty_like(dd) for _ in range(world)]
     dist.all_gather(all_i, idx)
     dist.all_gather(all_d, dd)
-    ci = torch.cat(all_i, 1)
-    cd = torch.cat(all_d, 1)
-    # order by (distance, global index): stable sort by index, then by distance
-    o1 = torch.sort(ci, dim=1, stable=True).indices
-    ci, cd = torch.gather(ci, 1, o1), torch.gather(cd, 1, o1)
-    o2 = torch.sort(cd, dim=1, stable=True).indices[:, :k]
-    out_i, out_d = torch.gather(ci, 1, o2), torch.gather(cd, 1, o2)
+    out_i, out_d = merge_topk(all_i, all_d, k)
     if rank is not None:
         dist.all_reduce(rank, op=dist.ReduceOp.SUM)
     return out_i, out_d, rank
+
+
+def merge_topk(all_i, all_d, k):
+    """Merge per-shard top-k lists ([Q, k] each) into the global top-k ordered by
+    (distance, global index); entries with index -1 (short shards) sort last."""
+    ci = torch.cat(list(all_i), 1)
+    cd = torch.cat(list(all_d), 1).clone()
+    cd[ci < 0] = float("inf")
+    # stable sort by index, then stable sort by distance == lexicographic (distance, index)
+    o1 = torch.sort(ci, dim=1, stable=True).indices
+    ci, cd = torch.gather(ci, 1, o1), torch.gather(cd, 1, o1)
+    o2 = torch.sort(cd, dim=1, stable=True).indices[:, :k]
+    return torch.gather(ci, 1, o2), torch.gather(cd, 1, o2)
