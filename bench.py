@@ -28,6 +28,18 @@ import torch.distributed as dist  # noqa: E402
 
 LAYERS, OUT_DIM, RES, WIDTH, HEADS = (3, 4, 6, 3), 512, 224, 64, 32
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+# per-launch HBM bytes of each kernel from the committed rocprofv3 PMC passes
+# (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/summarize_pmc.py)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+
+
+def pmc_traffic(kernel):
+    try:
+        with open(PMC_TRAFFIC) as f:
+            k = json.load(f)["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if k is None else round(k["hbm_bytes_per_launch"])
 
 
 def encoder_flops_per_image(layers=LAYERS, out_dim=OUT_DIM, res=RES, width=WIDTH):
@@ -64,7 +76,7 @@ def train_flops_per_triplet():
     return 3 * (3 * encoder_flops_per_image() - stem1)
 
 
-def cpu_baseline(batch=8, steps=2):
+def cpu_baseline(batch=32, steps=3):
     """The oracle (torch CPU fp32 restatement of the reference path) on the host
     cores: same model/config, a bounded sample of `batch` triplets per step."""
     from oracle import encoder as oenc, steps as osteps
@@ -84,6 +96,78 @@ def cpu_baseline(batch=8, steps=2):
                       f"{batch} triplets after 1 warm-up, torch CPU {torch.__version__} on {platform.processor() or 'x86_64'}"}
 
 
+def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
+    """BASELINE metric, second half: gallery kNN QPS at 1M x 512.
+    Synthetic gallery G ~ N(0,1); query i = G[(i*7919) mod N] + 0.5 N(0,1), so each
+    query has one planted positive.  Timed: knn.knn (or knn_sharded over the
+    ranks: gallery rows split, one all_gather + all_reduce) producing the exact
+    top-10 and the rank of the positive for all Q queries; inputs resident in HBM."""
+    import knn
+    g = torch.Generator(device=dev).manual_seed(7)
+    lo, hi = rank * N // world, (rank + 1) * N // world
+    gal = torch.randn(N, D, device=dev, generator=g)  # same full gallery on every rank (seeded)
+    pos = (torch.arange(Q, device=dev, dtype=torch.int64) * 7919) % N
+    qs = gal[pos] + 0.5 * torch.randn(Q, D, device=dev, generator=torch.Generator(device=dev).manual_seed(8))
+    shard = gal[lo:hi].contiguous()
+    del gal
+
+    def run():
+        if world > 1:
+            return knn.knn_sharded(qs, shard, lo, k, pos)
+        idx, dd, r, _ = knn.knn(qs, shard, k, pos)
+        return idx, dd, r
+
+    run()  # warm-up
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = []
+    import _hip
+    _hip.PROFILE = prof
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        idx, dd, r = run()
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    _hip.PROFILE = None
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1 in prof if kn == "knn_scan_kernel"]
+    scan_s = sum(s for _, s in scan) / len(scan)
+    scan_fl = sum(f for f, _ in scan) / len(scan)
+    rk = r.double() + 1
+    map10 = float(torch.where(rk <= k, 1.0 / rk, torch.zeros_like(rk)).mean())
+    return {"metric": "gallery kNN QPS @1M x 512 (exact top-10 + rank of positive)", "value": round(Q / el, 1),
+            "unit": "queries/s", "ms": round(el * 1e3, 3), "N": N, "D": D, "Q": Q, "k": k, "n_gpus": world,
+            "scaling": "strong", "compute": "bf16 MFMA scan + exact f64 rerank", "map@10": round(map10, 6),
+            "mrr": round(float((1.0 / rk).mean()), 6),
+            "roofline": {"bound": "mfma", "kernel": "knn_scan_kernel", "achieved": round(scan_fl / scan_s / 1e12, 2),
+                         "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
+                         "frac": round(scan_fl / scan_s / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
+                         "avg_launch_us": round(scan_s * 1e6, 2), "avg_launch_flops": scan_fl,
+                         "traffic": pmc_traffic("knn_scan_kernel")}}
+
+
+def cpu_retrieval_baseline(N=1_000_000, D=512, nq=8):
+    """reference-style per-query loop (inference.py:30-57: PairwiseDistance over the
+    whole gallery + full sort + position of the positive) via the oracle's float64
+    restatement on the host cores, on nq queries of the C4 workload, as queries/s."""
+    import numpy as np
+    from oracle import retrieval as oret
+    g, qs, pos = oret.synthetic_gallery(N, D, nq)
+    t0 = time.perf_counter()
+    for i in range(nq):
+        d = oret.l2_distances(qs[i], g)
+        o = oret.order(d)
+        int(np.nonzero(o == pos[i])[0][0])
+    dt = time.perf_counter() - t0
+    return {"value": round(nq / dt, 3), "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"{nq} queries x full {N}x{D} gallery, oracle/retrieval.py float64 distances + stable argsort "
+                      "(numpy, single-threaded), per-query like the reference"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +177,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-launch event timing")
+    ap.add_argument("--no-retrieval", action="store_true", help="skip the 1M x 512 kNN leg")
     args = ap.parse_args()
 
     import _hip
@@ -177,7 +262,8 @@ def main():
             peak = MFMA_PEAK_TFLOPS[args.dtype]
             achieved = fl / secs / 1e12
             roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": None, "kernel": dom, "launches": cnt,
+                    "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom),
+                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT), "kernel": dom, "launches": cnt,
                     "avg_launch_us": round(secs / cnt * 1e6, 2), "avg_launch_flops": fl / cnt,
                     "per_kernel": {k: {"launches": v[2], "avg_us": round(v[1] / v[2] * 1e6, 2),
                                        "tflops": round(v[0] / v[1] / 1e12, 1), "share_s": round(v[1], 4)}
@@ -197,8 +283,14 @@ def main():
             "loss": last_loss,
             "roofline": roof,
         }
+    ret = None if args.no_retrieval else retrieval_leg(dev, rank, world)
+    if rank == 0:
+        if ret is not None:
+            line["retrieval"] = ret
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
+            if ret is not None:
+                ret["cpu_baseline"] = cpu_retrieval_baseline()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
