@@ -49,6 +49,7 @@ _PB = ctypes.POINTER(BnBwdDesc)
 SIGNATURES = {
     "artsbir_version": [],
     "artsbir_last_error": [],
+    "artsbir_last_kernel": [],
     "artsbir_conv2d_fwd": [_P, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_conv2d_wgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_gemm_nt": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
@@ -96,7 +97,7 @@ SIGNATURES = {
     "artsbir_hinge_fwd": [_vp, _vp, _c_int, _c_float, _vp, _vp],
     "artsbir_hinge_bwd": [_vp, _vp, _c_int, _c_float, _vp, _vp, _vp, _vp],
 }
-_RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll,
+_RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_last_kernel": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll,
              "artsbir_knn_candidates_per_query": _c_int}
 
 _lib = None
@@ -138,22 +139,14 @@ def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes
         e0.record()
         rc = getattr(lib(), name)(*args)
         e1.record()
+        if kernel == "auto":  # the variant the library chose for this call
+            kernel = lib().artsbir_last_kernel().decode()
         prof.append((kernel, flops, nbytes, e0, e1))
     else:
         rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().artsbir_last_error().decode(errors="replace")
         raise HipError(f"{name} failed ({rc}): {msg}")
-
-
-def conv_kernel_name(dtype_code: int, cout: int) -> str:
-    """kernel template artsbir_conv2d_fwd / _dgrad / gemm_nt launch for this width"""
-    t = "bf16" if dtype_code == DT_BF16 else "f32"
-    return f"conv_gemm_kernel<{t},128,{64 if cout <= 64 else 128}>"
-
-
-def wgrad_kernel_name(dtype_code: int) -> str:
-    return f"wgrad_kernel<{'bf16' if dtype_code == DT_BF16 else 'f32'},128,128>"
 
 
 def ptr(t) -> int | None:

@@ -13,7 +13,10 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
+static thread_local const char* g_kernel = "";
+void set_last_kernel(const char* name) { g_kernel = name; }
 }  // namespace artsbir
 
 extern "C" const char* artsbir_last_error(void) { return artsbir::g_err; }
+extern "C" const char* artsbir_last_kernel(void) { return artsbir::g_kernel; }
 extern "C" int artsbir_version(void) { return 1; }

@@ -26,6 +26,8 @@ namespace artsbir {
 
 // error reporting (defined in capi.cpp)
 void set_error(const char* fmt, ...);
+// name of the GEMM kernel the last conv / gemm entry point launched (profiling)
+void set_last_kernel(const char* name);
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }

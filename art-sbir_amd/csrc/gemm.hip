@@ -28,7 +28,13 @@
 // (pixel offset + one validity bit per filter tap); per K-step only the tap
 // (r, s, ci) changes, and when C is a multiple of the K-step it is uniform
 // across the workgroup (scalar arithmetic).
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "common.h"
+#include "pgemm.h"
 
 namespace artsbir {
 
@@ -666,10 +672,120 @@ static void launch_conv_tile(const ConvArgs& a, hipStream_t st) {
 }
 
 template <typename T>
+static void launch_conv_old(const ConvArgs& a, hipStream_t st) {
+  const bool bf = sizeof(T) == 2;
+  if (a.Cout <= 64) {
+    set_last_kernel(bf ? "conv_gemm_kernel<bf16,128,64>" : "conv_gemm_kernel<f32,128,64>");
+    launch_conv_tile<T, 128, 64>(a, st);
+  } else {
+    set_last_kernel(bf ? "conv_gemm_kernel<bf16,128,128>" : "conv_gemm_kernel<f32,128,128>");
+    launch_conv_tile<T, 128, 128>(a, st);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Kernel choice per convolution shape (bf16): the register-staged kernel
+// above (-2), the pipelined LDS-DMA kernel's tile shapes (0..4) or the
+// persistent streaming kernel (10), pgemm.hip.  By default the first call of
+// a new shape times every applicable candidate on the caller's stream (output
+// written to the real buffers, BN statistics to a scratch buffer) and caches
+// the fastest, like a "find" step; ARTSBIR_TUNE=0 uses the static heuristic,
+// ARTSBIR_PGEMM_CFG=<c> forces candidate c (tests).
+// ---------------------------------------------------------------------------
+struct ConvKey {
+  long long M;
+  int H, W, C, Cout, R, S, stride, pad, Ho, Wo, res_mode, stats;
+  bool operator<(const ConvKey& o) const {
+    return std::tie(M, H, W, C, Cout, R, S, stride, pad, Ho, Wo, res_mode, stats) <
+           std::tie(o.M, o.H, o.W, o.C, o.Cout, o.R, o.S, o.stride, o.pad, o.Ho, o.Wo, o.res_mode, o.stats);
+  }
+};
+static std::map<ConvKey, int> g_conv_choice;
+static std::mutex g_tune_mu;
+static float* g_tune_stats = nullptr;
+static size_t g_tune_stats_n = 0;
+
+static bool run_candidate(int c, const ConvArgs& a, const PgArgs& p, hipStream_t st) {
+  if (c == -2) { launch_conv_old<bf16>(a, st); return true; }
+  return pgemm_launch_cfg(p, c, st);
+}
+
+static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
+  const size_t need = (size_t)ARTSBIR_NSLOT * 2 * a.Cout;
+  if (a.stats && need > g_tune_stats_n) {
+    if (g_tune_stats) hipFree(g_tune_stats);
+    g_tune_stats = nullptr;
+    g_tune_stats_n = 0;
+    if (hipMalloc(&g_tune_stats, need * sizeof(float)) != hipSuccess) return pgemm_default_cfg(p);
+    g_tune_stats_n = need;
+  }
+  ConvArgs at = a;
+  PgArgs pt = p;
+  if (a.stats) { at.stats = g_tune_stats; pt.stats = g_tune_stats; }
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  static const int cands[] = {-2, 0, 1, 2, 3, 4, 10};
+  int best = -2;
+  float best_ms = 1e30f;
+  for (int c : cands) {
+    if (!run_candidate(c, at, pt, st)) continue;  // also the warm-up
+    float ms = 1e30f;
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(e0, st);
+      run_candidate(c, at, pt, st);
+      hipEventRecord(e1, st);
+      hipEventSynchronize(e1);
+      float t = 0.f;
+      hipEventElapsedTime(&t, e0, e1);
+      if (t < ms) ms = t;
+    }
+    if (ms < best_ms) { best_ms = ms; best = c; }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return best;
+}
+
+template <typename T>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
   if ((long long)a.Cout * a.K * sizeof(T) > 0x7fffffffLL) { set_error("conv: weight tensor too large"); return -1; }
-  if (a.Cout <= 64) launch_conv_tile<T, 128, 64>(a, st);
-  else launch_conv_tile<T, 128, 128>(a, st);
+  if (sizeof(T) == 2 && !a.out_f32 && !a.accumulate && !a.bias && !a.in_scale) {
+    PgArgs p;
+    p.x = a.x; p.x_elems = a.x_elems; p.sN = a.sN; p.sH = a.sH; p.sW = a.sW;
+    p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
+    p.Ho = a.Ho; p.Wo = a.Wo; p.w = a.w; p.Cout = a.Cout; p.K = a.K; p.M = a.M;
+    p.y = a.y; p.ldy = a.ldy; p.stats = a.stats; p.res = a.res; p.res_mode = a.res_mode; p.dbg = 0;
+    int choice;
+    const char* force = getenv("ARTSBIR_PGEMM_CFG");
+    if (force) {
+      choice = atoi(force);
+    } else {
+      const ConvKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.Ho, a.Wo, a.res_mode,
+                        a.stats ? 1 : 0};
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      auto it = g_conv_choice.find(key);
+      if (it != g_conv_choice.end()) {
+        choice = it->second;
+      } else {
+        const char* tune = getenv("ARTSBIR_TUNE");
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        hipStreamIsCapturing(st, &cs);
+        if ((tune && atoi(tune) == 0) || cs != hipStreamCaptureStatusNone) {
+          choice = pgemm_default_cfg(p);
+          if (choice < 0) choice = -2;
+        } else {
+          choice = tune_conv(a, p, st);
+        }
+        g_conv_choice[key] = choice;
+      }
+    }
+    if (choice != -2 && pgemm_launch_cfg(p, choice, st)) {
+      ARTSBIR_CHECK_LAUNCH("pgemm");
+      return 0;
+    }
+  }
+  launch_conv_old<T>(a, st);
   ARTSBIR_CHECK_LAUNCH("conv_gemm");
   return 0;
 }
@@ -784,8 +900,14 @@ static void launch_wgrad_tile(WgradArgs& a, hipStream_t st) {
 
 template <typename T>
 static int launch_wgrad(WgradArgs& a, hipStream_t st) {
-  if (a.Cout <= 64) launch_wgrad_tile<T, 64, 128>(a, st);
-  else launch_wgrad_tile<T, 128, 128>(a, st);
+  const bool bf = sizeof(T) == 2;
+  if (a.Cout <= 64) {
+    set_last_kernel(bf ? "wgrad_kernel<bf16,64,128>" : "wgrad_kernel<f32,64,128>");
+    launch_wgrad_tile<T, 64, 128>(a, st);
+  } else {
+    set_last_kernel(bf ? "wgrad_kernel<bf16,128,128>" : "wgrad_kernel<f32,128,128>");
+    launch_wgrad_tile<T, 128, 128>(a, st);
+  }
   ARTSBIR_CHECK_LAUNCH("wgrad");
   return 0;
 }

@@ -1,0 +1,662 @@
+// Pipelined implicit-GEMM convolution (bf16 in, f32 accumulate, bf16 out) for
+// gfx950: conv forward and conv data-gradient of the encoder
+// (models.py:198-221 Bottleneck convs, models.py:310-316 stem).
+//
+// Structure (cdna_hip_programming.md §5, "glds" rows):
+//  * the output tile is computed transposed, out^T[channel][pixel], so that an
+//    MFMA accumulator lane holds 4 consecutive channels of one pixel; with the
+//    channel order inside the tile permuted (below) a lane holds 8 consecutive
+//    channels across two 16-row MFMA tiles and the epilogue stores 16-B bf16
+//    vectors straight from registers (no LDS staging, BN statistics from the
+//    f32 accumulators);
+//  * both operands are staged by LDS-DMA (buffer_load ... lds, 16 B per lane):
+//    one wave instruction fills 8 rows x 128 B (8 lanes per row = one full
+//    128-B line of k), the LDS image of a row is its 8 k-chunks in slot order
+//    chunk ^ (row & 7) (the XOR swizzle is applied to the per-lane SOURCE
+//    address; the LDS destination stays lane-linear), which makes the MFMA
+//    fragment reads (16 rows x one chunk per ds_read_b128) conflict-free;
+//  * an NSTAGE ring of LDS stages, one raw s_barrier per K-step, counted
+//    s_waitcnt vmcnt so that NSTAGE-2 stages stay in flight across the barrier;
+//  * implicit im2col: per pixel row a tap-validity mask; out-of-range (padding,
+//    tails) source offsets are 0x80000000, which the buffer unit turns into
+//    zeros written to LDS.
+#include <cstdlib>
+
+#include "common.h"
+#include "pgemm.h"
+
+namespace artsbir {
+
+#define PG_OOB 0x80000000u
+typedef __attribute__((address_space(3))) void* pg_lds_t;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pg_rsrc(const void* base, long long bytes) {
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  if (bytes < 0) bytes = 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// LDS-DMA of 16 B per lane to lds + 16 * lane.  Inline asm on purpose: hipcc
+// does not track it, so it neither drains it with vmcnt(0) before every
+// ds_read nor at barriers; completion is counted by hand (vm_wait below).
+// M0 is written and restored inside the statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(pg_lds_t)lds);
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(base), "s"(r)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until at most `ahead` stages of this wave's loads are outstanding
+template <int LPS, int NSTAGE>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  if constexpr (NSTAGE >= 4) {
+    if (ahead >= 2) { vm_wait<2 * LPS>(); return; }
+  }
+  if constexpr (NSTAGE >= 3) {
+    if (ahead >= 1) { vm_wait<LPS>(); return; }
+  }
+  vm_wait<0>();
+}
+
+__device__ __forceinline__ long long pg_xcd_remap(long long bid, long long nwg) {
+  if (nwg < 8) return bid;
+  const long long q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// channel held by LDS weight row rho of a tile (rho = 16 i + 4 q + r  ->
+// 32 (i >> 1) + 8 q + 4 (i & 1) + r): MFMA output lane q then owns 8
+// consecutive channels of each 32-channel pair of 16-row tiles.
+__device__ __forceinline__ int pg_perm(int rho) {
+  return 32 * (rho >> 5) + 8 * ((rho >> 2) & 3) + 4 * ((rho >> 4) & 1) + (rho & 3);
+}
+
+// Sum each of 16 per-lane values (s1[0..8), s2[0..8)) over the 16 lanes of a
+// DPP row (lanes with the same lane >> 4) with 4 row_shr DPP adds per value
+// (VALU only, no LDS round trips); the row totals end in lane 15 of the row.
+__device__ __forceinline__ float dpp_row_sum(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x112, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x114, 0xf, 0xf, true));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x118, 0xf, 0xf, true));
+  return x;
+}
+
+// Block-level BN statistics: every compute wave adds its reduce16 result into
+// an LDS accumulator red[2][BCH] (ds_add_f32); the last wave of the tile (LDS
+// counter) flushes it with 2*BCH global atomics into the replica slot and
+// zeroes it.  Cuts global atomics by the number of waves sharing a channel.
+template <int BCH>
+__device__ __forceinline__ void stats_flush(float* red, int* cnt, int last_count, const PgArgs& a, int bch, int slot,
+                                            int lane) {
+  // LDS operations of one wave complete in order; the wait makes this wave's
+  // adds land before its counter increment (no global-memory fence needed)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  int old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = __shfl(old, 0, 64);
+  if (old != last_count) return;
+  asm volatile("" ::: "memory");
+  float* sp = a.stats + (long long)slot * 2 * a.Cout;
+  for (int i = lane; i < 2 * BCH; i += 64) {
+    const int m = i >= BCH ? 1 : 0;
+    const int ch = bch + i - m * BCH;
+    const float v = red[i];
+    red[i] = 0.f;
+    if (ch < a.Cout) atomicAdd(sp + m * a.Cout + ch, v);
+  }
+}
+
+template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI>
+__global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
+  constexpr int NW = WPX * WCH;
+  constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
+  constexpr int IPX = BPX / (8 * NW);
+  constexpr int ICH_TOT = BCH / 8;
+  constexpr int ICH = (ICH_TOT + NW - 1) / NW;
+  constexpr int WTPX = BPX / WPX, WTCH = BCH / WCH;
+  constexpr int NTP = WTPX / 16, MTC = WTCH / 16;
+  constexpr int LPS_HI = IPX + ICH;                            // loads per stage, waves with ICH weight loads
+  constexpr int LPS_LO = IPX + ICH_TOT / NW;                   // ... waves with one fewer
+  static_assert(IPX >= 1 && IPX * 8 * NW == BPX, "pixel loader");
+  static_assert(MTC % 2 == 0 && WTCH % 32 == 0, "channel pairs");
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + 2 * BCH * 4 + 16];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 2 * BCH * 4);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wpx = wid % WPX, wch = wid / WPX;
+  const int ntc = (a.Cout + BCH - 1) / BCH;
+  const long long ntp = (a.M + BPX - 1) / BPX;
+  const long long lid = pg_xcd_remap(blockIdx.x, ntp * ntc);
+  const long long bpx = (lid / ntc) * BPX;
+  const int bch = (int)(lid % ntc) * BCH;
+  const int HoWo = a.Ho * a.Wo;
+  const long long img0 = bpx / HoWo;
+  const __amdgpu_buffer_rsrc_t xr =
+      pg_rsrc(reinterpret_cast<const bf16*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * 2);
+  const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
+
+  // ---- loader decode: this lane fills slot (lane & 7) of row (lane >> 3)
+  // of each 8-row wave instruction, with k-chunk csrc = slot ^ (row & 7)
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const int csrc = lslot ^ lrow;
+  int rowoff[IPX];
+  unsigned rmask[IPX];
+#pragma unroll
+  for (int u = 0; u < IPX; ++u) {
+    const int row = (u * NW + wid) * 8 + lrow;
+    const long long gm = bpx + row;
+    const bool valid = gm < a.M;
+    const long long gmc = valid ? gm : bpx;
+    const long long img = gmc / HoWo;
+    const int rem = (int)(gmc - img * HoWo);
+    const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2);
+    unsigned msk = 0;
+    for (int r = 0; r < a.R; ++r)
+      for (int s = 0; s < a.S; ++s) {
+        const bool ok = valid && ih0 + r >= 0 && ih0 + r < a.H && iw0 + s >= 0 && iw0 + s < a.W;
+        msk |= (ok ? 1u : 0u) << (r * a.S + s);
+      }
+    rmask[u] = msk;
+  }
+  unsigned woff[ICH];
+#pragma unroll
+  for (int u = 0; u < ICH; ++u) {
+    const int g = u * NW + wid;
+    const int ch = bch + pg_perm(g * 8 + lrow);
+    woff[u] = (g < ICH_TOT && ch < a.Cout) ? (unsigned)(ch * a.K * 2 + csrc * 16) : PG_OOB;
+  }
+  const bool lps_hi = (ICH - 1) * NW + wid < ICH_TOT;
+
+  int u_ci = 0, u_s = 0, u_r = 0;  // uniform-tap walk (C % 64 == 0)
+  auto issue = [&](int kt, int buf) {
+    char* pxs = smem + buf * STAGE;
+    char* chs = pxs + PXB;
+    int rs, tapoff;
+    bool kval;
+    if constexpr (!MULTI) {
+      rs = u_r * a.S + u_s;
+      tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + u_ci + csrc * 8) * 2;
+      kval = true;
+      u_ci += 64;
+      if (u_ci == a.C) {
+        u_ci = 0;
+        if (++u_s == a.S) { u_s = 0; ++u_r; }
+      }
+    } else {
+      const int cpt = a.C >> 3;  // 16-B chunks per tap: 1, 2 or 4
+      const int sub = csrc / cpt;
+      const int ci = (csrc - sub * cpt) * 8;
+      rs = kt * (64 / a.C) + sub;
+      kval = rs < a.R * a.S;
+      const int r = rs / a.S, s = rs - (rs / a.S) * a.S;
+      tapoff = (r * (int)a.sH + s * (int)a.sW + ci) * 2;
+    }
+#pragma unroll
+    for (int u = 0; u < IPX; ++u) {
+      const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
+      glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+    }
+    const bool wk = kt * 64 + csrc * 8 < a.K;
+#pragma unroll
+    for (int u = 0; u < ICH; ++u) {
+      if (u * NW + wid < ICH_TOT)
+        glds16(wr, chs + (u * NW + wid) * 1024, (wk && woff[u] != PG_OOB) ? woff[u] + kt * 128 : PG_OOB);
+    }
+  };
+
+  f32x4 acc[MTC][NTP];
+#pragma unroll
+  for (int i = 0; i < MTC; ++i)
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* pxs = smem + buf * STAGE;
+    const char* chs = pxs + PXB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int so = ((kk * 4 + fq) ^ (fr & 7)) << 4;
+      uint4 af[MTC], bv[NTP];
+#pragma unroll
+      for (int i = 0; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * 128 + so);
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * 128 + so);
+#pragma unroll
+      for (int i = 0; i < MTC; ++i)
+#pragma unroll
+        for (int j = 0; j < NTP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
+                                                              *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j], 0,
+                                                              0, 0);
+    }
+  };
+
+  if (a.stats) {
+    for (int i = tid; i < 2 * BCH; i += 64 * NW) red[i] = 0.f;
+    if (tid == 0) *red_cnt = 0;
+  }
+  const int nk = (a.K + 63) / 64;
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    int ahead = nk - 1 - kt;
+    if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
+    if (lps_hi) wait_stages<LPS_HI, NSTAGE>(ahead);
+    else wait_stages<LPS_LO, NSTAGE>(ahead);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    compute(kt % NSTAGE);
+  }
+
+  // ---- epilogue from registers: lane (fr, fq) holds, per channel pair p and
+  // pixel tile j, channels ch0..ch0+7 of pixel px
+  const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
+#pragma unroll
+  for (int p = 0; p < MTC / 2; ++p) {
+    const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+    const bool chok = ch0 < a.Cout;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const long long px = bpx + wpx * WTPX + j * 16 + fr;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+      if (px < a.M && chok) {
+        if (a.stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+        }
+        if (a.res_mode) {
+          long long ri = px;
+          float sc = 1.f;
+          if (a.res_mode == 2) {
+            const long long img = px / HoWo;
+            const int rem = (int)(px - img * HoWo);
+            const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+            ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+            sc = 0.25f;
+          }
+          const Vec16<bf16> rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + ch0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += sc * to_f(rv.v[e]);
+        }
+        Vec16<bf16> o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+        st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+      }
+    }
+    if (a.stats) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
+      if (fr == 15 && chok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(red + (ch0 - bch) + e, s1[e]);
+          atomicAdd(red + BCH + (ch0 - bch) + e, s2[e]);
+        }
+      }
+    }
+  }
+  if (a.stats) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Persistent producer/consumer variant for layers with many 256-pixel tiles
+// (stem, layer1-3, low K).  4 loader waves only issue LDS-DMA, so their vmcnt
+// counts exactly their own loads; 8 compute waves only read LDS, run MFMAs and
+// store.  One s_barrier per stage hands a landed stage to the compute waves
+// and the slot they just drained back to the loaders.  The stage sequence runs
+// across tile boundaries: the next tile's loads are in flight while this
+// tile's epilogue stores drain, which is what the low-K layers (1-5 K-steps
+// per tile) need to stream at HBM rate.
+// ---------------------------------------------------------------------------
+template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI>
+__global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
+  constexpr int BPX = 256, NWC = 8, NWL = 4;
+  static_assert(WPX * WCH == NWC, "compute waves");
+  constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
+  constexpr int LPX = BPX / (8 * NWL);
+  constexpr int LCH = BCH / (8 * NWL);
+  constexpr int LPS = LPX + LCH;
+  constexpr int WTPX = BPX / WPX, WTCH = BCH / WCH;
+  constexpr int NTP = WTPX / 16, MTC = WTCH / 16;
+  static_assert(LCH >= 1 && MTC % 2 == 0, "shape");
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + 2 * BCH * 4 + 16];
+  float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
+  int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 2 * BCH * 4);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntc = (a.Cout + BCH - 1) / BCH;
+  const int G = gridDim.x;
+  const int bslot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int my_tiles = bslot < ntiles ? (ntiles - 1 - bslot) / G + 1 : 0;
+  const int nk = (a.K + 63) / 64;
+  const int total = my_tiles * nk;
+  const int HoWo = a.Ho * a.Wo;
+
+  if (wid >= NWC) {
+    // ------------------------------------------------------------ loaders
+    const int lw = wid - NWC;
+    const int lrow = lane >> 3, lslot = lane & 7;
+    const int csrc = lslot ^ lrow;
+    const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
+    __amdgpu_buffer_rsrc_t xr = wr;
+    int rowoff[LPX];
+    unsigned rmask[LPX];
+    unsigned woff[LCH];
+    int u_ci = 0, u_s = 0, u_r = 0;
+    auto start_tile = [&](int i) {
+      const long long t = (long long)i * G + bslot;
+      const long long bpx = (t / ntc) * BPX;
+      const int bch = (int)(t % ntc) * BCH;
+      const long long img0 = bpx / HoWo;
+      xr = pg_rsrc(reinterpret_cast<const bf16*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * 2);
+#pragma unroll
+      for (int u = 0; u < LPX; ++u) {
+        const int row = (u * NWL + lw) * 8 + lrow;
+        const long long gm = bpx + row;
+        const bool valid = gm < a.M;
+        const long long gmc = valid ? gm : bpx;
+        const long long img = gmc / HoWo;
+        const int rem = (int)(gmc - img * HoWo);
+        const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+        const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+        rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2);
+        unsigned msk = 0;
+        for (int r = 0; r < a.R; ++r)
+          for (int s = 0; s < a.S; ++s) {
+            const bool ok = valid && ih0 + r >= 0 && ih0 + r < a.H && iw0 + s >= 0 && iw0 + s < a.W;
+            msk |= (ok ? 1u : 0u) << (r * a.S + s);
+          }
+        rmask[u] = msk;
+      }
+#pragma unroll
+      for (int u = 0; u < LCH; ++u) {
+        const int ch = bch + pg_perm((u * NWL + lw) * 8 + lrow);
+        woff[u] = ch < a.Cout ? (unsigned)(ch * a.K * 2 + csrc * 16) : PG_OOB;
+      }
+      u_ci = 0; u_s = 0; u_r = 0;
+    };
+    auto issue = [&](int sidx) {
+      const int i = sidx / nk, kt = sidx - i * nk;
+      if (kt == 0) start_tile(i);
+      char* pxs = smem + (sidx % NSTAGE) * STAGE;
+      char* chs = pxs + PXB;
+      int rs, tapoff;
+      bool kval;
+      if constexpr (!MULTI) {
+        rs = u_r * a.S + u_s;
+        tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + u_ci + csrc * 8) * 2;
+        kval = true;
+        u_ci += 64;
+        if (u_ci == a.C) {
+          u_ci = 0;
+          if (++u_s == a.S) { u_s = 0; ++u_r; }
+        }
+      } else {
+        const int cpt = a.C >> 3;
+        const int sub = csrc / cpt;
+        const int ci = (csrc - sub * cpt) * 8;
+        rs = kt * (64 / a.C) + sub;
+        kval = rs < a.R * a.S;
+        const int r = rs / a.S, s = rs - (rs / a.S) * a.S;
+        tapoff = (r * (int)a.sH + s * (int)a.sW + ci) * 2;
+      }
+#pragma unroll
+      for (int u = 0; u < LPX; ++u) {
+        const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
+        glds16(xr, pxs + (u * NWL + lw) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+      }
+      const bool wk = kt * 64 + csrc * 8 < a.K;
+#pragma unroll
+      for (int u = 0; u < LCH; ++u)
+        glds16(wr, chs + (u * NWL + lw) * 1024, (wk && woff[u] != PG_OOB) ? woff[u] + kt * 128 : PG_OOB);
+    };
+    for (int s = 0; s < NSTAGE - 1; ++s)
+      if (s < total) issue(s);
+    if (total > 0) {
+      int ahead = total - 1;
+      if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
+      wait_stages<LPS, NSTAGE>(ahead);
+    }
+    for (int s = 0; s < total; ++s) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);
+      if (s + 1 < total) {
+        int ahead = total - 2 - s;
+        if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
+        wait_stages<LPS, NSTAGE>(ahead);
+      }
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------- compute
+  if (a.stats) {  // ordered before any use by the first stage barrier
+    for (int i = tid; i < 2 * BCH; i += 64 * NWC) red[i] = 0.f;
+    if (tid == 0) *red_cnt = 0;
+  }
+  const int wpx = wid % WPX, wch = wid / WPX;
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[MTC][NTP];
+#pragma unroll
+  for (int i = 0; i < MTC; ++i)
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < total; ++s) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    {
+      const char* pxs = smem + (s % NSTAGE) * STAGE;
+      const char* chs = pxs + PXB;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int so = ((kk * 4 + fq) ^ (fr & 7)) << 4;
+        uint4 af[MTC], bv[NTP];
+#pragma unroll
+        for (int i = 0; i < MTC; ++i)
+          af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * 128 + so);
+#pragma unroll
+        for (int j = 0; j < NTP; ++j)
+          bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * 128 + so);
+#pragma unroll
+        for (int i = 0; i < MTC; ++i)
+#pragma unroll
+          for (int j = 0; j < NTP; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
+                                                                *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j],
+                                                                0, 0, 0);
+      }
+    }
+    const int ti = s / nk;
+    if (s - ti * nk != nk - 1) continue;
+    // ---- epilogue of tile ti
+    const long long t = (long long)ti * G + bslot;
+    const long long bpx = (t / ntc) * BPX;
+    const int bch = (int)(t % ntc) * BCH;
+    const int slot = (int)(t % ARTSBIR_NSLOT);
+#pragma unroll
+    for (int p = 0; p < MTC / 2; ++p) {
+      const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+      const bool chok = ch0 < a.Cout;
+      float s1[8], s2[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) {
+        const long long px = bpx + wpx * WTPX + j * 16 + fr;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+        if (px < a.M && chok) {
+          if (a.stats) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+          }
+          if (a.res_mode) {
+            long long ri = px;
+            float sc = 1.f;
+            if (a.res_mode == 2) {
+              const long long img = px / HoWo;
+              const int rem = (int)(px - img * HoWo);
+              const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+              ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+              sc = 0.25f;
+            }
+            const Vec16<bf16> rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + ch0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += sc * to_f(rv.v[e]);
+          }
+          Vec16<bf16> o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+          st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+        }
+      }
+      if (a.stats) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
+        if (fr == 15 && chok) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            atomicAdd(red + (ch0 - bch) + e, s1[e]);
+            atomicAdd(red + BCH + (ch0 - bch) + e, s2[e]);
+          }
+        }
+      }
+    }
+    // the flushing wave zeroes red before it reaches the next stage barrier,
+    // and no wave adds for tile ti+1 before passing that barrier
+    if (a.stats) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane);
+#pragma unroll
+    for (int i = 0; i < MTC; ++i)
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launch: pick the tile shape with the best (tile utilisation x CU fill)
+// ---------------------------------------------------------------------------
+struct PgCfg {
+  int bpx, bch, lds, threads;
+  float factor;
+};
+static const PgCfg kCfgs[] = {
+    {256, 256, 2 * 256 * 256, 512, 1.00f},          // 0: 256 x 256, 2 stages
+    {256, 128, 3 * (256 + 128) * 128, 512, 0.95f},  // 1: 256 x 128, 3 stages
+    {256, 64, 3 * (256 + 64) * 128, 512, 0.85f},    // 2: 256 x 64, 3 stages
+    {128, 128, 2 * 256 * 128, 256, 0.80f},          // 3: 128 x 128, 2 stages, 4 waves
+    {256, 32, 4 * (256 + 32) * 128, 512, 0.70f},    // 4: 256 x 32, 4 stages
+};
+
+template <bool MULTI>
+static void pg_launch_cfg(int c, const PgArgs& a, long long tiles, hipStream_t st) {
+  switch (c) {
+    case 0: hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 2, 2, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, MULTI>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
+  }
+}
+
+static bool pg_supported(const PgArgs& a, bool& multi) {
+  if (a.Cout % 32 != 0 || a.M <= 0) return false;
+  if (a.C % 64 == 0) multi = false;
+  else if (a.C == 8 || a.C == 16 || a.C == 32) multi = true;
+  else return false;
+  if (a.R * a.S > 32 || a.K % 8 != 0) return false;
+  if ((long long)a.Cout * a.K * 2 > 0x7fffffffLL) return false;
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 > 0x7fffffffLL) return false;
+  if (a.M > (1LL << 40)) return false;
+  return true;
+}
+
+// candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
+bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
+  bool multi;
+  if (!pg_supported(a, multi)) return false;
+  if (c == 10) {
+    const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
+    const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);
+    if (nt > 0x7fffffffLL) return false;
+    const int grid = (int)(nt < 256 ? nt : 256);
+    const int ntl = (int)nt;
+    set_last_kernel(bch == 32 ? "pstream_kernel<32>" : bch == 64 ? "pstream_kernel<64>" : "pstream_kernel<128>");
+    if (bch == 32) {
+      if (multi) hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, true>), dim3(grid), dim3(768), 0, st, a, ntl);
+      else hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, false>), dim3(grid), dim3(768), 0, st, a, ntl);
+    } else if (bch == 64) {
+      if (multi) hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, true>), dim3(grid), dim3(768), 0, st, a, ntl);
+      else hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false>), dim3(grid), dim3(768), 0, st, a, ntl);
+    } else {
+      if (multi) hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, true>), dim3(grid), dim3(768), 0, st, a, ntl);
+      else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, false>), dim3(grid), dim3(768), 0, st, a, ntl);
+    }
+    return true;
+  }
+  if (c < 0 || c > 4) return false;
+  const PgCfg& g = kCfgs[c];
+  const long long tiles = ((a.M + g.bpx - 1) / g.bpx) * ((a.Cout + g.bch - 1) / g.bch);
+  if (tiles > 0x7fffffffLL) return false;
+  static const char* names[] = {"pgemm_kernel<256,256>", "pgemm_kernel<256,128>", "pgemm_kernel<256,64>",
+                                "pgemm_kernel<128,128>", "pgemm_kernel<256,32>"};
+  set_last_kernel(names[c]);
+  if (multi) pg_launch_cfg<true>(c, a, tiles, st);
+  else pg_launch_cfg<false>(c, a, tiles, st);
+  return true;
+}
+
+// static choice (no tuning): streaming kernel for many tiles, else best-scored tile
+int pgemm_default_cfg(const PgArgs& a) {
+  bool multi;
+  if (!pg_supported(a, multi)) return -1;
+  const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
+  if (((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch) >= 4 * 256) return 10;
+  int best = -1;
+  float best_score = -1.f;
+  for (int c = 0; c < 5; ++c) {
+    const PgCfg& g = kCfgs[c];
+    const long long tiles = ((a.M + g.bpx - 1) / g.bpx) * ((a.Cout + g.bch - 1) / g.bch);
+    const double util = (double)a.M * a.Cout / ((double)tiles * g.bpx * g.bch);
+    const int per_cu = (160 * 1024) / g.lds;
+    const long long slots = 256LL * (per_cu < 1 ? 1 : per_cu);
+    const long long waves = (tiles + slots - 1) / slots;
+    const double fill = (double)tiles / (double)(waves * slots);
+    const float score = (float)(g.factor * util * fill);
+    if (score > best_score) { best_score = score; best = c; }
+  }
+  return best;
+}
+
+}  // namespace artsbir

@@ -169,11 +169,11 @@ class Engine:
     # ------------------------------------------------------------- primitives
     def _gemm_nt(self, M, N, K, a, lda, b, c, ldc, out_f32, acc, bias):
         call("artsbir_gemm_nt", self.dt, M, N, K, ptr(a), lda, ptr(b), ptr(c), ldc, out_f32, acc, ptr(bias), None,
-             _s(), kernel=_hip.conv_kernel_name(self.dt, N), flops=2.0 * M * N * K)
+             _s(), kernel="auto", flops=2.0 * M * N * K)
 
     def _gemm_tn(self, M, N, K, dy, ldd, x, ldx, dw):
         call("artsbir_gemm_tn", self.dt, M, N, K, ptr(dy), ldd, ptr(x), ldx, ptr(dw), _s(),
-             kernel=_hip.wgrad_kernel_name(self.dt), flops=2.0 * M * N * K)
+             kernel="auto", flops=2.0 * M * N * K)
 
     def _conv(self, a: Act, fw, cout, R, S, stride, pad, stats_buf=None):
         B, H, W, C = a.shape
@@ -184,7 +184,7 @@ class Engine:
         bn = a.bn
         call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None,
              ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None, a.relu,
-             ptr(stats_buf), _s(), kernel=_hip.conv_kernel_name(self.dt, cout),
+             ptr(stats_buf), _s(), kernel="auto",
              flops=2.0 * B * Ho * Wo * cout * R * S * C)
         return y
 
@@ -412,7 +412,7 @@ class Engine:
             target = torch.zeros(co, R, S, C, dtype=torch.float32, device=dy.device)
         Ho, Wo = dy.shape[1], dy.shape[2]
         call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), ptr(bn.scale) if bn else None,
-             ptr(bn.shift) if bn else None, a.relu, ptr(target), _s(), kernel=_hip.wgrad_kernel_name(self.dt),
+             ptr(bn.shift) if bn else None, a.relu, ptr(target), _s(), kernel="auto",
              flops=2.0 * B * Ho * Wo * co * R * S * C)
         if target is not g:
             call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
@@ -423,7 +423,7 @@ class Engine:
         dx = self._empty(B, H, W, C, device=dy.device)
         d = self._desc(B, H, W, C, co, R, S, 1, pad)
         call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
-             kernel=_hip.conv_kernel_name(self.dt, C), flops=2.0 * B * H * W * C * R * S * co)
+             kernel="auto", flops=2.0 * B * H * W * C * R * S * co)
         return dx
 
     def _block_bwd(self, blk, bp, c, dout, grads, ws):

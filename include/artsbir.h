@@ -34,6 +34,9 @@ typedef struct artsbir_conv_desc {
 /* ---- library ---------------------------------------------------------- */
 const char* artsbir_last_error(void);
 int artsbir_version(void);
+/* Name of the GEMM kernel variant the last conv2d_fwd / conv2d_dgrad / gemm_nt /
+ * conv2d_wgrad / gemm_tn call on this thread launched (for per-kernel profiling). */
+const char* artsbir_last_kernel(void);
 
 /* ---- convolution / linear (models.py:198-221,310-319 nn.Conv2d; models.py:243-246 nn.Linear) */
 

@@ -28,6 +28,12 @@ def short(name):
     m = re.match(r"_ZN7artsbir12wgrad_kernelIDF16bLi(\d+)ELi(\d+)E", name)
     if m:
         return f"wgrad_kernel<bf16,{m.group(1)},{m.group(2)}>"
+    m = re.match(r"_ZN7artsbir12pgemm_kernelILi(\d+)ELi(\d+)E", name)
+    if m:
+        return f"pgemm_kernel<{m.group(1)},{m.group(2)}>"
+    m = re.match(r"_ZN7artsbir14pstream_kernelILi(\d+)E", name)
+    if m:
+        return f"pstream_kernel<{m.group(1)}>"
     m = re.match(r"_ZN7artsbir\d+(\w+?_kernel)", name)
     if m:
         return m.group(1)

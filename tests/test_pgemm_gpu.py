@@ -1,0 +1,114 @@
+"""The pipelined LDS-DMA conv kernel (pgemm.hip): bf16 forward with BN statistics
+and bf16 data-gradient with residual epilogues, every tile shape forced in turn,
+against torch fp32 (CPU) on the same bf16-rounded operands."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import _hip
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # N, H, W, C, Cout, R, S, stride, pad
+    (2, 9, 7, 8, 32, 3, 3, 2, 1),       # stem-1 like: 8-channel multi-tap K-steps, stride 2
+    (2, 8, 8, 32, 64, 3, 3, 1, 1),      # 32 channels: two taps per K-step
+    (3, 7, 5, 64, 256, 1, 1, 1, 0),
+    (2, 14, 14, 128, 128, 3, 3, 1, 1),
+    (1, 5, 5, 256, 96, 1, 1, 1, 0),     # partial channel tile
+    (8, 28, 28, 64, 128, 3, 3, 1, 1),   # many pixel tiles
+    (3, 12, 12, 512, 64, 1, 1, 2, 0),   # strided 1x1
+]
+CFGS = ["auto", "0", "1", "2", "3", "4", "10"]
+
+
+@pytest.fixture
+def cfg_env(request):
+    old = os.environ.get("ARTSBIR_PGEMM_CFG")
+    yield
+    if old is None:
+        os.environ.pop("ARTSBIR_PGEMM_CFG", None)
+    else:
+        os.environ["ARTSBIR_PGEMM_CFG"] = old
+
+
+def _set(cfg):
+    if cfg == "auto":
+        os.environ.pop("ARTSBIR_PGEMM_CFG", None)
+    else:
+        os.environ["ARTSBIR_PGEMM_CFG"] = cfg
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("case", CASES)
+def test_pgemm_fwd_stats(case, cfg, dev, cfg_env):
+    _set(cfg)
+    N, H, W, C, Co, R, S, st, pd = case
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Co, C, R, S, generator=g) / (C * R * S) ** 0.5).bfloat16().float()
+    ref = F.conv2d(x, w, stride=st, padding=pd)
+    Ho, Wo = ref.shape[2:]
+    xd = _nhwc(x).to(dev, torch.bfloat16)
+    wd = w.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    y = torch.full((N * Ho * Wo, Co), float("nan"), device=dev, dtype=torch.bfloat16)
+    stats = torch.zeros(_hip.NSLOT, 2, Co, device=dev)
+    d = _hip.conv_desc(torch.bfloat16, N, H, W, C, Co, R, S, st, pd)
+    _hip.call("artsbir_conv2d_fwd", d, xd.data_ptr(), wd.data_ptr(), y.data_ptr(), Co, 0, 0, None, None, None, 0,
+              stats.data_ptr(), _hip.stream())
+    torch.cuda.synchronize()
+    out = y.float().cpu().view(N, Ho, Wo, Co).permute(0, 3, 1, 2)
+    assert torch.isfinite(out).all()
+    assert torch.allclose(out, ref, atol=2e-2, rtol=1e-2), (out - ref).abs().max()
+    s = stats.sum(0).cpu()
+    r2 = ref.permute(0, 2, 3, 1).reshape(-1, Co)
+    assert torch.allclose(s[0], r2.sum(0), atol=1e-2, rtol=1e-3)
+    assert torch.allclose(s[1], (r2 * r2).sum(0), atol=1e-2, rtol=1e-3)
+
+
+DG_CASES = [
+    # N, H, W, Cin, Cout, R, pad, res_mode
+    (2, 8, 8, 64, 64, 3, 1, 0),
+    (2, 8, 8, 64, 64, 3, 1, 1),
+    (2, 8, 8, 256, 64, 1, 0, 2),
+    (3, 14, 14, 128, 256, 1, 0, 1),
+    (2, 10, 6, 32, 64, 3, 1, 0),        # dY with 64 channels -> 32-channel dX (stem)
+    (2, 10, 6, 32, 32, 3, 1, 0),        # 32-channel dY: multi-tap
+    (8, 28, 28, 128, 128, 3, 1, 2),
+]
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("case", DG_CASES)
+def test_pgemm_dgrad_residual(case, cfg, dev, cfg_env):
+    _set(cfg)
+    N, H, W, Ci, Co, R, pd, rm = case
+    g = torch.Generator().manual_seed(2)
+    dy = torch.randn(N, Co, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Co, Ci, R, R, generator=g) / (Co * R * R) ** 0.5).bfloat16().float()
+    ref = torch.nn.grad.conv2d_input((N, Ci, H, W), w, dy, stride=1, padding=pd)
+    res = None
+    if rm == 1:
+        res = torch.randn(N, Ci, H, W, generator=g).bfloat16().float()
+        ref = ref + res
+    elif rm == 2:
+        res = torch.randn(N, Ci, H // 2, W // 2, generator=g).bfloat16().float()
+        ref = ref + 0.25 * F.interpolate(res, scale_factor=2, mode="nearest")
+    wdflip = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Ci][R][S][Co]
+    dyd = _nhwc(dy).to(dev, torch.bfloat16)
+    wdd = wdflip.to(dev, torch.bfloat16)
+    dx = torch.full((N * H * W, Ci), float("nan"), device=dev, dtype=torch.bfloat16)
+    resd = _nhwc(res).to(dev, torch.bfloat16) if res is not None else None
+    d = _hip.conv_desc(torch.bfloat16, N, H, W, Ci, Co, R, R, 1, pd)
+    _hip.call("artsbir_conv2d_dgrad", d, dyd.data_ptr(), wdd.data_ptr(), dx.data_ptr(),
+              resd.data_ptr() if resd is not None else None, rm, _hip.stream())
+    torch.cuda.synchronize()
+    out = dx.float().cpu().view(N, H, W, Ci).permute(0, 3, 1, 2)
+    assert torch.isfinite(out).all()
+    assert torch.allclose(out, ref, atol=2e-2, rtol=1e-2), (out - ref).abs().max()
