@@ -898,8 +898,112 @@ static void launch_wgrad_tile(WgradArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((wgrad_kernel<T, BM, BN, false>), dim3((unsigned)(tiles * splits)), dim3(256), 0, st, a);
 }
 
+// wgrad kernel choice per shape (bf16): register-staged wgrad_kernel (-1) or
+// a tile configuration c >= 0 of the pipelined LDS-DMA transposed-read kernel
+// (pwgrad.hip); tuned on first use into a scratch gradient buffer (the real dW
+// is accumulated into, so candidates must not touch it); ARTSBIR_TUNE=0 keeps
+// the register-staged kernel, ARTSBIR_WGRAD_CFG=<c> forces a candidate.
+struct WgKey {
+  long long M;
+  int H, W, C, Cout, R, S, stride, pad, dense, K;
+  long long ldd, ldx;
+  bool operator<(const WgKey& o) const {
+    return std::tie(M, H, W, C, Cout, R, S, stride, pad, dense, K, ldd, ldx) <
+           std::tie(o.M, o.H, o.W, o.C, o.Cout, o.R, o.S, o.stride, o.pad, o.dense, o.K, o.ldd, o.ldx);
+  }
+};
+static std::map<WgKey, int> g_wg_choice;
+static float* g_tune_dw = nullptr;
+static size_t g_tune_dw_n = 0;
+
+static PwArgs to_pw(const WgradArgs& a) {
+  PwArgs p;
+  p.dy = a.dy; p.dy_elems = a.dy_elems; p.ldd = a.ldd;
+  p.x = a.x; p.x_elems = a.x_elems; p.sN = a.sN; p.sH = a.sH; p.sW = a.sW;
+  p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
+  p.Ho = a.Ho; p.Wo = a.Wo; p.dense = a.dense; p.ldx = a.ldx;
+  p.Cout = a.Cout; p.K = a.K; p.M = a.M; p.m_per_split = 0; p.dw = a.dw;
+  return p;
+}
+
+template <typename T>
+static void launch_wgrad_old(WgradArgs& a, hipStream_t st);
+
+// candidate -1: register-staged wgrad_kernel; c >= 0: pipelined config c
+static bool run_wg_candidate(int c, WgradArgs& a, hipStream_t st) {
+  if (c >= 0) return pwgrad_launch(to_pw(a), c, st);
+  launch_wgrad_old<bf16>(a, st);
+  return true;
+}
+
+static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
+  const size_t need = (size_t)a.Cout * a.K;
+  if (need > g_tune_dw_n) {
+    if (g_tune_dw) hipFree(g_tune_dw);
+    g_tune_dw = nullptr;
+    g_tune_dw_n = 0;
+    if (hipMalloc(&g_tune_dw, need * sizeof(float)) != hipSuccess) return -1;
+    g_tune_dw_n = need;
+  }
+  WgradArgs at = a;
+  at.dw = g_tune_dw;
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  int best = -1;
+  float best_ms = 1e30f;
+  for (int c = -1; c < pwgrad_num_cfgs(); ++c) {
+    if (!run_wg_candidate(c, at, st)) continue;
+    float ms = 1e30f;
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(e0, st);
+      run_wg_candidate(c, at, st);
+      hipEventRecord(e1, st);
+      hipEventSynchronize(e1);
+      float t = 0.f;
+      hipEventElapsedTime(&t, e0, e1);
+      if (t < ms) ms = t;
+    }
+    if (ms < best_ms) { best_ms = ms; best = c; }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return best;
+}
+
 template <typename T>
 static int launch_wgrad(WgradArgs& a, hipStream_t st) {
+  if (sizeof(T) == 2 && !a.in_scale) {
+    int choice;
+    const char* force = getenv("ARTSBIR_WGRAD_CFG");
+    if (force) {
+      choice = atoi(force);
+    } else {
+      const WgKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.dense, a.K, a.ldd, a.ldx};
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      auto it = g_wg_choice.find(key);
+      if (it != g_wg_choice.end()) {
+        choice = it->second;
+      } else {
+        const char* tune = getenv("ARTSBIR_TUNE");
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        hipStreamIsCapturing(st, &cs);
+        choice = ((tune && atoi(tune) == 0) || cs != hipStreamCaptureStatusNone) ? -1 : tune_wgrad(a, st);
+        g_wg_choice[key] = choice;
+      }
+    }
+    if (choice >= 0 && pwgrad_launch(to_pw(a), choice, st)) {
+      ARTSBIR_CHECK_LAUNCH("pwgrad");
+      return 0;
+    }
+  }
+  launch_wgrad_old<T>(a, st);
+  ARTSBIR_CHECK_LAUNCH("wgrad");
+  return 0;
+}
+
+template <typename T>
+static void launch_wgrad_old(WgradArgs& a, hipStream_t st) {
   const bool bf = sizeof(T) == 2;
   if (a.Cout <= 64) {
     set_last_kernel(bf ? "wgrad_kernel<bf16,64,128>" : "wgrad_kernel<f32,64,128>");
@@ -908,8 +1012,6 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
     set_last_kernel(bf ? "wgrad_kernel<bf16,128,128>" : "wgrad_kernel<f32,128,128>");
     launch_wgrad_tile<T, 128, 128>(a, st);
   }
-  ARTSBIR_CHECK_LAUNCH("wgrad");
-  return 0;
 }
 
 extern "C" int artsbir_conv2d_wgrad(const artsbir_conv_desc* d, const void* dy, const void* x,

@@ -264,6 +264,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
     if (lps_hi) wait_stages<LPS_HI, NSTAGE>(ahead);
     else wait_stages<LPS_LO, NSTAGE>(ahead);
+    // retire this wave's LDS reads of the slot the next issue overwrites
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
@@ -447,6 +449,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       wait_stages<LPS, NSTAGE>(ahead);
     }
     for (int s = 0; s < total; ++s) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);
@@ -472,6 +475,8 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
 #pragma unroll
     for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < total; ++s) {
+    // retire this wave's LDS reads of the slot the next issue overwrites
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     {

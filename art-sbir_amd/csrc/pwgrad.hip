@@ -1,0 +1,355 @@
+// Pipelined weight-gradient GEMM (bf16 in, f32 accumulate, f32 atomics out)
+// for gfx950: dW[co][k] += sum_m dY[m][co] * Xcol[m][k]  — the backward of
+// every nn.Conv2d / nn.Linear weight on the encoder path
+// (models.py:198-221, 310-316; attention-pool projections models.py:243-246).
+//
+// Both operands are reduction-major in HBM (rows m = output pixels).  They are
+// staged by LDS-DMA in their natural row-major form — dY rows of co, Xcol rows
+// of k (implicit im2col with per-row padding masks) — and the MFMA fragments,
+// which need 8 consecutive m per lane, are read with the gfx950 transposing
+// LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): no register
+// transposes.  LDS image: every operand tile is viewed as rows of 128
+// bf16 (256 B) with 16-B chunk ch of pseudo-row pr stored at slot
+// ch ^ (((pr & 3) << 2) | ((pr >> 2) & 3)) (guide T10 image (b)); the XOR is
+// applied to the per-lane LDS-DMA source address.  An NSTAGE ring with counted
+// vmcnt keeps NSTAGE-2 stages in flight across the per-K-step barrier; the
+// reduction over m is split over workgroups (f32 atomics into dW).
+#include <cstdlib>
+
+#include "common.h"
+#include "pgemm.h"
+
+namespace artsbir {
+
+#define PW_OOB 0x80000000u
+typedef __attribute__((address_space(3))) void* pw_lds_t;
+typedef short pw_v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) pw_v4s* pw_lds_v4s;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pw_rsrc(const void* base, long long bytes) {
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  if (bytes < 0) bytes = 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ void pw_glds16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(pw_lds_t)lds);
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(base), "s"(r)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void pw_vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int LPS, int NSTAGE>
+__device__ __forceinline__ void pw_wait_stages(int ahead) {
+  if constexpr (NSTAGE >= 4) {
+    if (ahead >= 2) { pw_vm_wait<2 * LPS>(); return; }
+  }
+  if constexpr (NSTAGE >= 3) {
+    if (ahead >= 1) { pw_vm_wait<LPS>(); return; }
+  }
+  pw_vm_wait<0>();
+}
+
+__device__ __forceinline__ int pw_swz(int pr) { return ((pr & 3) << 2) | ((pr >> 2) & 3); }
+
+// byte offset in a tile image of element (m, c) of a tile TW elements wide
+template <int TW>
+__device__ __forceinline__ int pw_off(int m, int c) {
+  const int f = m * TW + c;
+  const int pr = f >> 7, pc = f & 127;
+  return pr * 256 + (((pc >> 3) ^ pw_swz(pr)) << 4) + ((pc & 7) << 1);
+}
+
+// 4 consecutive-m x 16-column block for the transposing read: lane t = 4q + p
+// of a 16-lane group supplies row m0 + q, columns c0 + 4p .. c0 + 4p + 3
+template <int TW>
+__device__ __forceinline__ pw_v4s pw_tr(const char* tile, int m0, int c0, int t) {
+  const char* p = tile + pw_off<TW>(m0 + (t >> 2), c0 + 4 * (t & 3));
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_v4s)(pw_lds_t)p);
+}
+
+__device__ __forceinline__ long long pw_xcd_remap(long long bid, long long nwg) {
+  if (nwg < 8) return bid;
+  const long long q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+template <int BCO, int BKK, int WCO, int WKK, int NSTAGE, bool DENSE>
+__global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
+  constexpr int NW = WCO * WKK;
+  constexpr int BM = 64;  // m rows per stage
+  constexpr int AB = BM * BCO * 2, BB = BM * BKK * 2, STAGE = AB + BB;
+  constexpr int IA = AB / 1024, IB = BB / 1024;  // 1-KB LDS-DMA instructions per operand per stage
+  static_assert(IA % NW == 0 || NW % IA == 0, "A loader split");
+  static_assert(IB % NW == 0, "B loader split");
+  constexpr int LA = IA >= NW ? IA / NW : 1;     // A instructions per wave (waves >= IA issue none)
+  constexpr int LB = IB / NW;
+  constexpr int WTCO = BCO / WCO, WTK = BKK / WKK;
+  constexpr int MT = WTCO / 16, NT = WTK / 16;
+  constexpr int LPS_HI = LA + LB, LPS_LO = (IA >= NW ? LA : 0) + LB;
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntco = (a.Cout + BCO - 1) / BCO, ntk = (a.K + BKK - 1) / BKK;
+  const int ntiles = ntco * ntk;
+  const long long nwg = (long long)gridDim.x;
+  const long long lid = pw_xcd_remap(blockIdx.x, nwg);
+  const long long split = lid / ntiles;
+  const int tile = (int)(lid % ntiles);
+  const int co0 = (tile / ntk) * BCO, k0 = (tile % ntk) * BKK;
+  const long long m_beg = split * a.m_per_split;
+  long long m_end = m_beg + a.m_per_split;
+  if (m_end > a.M) m_end = a.M;
+  const int nk = (int)((m_end - m_beg + BM - 1) / BM);
+
+  const __amdgpu_buffer_rsrc_t dr = pw_rsrc(reinterpret_cast<const bf16*>(a.dy) + m_beg * a.ldd,
+                                            (a.dy_elems - m_beg * a.ldd) * 2);
+  const int HoWo = a.Ho * a.Wo;
+  const long long img_beg = DENSE ? 0 : m_beg / HoWo;
+  const __amdgpu_buffer_rsrc_t xr =
+      DENSE ? pw_rsrc(reinterpret_cast<const bf16*>(a.x) + m_beg * a.ldx, (a.x_elems - m_beg * a.ldx) * 2)
+            : pw_rsrc(reinterpret_cast<const bf16*>(a.x) + img_beg * a.sN, (a.x_elems - img_beg * a.sN) * 2);
+
+  // ---- loader decode (fixed per lane): for each instruction, the tile
+  // element (m_local, c) whose 16-B chunk this lane moves
+  const int lpr = lane >> 4, lslot = lane & 15;
+  bool a_on[LA];
+  int a_m[LA];
+  unsigned a_col[LA];  // byte offset of the co columns, PW_OOB if out of range
+#pragma unroll
+  for (int u = 0; u < LA; ++u) {
+    const int g = u * NW + wid;
+    a_on[u] = g < IA;
+    const int pr = g * 4 + lpr;
+    const int f = pr * 128 + ((lslot ^ pw_swz(pr)) << 3);
+    a_m[u] = f / BCO;
+    const int co = co0 + f % BCO;
+    a_col[u] = co < a.Cout ? (unsigned)(co * 2) : PW_OOB;
+  }
+  int b_m[LB];
+  unsigned b_tap[LB];  // DENSE: byte offset of the k columns; conv: ci * 2
+  int b_r[LB], b_s[LB];
+  int b_p[LB];  // conv: pixel index of this instruction's row at K-step 0, relative to image img_beg
+#pragma unroll
+  for (int u = 0; u < LB; ++u) {
+    const int g = u * NW + wid;
+    const int pr = g * 4 + lpr;
+    const int f = pr * 128 + ((lslot ^ pw_swz(pr)) << 3);
+    b_m[u] = f / BKK;
+    const int k = k0 + f % BKK;
+    if (k >= a.K) {
+      b_tap[u] = PW_OOB;
+      b_r[u] = 0; b_s[u] = 0;
+    } else if (DENSE) {
+      b_tap[u] = (unsigned)(k * 2);
+      b_r[u] = 0; b_s[u] = 0;
+    } else {
+      const int rs = k / a.C, ci = k - (k / a.C) * a.C;
+      b_r[u] = rs / a.S;
+      b_s[u] = rs - b_r[u] * a.S;
+      b_tap[u] = (unsigned)(ci * 2);  // the tap (r, s) enters through ih, iw
+    }
+    b_p[u] = DENSE ? 0 : (int)(m_beg - img_beg * HoWo) + b_m[u];
+  }
+  const bool lps_hi = a_on[0];
+  const float inv_howo = 1.0f / (float)HoWo, inv_wo = 1.0f / (float)a.Wo;
+
+  auto issue = [&](int kt, int buf) {
+    char* as = smem + buf * STAGE;
+    char* bs = as + AB;
+    const long long mrow0 = (long long)kt * BM;  // relative to m_beg
+#pragma unroll
+    for (int u = 0; u < LA; ++u) {
+      if (!a_on[u]) continue;
+      const long long m = mrow0 + a_m[u];
+      const bool ok = m_beg + m < m_end && a_col[u] != PW_OOB;
+      pw_glds16(dr, as + (u * NW + wid) * 1024, ok ? (unsigned)(m * a.ldd * 2) + a_col[u] : PW_OOB);
+    }
+#pragma unroll
+    for (int u = 0; u < LB; ++u) {
+      const long long m = mrow0 + b_m[u];
+      bool ok = m_beg + m < m_end && b_tap[u] != PW_OOB;
+      unsigned off;
+      if (DENSE) {
+        off = (unsigned)(m * a.ldx * 2) + b_tap[u];
+      } else {
+        // pixel -> (image, oh, ow) by float-reciprocal division (exact: p < 2^22)
+        const int p = b_p[u] + kt * BM;
+        int im = (int)((float)p * inv_howo);
+        int rem = p - im * HoWo;
+        if (rem < 0) { --im; rem += HoWo; } else if (rem >= HoWo) { ++im; rem -= HoWo; }
+        int oh = (int)((float)rem * inv_wo);
+        int ow = rem - oh * a.Wo;
+        if (ow < 0) { --oh; ow += a.Wo; } else if (ow >= a.Wo) { ++oh; ow -= a.Wo; }
+        const int ih = oh * a.stride - a.pad + b_r[u];
+        const int iw = ow * a.stride - a.pad + b_s[u];
+        ok = ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+        off = (unsigned)(((long long)im * a.sN + (long long)ih * a.sH + (long long)iw * a.sW) * 2) + b_tap[u];
+      }
+      pw_glds16(xr, bs + (u * NW + wid) * 1024, ok ? off : PW_OOB);
+    }
+  };
+
+  const int wco = wid / WKK, wkk = wid % WKK;
+  const int t = lane & 15, g = lane >> 4;
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) {
+    const char* as = smem + buf * STAGE;
+    const char* bs = as + AB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int mb = kk * 32 + 8 * g;
+      bf16x8 af[MT], bv[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const pw_v4s lo = pw_tr<BCO>(as, mb, wco * WTCO + 16 * i, t);
+        const pw_v4s hi = pw_tr<BCO>(as, mb + 4, wco * WTCO + 16 * i, t);
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const pw_v4s lo = pw_tr<BKK>(bs, mb, wkk * WTK + 16 * j, t);
+        const pw_v4s hi = pw_tr<BKK>(bs, mb + 4, wkk * WTK + 16 * j, t);
+        bv[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    int ahead = nk - 1 - kt;
+    if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
+    if (lps_hi) pw_wait_stages<LPS_HI, NSTAGE>(ahead);
+    else pw_wait_stages<LPS_LO, NSTAGE>(ahead);
+    // retire this wave's LDS reads of the slot the next issue overwrites
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1, (kt + NSTAGE - 1) % NSTAGE);
+    compute(kt % NSTAGE);
+  }
+
+  // acc[i][j][r]: co = co0 + wco*WTCO + 16 i + 4 g + r, k = k0 + wkk*WTK + 16 j + t
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int k = k0 + wkk * WTK + 16 * j + t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wco * WTCO + 16 * i + 4 * g + r;
+        if (co < a.Cout && k < a.K) atomicAdd(a.dw + (long long)co * a.K + k, acc[i][j][r]);
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// tile configurations (BCO x BKK output tile, waves WCO x WKK, LDS stages)
+struct PwCfg {
+  int bco, bkk, threads;
+};
+static const PwCfg kPw[] = {
+    {128, 128, 256},  // 0: 4 waves 64x64, 4 stages
+    {128, 256, 512},  // 1: 8 waves 64x64, 3 stages
+    {256, 128, 512},  // 2: 8 waves 64x64, 3 stages
+    {64, 256, 512},   // 3: 8 waves 64x32, 3 stages
+    {64, 128, 256},   // 4: 4 waves 64x32, 4 stages
+    {32, 128, 256},   // 5: 4 waves 32x32, 4 stages
+    {64, 512, 512},   // 6: 8 waves 64x64, 2 stages
+};
+constexpr int kNumPw = 7;
+
+template <bool DENSE>
+static void pw_launch_c(int c, const PwArgs& a, long long blocks, hipStream_t st) {
+  const dim3 g((unsigned)blocks);
+  switch (c) {
+    case 0: hipLaunchKernelGGL((pwgrad_kernel<128, 128, 2, 2, 4, DENSE>), g, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((pwgrad_kernel<128, 256, 2, 4, 3, DENSE>), g, dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pwgrad_kernel<256, 128, 4, 2, 3, DENSE>), g, dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((pwgrad_kernel<64, 256, 1, 8, 3, DENSE>), g, dim3(512), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((pwgrad_kernel<64, 128, 1, 4, 4, DENSE>), g, dim3(256), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((pwgrad_kernel<32, 128, 1, 4, 4, DENSE>), g, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((pwgrad_kernel<64, 512, 1, 8, 2, DENSE>), g, dim3(512), 0, st, a); break;
+  }
+}
+
+// split-K levels: (target workgroups, minimum K-steps per workgroup).  Fewer,
+// longer splits trade CU fill for fewer f32 atomics into dW (large outputs).
+static const int kSplitTarget[] = {1536, 512, 256};
+static const int kSplitMinSteps[] = {8, 24, 64};
+constexpr int kNumLevels = 3;
+
+int pwgrad_num_cfgs() { return kNumPw * kNumLevels; }
+
+// candidate c = cfg + kNumPw * level of the pipelined wgrad; false (nothing
+// launched) if not applicable
+bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
+  if (cand < 0 || cand >= kNumPw * kNumLevels) return false;
+  const int c = cand % kNumPw, level = cand / kNumPw;
+  if (a.Cout % 8 || a.K % 8 || a.M <= 0) return false;
+  if (!a.dense && (a.C % 8 || a.R * a.S > 32)) return false;
+  const PwCfg& g = kPw[c];
+  // skip shapes where most of the tile would be padding
+  if (g.bco > 32 && a.Cout <= g.bco / 2) return false;
+  if (g.bkk > 128 && a.K <= g.bkk / 2) return false;
+  const long long ntiles = (long long)((a.Cout + g.bco - 1) / g.bco) * ((a.K + g.bkk - 1) / g.bkk);
+  const long long ksteps = (a.M + 63) / 64;
+  long long splits = (kSplitTarget[level] + ntiles - 1) / ntiles;
+  const long long max_splits = (ksteps + kSplitMinSteps[level] - 1) / kSplitMinSteps[level];
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  long long per = (ksteps + splits - 1) / splits;
+  // keep workgroup-relative byte offsets below 2^31 and pixel indices below 2^22
+  const long long row_bytes = (a.dense ? (a.ldx > a.ldd ? a.ldx : a.ldd) : a.ldd) * 2;
+  long long cap = (0x7fffffffLL / row_bytes) / 64 - 1;
+  if (!a.dense) {
+    const long long HoWo = (long long)a.Ho * a.Wo;
+    const long long imgs = 0x7fffffffLL / (a.sN * 2) - 2;
+    if (imgs < 1 || HoWo >= (1LL << 21)) return false;
+    const long long cap3 = imgs * HoWo / 64;
+    if (cap3 < cap) cap = cap3;
+    const long long cap4 = ((1LL << 22) - 2 * HoWo) / 64;
+    if (cap4 < cap) cap = cap4;
+  }
+  if (cap < 1) return false;
+  if (per > cap) per = cap;
+  a.m_per_split = per * 64;
+  splits = (ksteps + per - 1) / per;
+  const long long blocks = ntiles * splits;
+  if (blocks > 0x7fffffffLL) return false;
+  static const char* names[] = {"pwgrad_kernel<128,128>", "pwgrad_kernel<128,256>", "pwgrad_kernel<256,128>",
+                                "pwgrad_kernel<64,256>",  "pwgrad_kernel<64,128>",  "pwgrad_kernel<32,128>",
+                                "pwgrad_kernel<64,512>"};
+  set_last_kernel(names[c]);
+  if (a.dense) pw_launch_c<true>(c, a, blocks, st);
+  else pw_launch_c<false>(c, a, blocks, st);
+  return true;
+}
+
+}  // namespace artsbir

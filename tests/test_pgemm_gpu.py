@@ -112,3 +112,69 @@ def test_pgemm_dgrad_residual(case, cfg, dev, cfg_env):
     out = dx.float().cpu().view(N, H, W, Ci).permute(0, 3, 1, 2)
     assert torch.isfinite(out).all()
     assert torch.allclose(out, ref, atol=2e-2, rtol=1e-2), (out - ref).abs().max()
+
+
+WG_CASES = [
+    # N, H, W, C, Cout, R, S, stride, pad
+    (2, 9, 7, 8, 32, 3, 3, 2, 1),        # stem-1 like (8 channels, stride 2)
+    (2, 12, 12, 32, 32, 3, 3, 1, 1),     # 32 -> 32 (Cout tile 32)
+    (2, 12, 12, 32, 64, 3, 3, 1, 1),     # 32 -> 64 (Cout tile 64)
+    (3, 7, 5, 64, 256, 1, 1, 1, 0),      # dense 1x1
+    (2, 14, 14, 128, 128, 3, 3, 1, 1),
+    (4, 28, 28, 64, 64, 3, 3, 1, 1),     # many K-steps, split over workgroups
+    (3, 12, 12, 512, 64, 1, 1, 2, 0),    # strided 1x1 (not dense)
+    (1, 5, 5, 256, 96, 1, 1, 1, 0),      # partial Cout tile
+]
+
+
+@pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "4", "5", "6", "9", "16", "auto"])
+@pytest.mark.parametrize("case", WG_CASES)
+def test_wgrad_accumulates(case, cfg, dev):
+    old = os.environ.get("ARTSBIR_WGRAD_CFG")
+    if cfg == "auto":
+        os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+    else:
+        os.environ["ARTSBIR_WGRAD_CFG"] = cfg
+    try:
+        N, H, W, C, Co, R, S, st, pd = case
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+        w = torch.randn(Co, C, R, S, generator=g)
+        Ho = (H + 2 * pd - R) // st + 1
+        Wo = (W + 2 * pd - S) // st + 1
+        dy = torch.randn(N, Co, Ho, Wo, generator=g).bfloat16().float()
+        wr = w.clone().requires_grad_(True)
+        F.conv2d(x, wr, stride=st, padding=pd).backward(dy)
+        init = torch.randn(Co, R, S, C, generator=g)
+        ref = init + wr.grad.permute(0, 2, 3, 1)
+        dw = init.clone().to(dev)
+        d = _hip.conv_desc(torch.bfloat16, N, H, W, C, Co, R, S, st, pd)
+        dyd, xd = _nhwc(dy).to(dev, torch.bfloat16), _nhwc(x).to(dev, torch.bfloat16)
+        _hip.call("artsbir_conv2d_wgrad", d, dyd.data_ptr(), xd.data_ptr(), None, None, 0, dw.data_ptr(),
+                  _hip.stream())
+        torch.cuda.synchronize()
+        assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
+    finally:
+        if old is None:
+            os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+        else:
+            os.environ["ARTSBIR_WGRAD_CFG"] = old
+
+
+@pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "6"])
+@pytest.mark.parametrize("M,N,K,ldd,ldx", [(100, 96, 64, 96, 64), (3000, 512, 2048, 512, 2048), (77, 40, 24, 48, 32)])
+def test_gemm_tn_strided(M, N, K, ldd, ldx, cfg, dev):
+    os.environ["ARTSBIR_WGRAD_CFG"] = cfg
+    try:
+        g = torch.Generator().manual_seed(4)
+        dy = torch.randn(M, ldd, generator=g).bfloat16().float()
+        x = torch.randn(M, ldx, generator=g).bfloat16().float()
+        ref = dy[:, :N].t() @ x[:, :K]
+        dw = torch.zeros(N, K, device=dev)
+        dyd, xd = dy.to(dev, torch.bfloat16), x.to(dev, torch.bfloat16)
+        _hip.call("artsbir_gemm_tn", _hip.DT_BF16, M, N, K, dyd.data_ptr(), ldd, xd.data_ptr(), ldx, dw.data_ptr(),
+                  _hip.stream())
+        torch.cuda.synchronize()
+        assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
+    finally:
+        os.environ.pop("ARTSBIR_WGRAD_CFG", None)
