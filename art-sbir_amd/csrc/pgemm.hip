@@ -28,6 +28,18 @@
 namespace artsbir {
 
 #define PG_OOB 0x80000000u
+#ifndef PG_PRIO
+#define PG_PRIO 1
+#endif
+#if PG_PRIO
+// raise wave priority around each MFMA cluster (guide T5: keeps hipcc from
+// spreading the cluster across the stage barriers)
+#define PG_PRIO_ON() __builtin_amdgcn_s_setprio(1)
+#define PG_PRIO_OFF() __builtin_amdgcn_s_setprio(0)
+#else
+#define PG_PRIO_ON()
+#define PG_PRIO_OFF()
+#endif
 typedef __attribute__((address_space(3))) void* pg_lds_t;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pg_rsrc(const void* base, long long bytes) {
@@ -241,6 +253,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
       for (int i = 0; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * 128 + so);
 #pragma unroll
       for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * 128 + so);
+      PG_PRIO_ON();
 #pragma unroll
       for (int i = 0; i < MTC; ++i)
 #pragma unroll
@@ -248,6 +261,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
                                                               *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j], 0,
                                                               0, 0);
+      PG_PRIO_OFF();
     }
   };
 
@@ -492,6 +506,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
 #pragma unroll
         for (int j = 0; j < NTP; ++j)
           bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * 128 + so);
+        PG_PRIO_ON();
 #pragma unroll
         for (int i = 0; i < MTC; ++i)
 #pragma unroll
@@ -499,6 +514,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
                                                                 *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j],
                                                                 0, 0, 0);
+        PG_PRIO_OFF();
       }
     }
     const int ti = s / nk;

@@ -21,6 +21,15 @@
 //     could have dropped a true top-k item (then the host reruns that query
 //     with an exhaustive exact scan);
 //  3. knn_uncertain_kernel: exact checks of the queued uncertain items.
+//
+// Error bound of the approximate squared distance |q|^2 + |g|^2 - 2 q.g
+// (norms in f32 from the f32 rows, the dot product from the compute copies):
+// bf16 rounding of each operand is relative <= 2^-8, so each product is off by
+// <= (2^-7 + 2^-16)|q_i g_i| and the dot by <= 2^-7 sum|q_i g_i| <= 2^-7 |q||g|
+// (Cauchy-Schwarz); products of bf16 are exact in f32 and the f32 accumulation
+// adds < 2^-13 |q||g| for D <= 4096.  Hence |err(d^2)| <= rel |q| |g|max + 1e-3
+// with rel = 2^-6 + 2^-12 (bf16) or 2^-14 (exact-f32 MFMA); every decision
+// that could depend on the approximation is re-made in f64.
 #include "common.h"
 #include "../../include/artsbir.h"
 
@@ -95,7 +104,7 @@ __global__ void knn_band_kernel(const float* __restrict__ q, const float* __rest
   const int qi = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (qi >= nq) return;
   const long long p = pos[qi];
-  const double eps = rel * (2.0 * sqrt((double)qsq[qi] * gsq_max) + qsq[qi] + gsq_max) + 1e-3;
+  const double eps = rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
   if (p < g_base || p >= g_base + n_g) {
     // positive not in this shard: the caller provides dpos from its owner
     if (lane == 0) {
@@ -117,7 +126,7 @@ __global__ void knn_band_from_dpos_kernel(const double* __restrict__ dpos, const
                                           int nq, float rel, float* __restrict__ lo, float* __restrict__ hi) {
   const int qi = blockIdx.x * blockDim.x + threadIdx.x;
   if (qi >= nq) return;
-  const double eps = rel * (2.0 * sqrt((double)qsq[qi] * gsq_max) + qsq[qi] + gsq_max) + 1e-3;
+  const double eps = rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
   const double d = dpos[qi];
   lo[qi] = d >= 0 ? (float)(d * d - eps) : -1.f;
   hi[qi] = d >= 0 ? (float)(d * d + eps) : -1.f;
@@ -344,7 +353,7 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
   const float* qr = q + (long long)qi * D;
   const float* cd = cand_d + (long long)qi * nc;
   const int* ci = cand_i + (long long)qi * nc;
-  const double eps = rel * (2.0 * sqrt((double)qsq[qi] * gsq_max) + qsq[qi] + gsq_max) + 1e-3;
+  const double eps = rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
   __shared__ double rd[4];
   __shared__ int ri[4], rslot[4];
   // (1) a_k = k-th smallest approximate value: the k items with approx <= a_k have

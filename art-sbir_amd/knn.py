@@ -18,9 +18,10 @@ import torch
 import _hip
 from _hip import call, ptr
 
-# relative bound on the error of the approximate squared distance
-# |q|^2+|g|^2-2q.g (bf16 operands + f32 accumulation, or exact f32 MFMA)
-REL = {_hip.DT_BF16: 2.0 ** -6, _hip.DT_F32: 2.0 ** -14}
+# |approx d^2 - exact d^2| <= REL * |q| * max|g| + 1e-3 for the approximate squared
+# distance |q|^2+|g|^2-2q.g (bf16 operands + f32 accumulation, or exact f32
+# MFMA); derivation in csrc/retrieval.hip
+REL = {_hip.DT_BF16: 2.0 ** -6 + 2.0 ** -12, _hip.DT_F32: 2.0 ** -14}
 TILES_PER_CHUNK = 64
 UNC_CAP = 1 << 20
 
