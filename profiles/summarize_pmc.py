@@ -34,6 +34,9 @@ def short(name):
     m = re.match(r"_ZN7artsbir14pstream_kernelILi(\d+)E", name)
     if m:
         return f"pstream_kernel<{m.group(1)}>"
+    m = re.match(r"_ZN7artsbir13pwgrad_kernelILi(\d+)ELi(\d+)E", name)
+    if m:
+        return f"pwgrad_kernel<{m.group(1)},{m.group(2)}>"
     m = re.match(r"_ZN7artsbir\d+(\w+?_kernel)", name)
     if m:
         return m.group(1)
