@@ -212,6 +212,8 @@ __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, lo
     load8<T>(reinterpret_cast<const T*>(a.mask) + offs[0], m);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[0][e] = m[e] > 0.f ? g[0][e] : 0.f;
+  } else if constexpr (KIND == 2) {
+    load8<T>(reinterpret_cast<const T*>(a.d) + offs[0], g[0]);  // g given (masked upstream)
   } else {
     float dv[8];
     load8<T>(reinterpret_cast<const T*>(a.d) + (long long)u * a.C + cg * 8, dv);
@@ -251,6 +253,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
       long long offs[NQ];
       float g[NQ][8];
       bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, ms, mh);
+      if constexpr (POOL == 1) {  // g written back (in place over d allowed)
+        if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + offs[0], g[0]);
+      }
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         if (t >= a.ntarget) break;
@@ -543,7 +548,8 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
   if (d->ntarget < 1 || d->ntarget > 2) { set_error("bn_bwd: ntarget must be 1 or 2"); return -1; }
   if (d->kind == 1 && d->pool > 2) { set_error("bn_bwd: pool must be <= 2"); return -1; }
   if (d->kind == 1 && d->pool == 2 && (d->H % 2 || d->W % 2)) { set_error("bn_bwd: odd H/W with pool"); return -1; }
-  if (d->kind == 0 && d->pool > 1) { set_error("bn_bwd: pool only with kind 1"); return -1; }
+  if (d->kind < 0 || d->kind > 2) { set_error("bn_bwd: kind must be 0, 1 or 2"); return -1; }
+  if (d->kind != 1 && d->pool > 1) { set_error("bn_bwd: pool only with kind 1"); return -1; }
   if ((long long)d->B * d->H * d->W >= (1LL << 31)) { set_error("bn_bwd: too many pixels"); return -1; }
   a.kind = d->kind; a.pool = d->pool; a.d = d->d; a.mask = d->mask; a.msc = d->mask_scale; a.msh = d->mask_shift;
   a.ntarget = d->ntarget;
@@ -571,6 +577,7 @@ static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
     else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP>), dim3(grid), dim3(256), 0, st, a, upb);          \
   } while (0)
   if (a.kind == 0) BNB_LAUNCH(0, 1);
+  else if (a.kind == 2) BNB_LAUNCH(2, 1);
   else if (P == 2) BNB_LAUNCH(1, 2);
   else BNB_LAUNCH(1, 1);
 #undef BNB_LAUNCH

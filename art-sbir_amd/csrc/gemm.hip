@@ -124,9 +124,13 @@ struct ConvArgs {
   int out_f32;
   int accumulate;
   const float* bias;
-  float* stats;     // [NSLOT][2][Cout]
+  float* stats;     // [NSLOT][2][Cout] (x nseg)
   const void* res;  // epilogue residual (T): mode 1 same index, mode 2 2x2 average-unpool
   int res_mode;
+  // host-side only (the launcher splits / fuses; kernels ignore them)
+  int nseg;                 // BN segments (separate reference forward calls) of equal size
+  const void* bnb_desc;     // artsbir_bn_bwd_desc of a fused BN-backward reduction (dgrad)
+  long long bnb_pstride;    // floats between the BN parameters of consecutive segments
 };
 
 template <typename T, int BM, int BN, bool UNIFORM_TAP, bool AFFINE>
@@ -694,10 +698,11 @@ static void launch_conv_old(const ConvArgs& a, hipStream_t st) {
 // ---------------------------------------------------------------------------
 struct ConvKey {
   long long M;
-  int H, W, C, Cout, R, S, stride, pad, Ho, Wo, res_mode, stats;
+  int H, W, C, Cout, R, S, stride, pad, Ho, Wo, res_mode, stats, nseg, bnb;
   bool operator<(const ConvKey& o) const {
-    return std::tie(M, H, W, C, Cout, R, S, stride, pad, Ho, Wo, res_mode, stats) <
-           std::tie(o.M, o.H, o.W, o.C, o.Cout, o.R, o.S, o.stride, o.pad, o.Ho, o.Wo, o.res_mode, o.stats);
+    return std::tie(M, H, W, C, Cout, R, S, stride, pad, Ho, Wo, res_mode, stats, nseg, bnb) <
+           std::tie(o.M, o.H, o.W, o.C, o.Cout, o.R, o.S, o.stride, o.pad, o.Ho, o.Wo, o.res_mode, o.stats, o.nseg,
+                    o.bnb);
   }
 };
 static std::map<ConvKey, int> g_conv_choice;
@@ -705,14 +710,72 @@ static std::mutex g_tune_mu;
 static float* g_tune_stats = nullptr;
 static size_t g_tune_stats_n = 0;
 
+// The register-staged kernel over each BN segment in turn (its statistics
+// epilogue has no segment logic).
+template <typename T>
+static void launch_conv_old_seg(const ConvArgs& a, hipStream_t st) {
+  if (a.nseg <= 1 || !a.stats) { launch_conv_old<T>(a, st); return; }
+  const long long seg_m = a.M / a.nseg, seg_img = seg_m / ((long long)a.Ho * a.Wo);
+  for (int s = 0; s < a.nseg; ++s) {
+    ConvArgs p = a;
+    p.nseg = 1;
+    p.x = reinterpret_cast<const T*>(a.x) + s * seg_img * a.sN;
+    p.x_elems = seg_img * a.sN;
+    p.M = seg_m;
+    p.y = reinterpret_cast<T*>(a.y) + s * seg_m * a.ldy;
+    p.stats = a.stats + (long long)s * ARTSBIR_NSLOT * 2 * a.Cout;
+    launch_conv_old<T>(p, st);
+  }
+}
+
+// Fused BN-backward reduction done as a separate pass (f32 mode, or a shape the
+// pipelined kernel does not take): artsbir_bn_bwd_reduce per segment, writing
+// g = d * mask back over d.
+static int bnb_reduce_pass(const ConvArgs& a, const artsbir_bn_bwd_desc* bd, hipStream_t st) {
+  const long long seg_m = a.M / a.nseg;
+  const int seg_img = (int)(seg_m / ((long long)a.Ho * a.Wo));
+  const long long es = bd->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+  for (int s = 0; s < a.nseg; ++s) {
+    artsbir_bn_bwd_desc d = *bd;
+    const long long eo = s * seg_m * a.Cout * es;  // byte offset of the segment's elements
+    const long long po = s * a.bnb_pstride;
+    d.pool = 0;
+    d.d = reinterpret_cast<const char*>(a.y) + eo;
+    d.gout = reinterpret_cast<char*>(a.y) + eo;
+    if (bd->mask) d.mask = reinterpret_cast<const char*>(bd->mask) + eo;
+    if (bd->mask_scale) { d.mask_scale = bd->mask_scale + po; d.mask_shift = bd->mask_shift + po; }
+    for (int t = 0; t < bd->ntarget; ++t) {
+      d.y[t] = reinterpret_cast<const char*>(bd->y[t]) + eo;
+      d.mean[t] = bd->mean[t] + po;
+      d.istd[t] = bd->istd[t] + po;
+      d.slots[t] = bd->slots[t] + (long long)s * ARTSBIR_NSLOT * 2 * a.Cout;
+    }
+    d.B = seg_img; d.H = a.Ho; d.W = a.Wo; d.C = a.Cout;
+    const int rc = artsbir_bn_bwd_reduce(&d, st);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+template <typename T>
+static int run_old(const ConvArgs& a, hipStream_t st) {
+  launch_conv_old_seg<T>(a, st);
+  ARTSBIR_CHECK_LAUNCH("conv_gemm");
+  if (a.bnb_desc) return bnb_reduce_pass(a, reinterpret_cast<const artsbir_bn_bwd_desc*>(a.bnb_desc), st);
+  return 0;
+}
+
 static bool run_candidate(int c, const ConvArgs& a, const PgArgs& p, hipStream_t st) {
-  if (c == -2) { launch_conv_old<bf16>(a, st); return true; }
+  if (c == -2) return run_old<bf16>(a, st) == 0;
   return pgemm_launch_cfg(p, c, st);
 }
 
 static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
-  const size_t need = (size_t)ARTSBIR_NSLOT * 2 * a.Cout;
-  if (a.stats && need > g_tune_stats_n) {
+  // statistics / BN-backward sums of the trial runs go to a scratch buffer
+  const artsbir_bn_bwd_desc* bd = reinterpret_cast<const artsbir_bn_bwd_desc*>(a.bnb_desc);
+  const size_t per = (size_t)a.nseg * ARTSBIR_NSLOT * 2 * a.Cout;
+  const size_t need = bd ? per * bd->ntarget : (a.stats ? per : 0);
+  if (need > g_tune_stats_n) {
     if (g_tune_stats) hipFree(g_tune_stats);
     g_tune_stats = nullptr;
     g_tune_stats_n = 0;
@@ -721,7 +784,13 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   }
   ConvArgs at = a;
   PgArgs pt = p;
+  artsbir_bn_bwd_desc bt;
   if (a.stats) { at.stats = g_tune_stats; pt.stats = g_tune_stats; }
+  if (bd) {
+    bt = *bd;
+    for (int t = 0; t < bd->ntarget; ++t) { bt.slots[t] = g_tune_stats + t * per; pt.bnb_slots[t] = bt.slots[t]; }
+    at.bnb_desc = &bt;
+  }
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -750,19 +819,38 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
 template <typename T>
 static int launch_conv(const ConvArgs& a, hipStream_t st) {
   if ((long long)a.Cout * a.K * sizeof(T) > 0x7fffffffLL) { set_error("conv: weight tensor too large"); return -1; }
+  if (a.nseg < 1 || a.M % a.nseg || (a.M / a.nseg) % ((long long)a.Ho * a.Wo)) {
+    set_error("conv: %d BN segments do not split %lld output pixels into whole images", a.nseg, a.M);
+    return -1;
+  }
+  const artsbir_bn_bwd_desc* bd = reinterpret_cast<const artsbir_bn_bwd_desc*>(a.bnb_desc);
   if (sizeof(T) == 2 && !a.out_f32 && !a.accumulate && !a.bias && !a.in_scale) {
-    PgArgs p;
+    PgArgs p{};
     p.x = a.x; p.x_elems = a.x_elems; p.sN = a.sN; p.sH = a.sH; p.sW = a.sW;
     p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
     p.Ho = a.Ho; p.Wo = a.Wo; p.w = a.w; p.Cout = a.Cout; p.K = a.K; p.M = a.M;
     p.y = a.y; p.ldy = a.ldy; p.stats = a.stats; p.res = a.res; p.res_mode = a.res_mode; p.dbg = 0;
+    p.seg_m = a.nseg > 1 ? a.M / a.nseg : 0;
+    p.seg_stride = (long long)ARTSBIR_NSLOT * 2 * a.Cout;
+    if (bd) {
+      p.bnb = bd->kind == 1 ? 1 : 2;
+      p.bnb_nt = bd->ntarget;
+      for (int t = 0; t < bd->ntarget; ++t) {
+        p.bnb_y[t] = bd->y[t];
+        p.bnb_mean[t] = bd->mean[t];
+        p.bnb_istd[t] = bd->istd[t];
+        p.bnb_slots[t] = bd->slots[t];
+      }
+      p.bnb_msc = bd->mask_scale; p.bnb_msh = bd->mask_shift; p.bnb_mask = bd->mask;
+      p.bnb_pstride = a.bnb_pstride;
+    }
     int choice;
     const char* force = getenv("ARTSBIR_PGEMM_CFG");
     if (force) {
       choice = atoi(force);
     } else {
       const ConvKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.Ho, a.Wo, a.res_mode,
-                        a.stats ? 1 : 0};
+                        a.stats ? 1 : 0, a.nseg, bd ? p.bnb * 4 + p.bnb_nt : 0};
       std::lock_guard<std::mutex> lk(g_tune_mu);
       auto it = g_conv_choice.find(key);
       if (it != g_conv_choice.end()) {
@@ -785,9 +873,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
       return 0;
     }
   }
-  launch_conv_old<T>(a, st);
-  ARTSBIR_CHECK_LAUNCH("conv_gemm");
-  return 0;
+  return run_old<T>(a, st);
 }
 
 extern "C" int artsbir_conv2d_fwd(const artsbir_conv_desc* d, const void* x, const void* w, void* y,
@@ -813,12 +899,65 @@ extern "C" int artsbir_conv2d_fwd(const artsbir_conv_desc* d, const void* x, con
   a.y = y; a.ldy = ldy > 0 ? ldy : d->Cout;
   a.out_f32 = out_f32; a.accumulate = accumulate; a.bias = bias; a.stats = stats;
   a.res = nullptr; a.res_mode = 0;
+  a.nseg = 1; a.bnb_desc = nullptr; a.bnb_pstride = 0;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
 }
 
+extern "C" int artsbir_conv2d_fwd_seg(const artsbir_conv_desc* d, const void* x, const void* w, void* y, int nseg,
+                                      float* stats, void* stream) {
+  if (check_conv(d)) return -1;
+  if (nseg < 1 || d->N % nseg) { set_error("conv2d_fwd_seg: %d segments do not divide batch %d", nseg, d->N); return -1; }
+  ConvArgs a;
+  int Ho, Wo;
+  fill_geom(d, Ho, Wo);
+  a.x = x;
+  a.sW = d->C;
+  a.sH = (long long)d->W * d->C;
+  a.sN = (long long)d->H * d->W * d->C;
+  a.x_elems = (long long)d->N * a.sN;
+  a.H = d->H; a.W = d->W; a.C = d->C;
+  a.R = d->R; a.S = d->S; a.stride = d->stride; a.pad = d->pad;
+  a.Ho = Ho; a.Wo = Wo;
+  a.in_scale = nullptr; a.in_shift = nullptr; a.in_relu = 0;
+  a.w = w; a.Cout = d->Cout; a.K = d->R * d->S * d->C;
+  a.M = (long long)d->N * Ho * Wo;
+  a.y = y; a.ldy = d->Cout;
+  a.out_f32 = 0; a.accumulate = 0; a.bias = nullptr; a.stats = stats;
+  a.res = nullptr; a.res_mode = 0;
+  a.nseg = nseg; a.bnb_desc = nullptr; a.bnb_pstride = 0;
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
+}
+
+static int dgrad_common(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx, const void* res,
+                        int res_mode, const artsbir_bn_bwd_desc* bnb, int nseg, long long pstride, void* stream);
+
 extern "C" int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx,
                                     const void* res, int res_mode, void* stream) {
+  return dgrad_common(d, dy, wd, dx, res, res_mode, nullptr, 1, 0, stream);
+}
+
+extern "C" int artsbir_conv2d_dgrad_bnb(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx,
+                                        const void* res, int res_mode, const artsbir_bn_bwd_desc* bnb, int nseg,
+                                        long long param_stride, void* stream) {
+  if (!bnb) { set_error("conv2d_dgrad_bnb: no BN descriptor"); return -1; }
+  if (bnb->kind != 0 && bnb->kind != 1) { set_error("conv2d_dgrad_bnb: kind must be 0 or 1"); return -1; }
+  if (bnb->kind == 1 && bnb->pool > 1) { set_error("conv2d_dgrad_bnb: pooled BN inputs are not fused"); return -1; }
+  if (bnb->ntarget < 1 || bnb->ntarget > 2 || (bnb->kind == 1 && bnb->ntarget != 1)) {
+    set_error("conv2d_dgrad_bnb: bad target count %d", bnb->ntarget);
+    return -1;
+  }
+  if (bnb->kind == 0 ? !bnb->mask : (!bnb->mask_scale || !bnb->mask_shift)) {
+    set_error("conv2d_dgrad_bnb: missing ReLU mask");
+    return -1;
+  }
+  if (bnb->dtype != d->dtype) { set_error("conv2d_dgrad_bnb: dtype mismatch"); return -1; }
+  return dgrad_common(d, dy, wd, dx, res, res_mode, bnb, nseg, param_stride, stream);
+}
+
+static int dgrad_common(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx, const void* res,
+                        int res_mode, const artsbir_bn_bwd_desc* bnb, int nseg, long long pstride, void* stream) {
   // data gradient of a stride-1 convolution: a convolution of dy [N][H][W][Cout]
   // with the flipped, transposed weights wd [Cin][R][S][Cout] and padding R-1-pad.
   if (check_conv(d)) return -1;
@@ -826,6 +965,7 @@ extern "C" int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, 
   if (d->Cout % 8 || d->C % 8) { set_error("conv2d_dgrad: channels must be multiples of 8"); return -1; }
   if (res_mode < 0 || res_mode > 2 || (res_mode && !res)) { set_error("conv2d_dgrad: bad residual"); return -1; }
   if (res_mode == 2 && (d->H % 2 || d->W % 2)) { set_error("conv2d_dgrad: unpool residual needs even H, W"); return -1; }
+  if (nseg < 1 || d->N % nseg) { set_error("conv2d_dgrad: %d segments do not divide batch %d", nseg, d->N); return -1; }
   ConvArgs a;
   const int pad = d->R - 1 - d->pad;
   a.x = dy;
@@ -841,6 +981,7 @@ extern "C" int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, 
   a.y = dx; a.ldy = d->C;
   a.out_f32 = 0; a.accumulate = 0; a.bias = nullptr; a.stats = nullptr;
   a.res = res; a.res_mode = res_mode;
+  a.nseg = nseg; a.bnb_desc = bnb; a.bnb_pstride = pstride;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
 }
@@ -863,6 +1004,7 @@ extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void*
   p.y = c; p.ldy = ldc > 0 ? ldc : N;
   p.out_f32 = out_f32; p.accumulate = accumulate; p.bias = bias; p.stats = stats;
   p.res = nullptr; p.res_mode = 0;
+  p.nseg = 1; p.bnb_desc = nullptr; p.bnb_pstride = 0;
   hipStream_t st = (hipStream_t)stream;
   return dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
 }

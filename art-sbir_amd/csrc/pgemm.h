@@ -16,10 +16,26 @@ struct PgArgs {
   long long M;            // output pixels
   void* y;                // bf16 output [M][ldy]
   long long ldy;
-  float* stats;           // optional [NSLOT][2][Cout] BN sums
+  float* stats;           // optional [nseg][NSLOT][2][Cout] BN sums
+  long long seg_m;        // > 0: output pixels per BN segment (one per separate forward call
+                          //      of the reference; statistics kept apart), 0: one segment
+  long long seg_stride;   // floats between the statistics of consecutive segments
   const void* res;        // optional residual (res_mode 1: same index, 2: 2x2 average-unpool)
   int res_mode;
   int dbg;                // experiment bits (ARTSBIR_PG_DBG), 0 in production
+  // fused BatchNorm-backward reduction (data gradient only, no stats): the
+  // output d is the gradient at a BN(+ReLU) output; g = d * mask is stored and
+  // sum g, sum g * xhat_t are added to bnb_slots[t] ([nseg][NSLOT][2][Cout])
+  int bnb;                // 0 off; 1: mask y_0 * msc + msh > 0; 2: mask bnb_mask > 0
+  int bnb_nt;             // BN inputs sharing g (1 or 2)
+  const void* bnb_y[2];   // bf16 [M][ldy] BN inputs (pre-BN convolution outputs)
+  const float* bnb_mean[2];
+  const float* bnb_istd[2];
+  const float* bnb_msc;   // bnb 1: scale / shift of the BN before the ReLU
+  const float* bnb_msh;
+  const void* bnb_mask;   // bnb 2: the ReLU output (block output)
+  float* bnb_slots[2];
+  long long bnb_pstride;  // floats between the per-channel parameters of consecutive segments
 };
 
 // Weight gradient dW[co][k] += sum_m dY[m][co] * Xcol[m][k] (pwgrad.hip).

@@ -109,12 +109,20 @@ __device__ __forceinline__ float dpp_row_sum(float x) {
 }
 
 // Block-level BN statistics: every compute wave adds its reduce16 result into
-// an LDS accumulator red[2][BCH] (ds_add_f32); the last wave of the tile (LDS
-// counter) flushes it with 2*BCH global atomics into the replica slot and
-// zeroes it.  Cuts global atomics by the number of waves sharing a channel.
+// an LDS accumulator red[seg][2][BCH] (ds_add_f32); the last wave of the tile
+// (LDS counter) flushes it with 2*BCH global atomics per segment into the
+// replica slot and zeroes it.  Cuts global atomics by the number of waves
+// sharing a channel.  Segments: when one launch covers several of the
+// reference's separate forward calls (the sketch / positive / negative
+// branches, train.py:28-30), each keeps its own statistics; a tile of BPX <=
+// seg_m pixels touches at most two segments (red[0] = the tile's first).
+//
+// The same accumulator serves the fused BatchNorm-backward reduction of the
+// data-gradient epilogue (a.bnb): rows 0..2 = sum g, sum g*xhat_0, sum g*xhat_1
+// go to slots_0[0], slots_0[1] (and slots_1[0], slots_1[1]).
 template <int BCH>
 __device__ __forceinline__ void stats_flush(float* red, int* cnt, int last_count, const PgArgs& a, int bch, int slot,
-                                            int lane) {
+                                            int lane, long long bpx, int bpx_n) {
   // LDS operations of one wave complete in order; the wait makes this wave's
   // adds land before its counter increment (no global-memory fence needed)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -123,17 +131,178 @@ __device__ __forceinline__ void stats_flush(float* red, int* cnt, int last_count
   old = __shfl(old, 0, 64);
   if (old != last_count) return;
   asm volatile("" ::: "memory");
-  float* sp = a.stats + (long long)slot * 2 * a.Cout;
-  for (int i = lane; i < 2 * BCH; i += 64) {
-    const int m = i >= BCH ? 1 : 0;
-    const int ch = bch + i - m * BCH;
-    const float v = red[i];
-    red[i] = 0.f;
-    if (ch < a.Cout) atomicAdd(sp + m * a.Cout + ch, v);
+  long long seg0 = 0;
+  int nsg = 1;
+  if (a.seg_m > 0) {
+    long long last = bpx + bpx_n - 1;
+    if (last >= a.M) last = a.M - 1;
+    seg0 = bpx / a.seg_m;
+    nsg = (int)(last / a.seg_m - seg0) + 1;
+  }
+  const int nrow = (a.bnb && a.bnb_nt == 2) ? 3 : 2;
+  for (int sg = 0; sg < nsg; ++sg) {
+    const long long so = (seg0 + sg) * a.seg_stride + (long long)slot * 2 * a.Cout;
+    float* rr = red + sg * 3 * BCH;
+    for (int i = lane; i < nrow * BCH; i += 64) {
+      const int m = i / BCH;
+      const int ch = bch + i - m * BCH;
+      const float v = rr[i];
+      rr[i] = 0.f;
+      if (ch >= a.Cout) continue;
+      if (!a.bnb) {
+        atomicAdd(a.stats + so + m * a.Cout + ch, v);
+      } else if (m == 0) {
+        atomicAdd(a.bnb_slots[0] + so + ch, v);
+        if (a.bnb_nt == 2) atomicAdd(a.bnb_slots[1] + so + ch, v);
+      } else {
+        atomicAdd(a.bnb_slots[m - 1] + so + a.Cout + ch, v);
+      }
+    }
   }
 }
 
-template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI>
+// LDS accumulator half of the wave's segment (0: the tile's first segment)
+__device__ __forceinline__ int stats_rseg(const PgArgs& a, long long bpx, long long wave_px0) {
+  if (a.seg_m <= 0) return 0;
+  return (int)(wave_px0 / a.seg_m - bpx / a.seg_m);
+}
+
+// floats of the LDS statistics accumulator of a BCH-channel tile (+ counter)
+template <int BCH>
+constexpr int pg_red_bytes() {
+  return 2 * 3 * BCH * 4 + 16;
+}
+
+// Epilogue of one output tile straight from the accumulators: lane (fr, fq)
+// holds, per channel pair p and pixel tile j, channels ch0..ch0+7 of pixel px,
+// stored as one 16-B bf16 vector.  Optional, in this order: forward BN
+// statistics (sum, sum of squares of the f32 result), residual add (dgrad:
+// res_mode 1 / 2), fused BN-backward reduction (dgrad, a.bnb): the result d is
+// the gradient at a BN+ReLU output, g = d * relu-mask is stored instead and
+// sum g, sum g*xhat_t (xhat_t = (y_t - mean_t) * istd_t) are accumulated for
+// up to two BN inputs t sharing g (models.py:234 bn3 + downsample BN).  The
+// per-lane sums are reduced over the 16 pixel lanes by DPP and added to the
+// tile's LDS accumulator (stats_flush writes it out).
+template <bool BNB, int BCH, int MTC, int NTP, int WTPX, int WTCH>
+__device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
+                                            int wpx, int wch, int fr, int fq, float* red) {
+  const int HoWo = a.Ho * a.Wo;
+  const long long wpx0 = bpx + wpx * WTPX;
+  float* rb = red + stats_rseg(a, bpx, wpx0) * 3 * BCH;
+  // segment of the wave's pixels (a wave past the last pixel of a tail tile
+  // stores nothing; clamp so its parameter loads stay inside the last segment)
+  const long long wseg = a.seg_m > 0 ? (wpx0 < a.M ? wpx0 : a.M - 1) / a.seg_m : 0;
+  const bool sums = BNB || a.stats != nullptr;
+  const bool two = BNB && a.bnb_nt == 2;
+#pragma unroll
+  for (int p = 0; p < MTC / 2; ++p) {
+    const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+    const bool chok = ch0 < a.Cout;
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+    // BN-backward per-channel constants: xhat_t = y * xa_t + xb_t; mask affine
+    float xa0[8], xb0[8], xa1[8], xb1[8], ms[8], mh[8];
+    if (BNB && chok) {
+      const long long po = wseg * a.bnb_pstride + ch0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float is = a.bnb_istd[0][po + e];
+        xa0[e] = is;
+        xb0[e] = -a.bnb_mean[0][po + e] * is;
+        xa1[e] = 0.f; xb1[e] = 0.f; ms[e] = 0.f; mh[e] = 0.f;
+      }
+      if (two) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float is = a.bnb_istd[1][po + e];
+          xa1[e] = is;
+          xb1[e] = -a.bnb_mean[1][po + e] * is;
+        }
+      }
+      if (a.bnb == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { ms[e] = a.bnb_msc[po + e]; mh[e] = a.bnb_msh[po + e]; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const long long px = wpx0 + j * 16 + fr;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+      if (px < a.M && chok) {
+        if (!BNB && a.stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+        }
+        if (a.res_mode) {
+          long long ri = px;
+          float sc = 1.f;
+          if (a.res_mode == 2) {
+            const long long img = px / HoWo;
+            const int rem = (int)(px - img * HoWo);
+            const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+            ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+            sc = 0.25f;
+          }
+          const Vec16<bf16> rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + ch0);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += sc * to_f(rv.v[e]);
+        }
+        if constexpr (BNB) {
+          const long long off = px * a.ldy + ch0;
+          const Vec16<bf16> y0 = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + off);
+          bool keep[8];
+          if (a.bnb == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) keep[e] = to_f(y0.v[e]) * ms[e] + mh[e] > 0.f;
+          } else {
+            const Vec16<bf16> mk = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + off);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) keep[e] = to_f(mk.v[e]) > 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            v[e] = keep[e] ? v[e] : 0.f;
+            s1[e] += v[e];
+            s2[e] += v[e] * (to_f(y0.v[e]) * xa0[e] + xb0[e]);
+          }
+          if (two) {
+            const Vec16<bf16> y1 = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + off);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s3[e] += v[e] * (to_f(y1.v[e]) * xa1[e] + xb1[e]);
+          }
+        }
+        Vec16<bf16> o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+        st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+      }
+    }
+    if (sums) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
+      if (two) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s3[e] = dpp_row_sum(s3[e]);
+      }
+      if (fr == 15 && chok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(rb + (ch0 - bch) + e, s1[e]);
+          atomicAdd(rb + BCH + (ch0 - bch) + e, s2[e]);
+        }
+        if (two) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) atomicAdd(rb + 2 * BCH + (ch0 - bch) + e, s3[e]);
+        }
+      }
+    }
+  }
+}
+
+template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB>
 __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   constexpr int NW = WPX * WCH;
   constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
@@ -146,9 +315,9 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   constexpr int LPS_LO = IPX + ICH_TOT / NW;                   // ... waves with one fewer
   static_assert(IPX >= 1 && IPX * 8 * NW == BPX, "pixel loader");
   static_assert(MTC % 2 == 0 && WTCH % 32 == 0, "channel pairs");
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + 2 * BCH * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + pg_red_bytes<BCH>()];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 2 * BCH * 4);
+  int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 6 * BCH * 4);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -265,8 +434,9 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     }
   };
 
-  if (a.stats) {
-    for (int i = tid; i < 2 * BCH; i += 64 * NW) red[i] = 0.f;
+  const bool sums = BNB || a.stats != nullptr;
+  if (sums) {
+    for (int i = tid; i < 6 * BCH; i += 64 * NW) red[i] = 0.f;
     if (tid == 0) *red_cnt = 0;
   }
   const int nk = (a.K + 63) / 64;
@@ -286,60 +456,10 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     compute(kt % NSTAGE);
   }
 
-  // ---- epilogue from registers: lane (fr, fq) holds, per channel pair p and
-  // pixel tile j, channels ch0..ch0+7 of pixel px
+  // ---- epilogue from registers
   const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
-#pragma unroll
-  for (int p = 0; p < MTC / 2; ++p) {
-    const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
-    const bool chok = ch0 < a.Cout;
-    float s1[8], s2[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-#pragma unroll
-    for (int j = 0; j < NTP; ++j) {
-      const long long px = bpx + wpx * WTPX + j * 16 + fr;
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
-      if (px < a.M && chok) {
-        if (a.stats) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
-        }
-        if (a.res_mode) {
-          long long ri = px;
-          float sc = 1.f;
-          if (a.res_mode == 2) {
-            const long long img = px / HoWo;
-            const int rem = (int)(px - img * HoWo);
-            const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-            ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
-            sc = 0.25f;
-          }
-          const Vec16<bf16> rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + ch0);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += sc * to_f(rv.v[e]);
-        }
-        Vec16<bf16> o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
-        st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
-      }
-    }
-    if (a.stats) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
-      if (fr == 15 && chok) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          atomicAdd(red + (ch0 - bch) + e, s1[e]);
-          atomicAdd(red + BCH + (ch0 - bch) + e, s2[e]);
-        }
-      }
-    }
-  }
-  if (a.stats) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane);
+  pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
+  if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
 }
 
 // ---------------------------------------------------------------------------
@@ -352,7 +472,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
 // tile's epilogue stores drain, which is what the low-K layers (1-5 K-steps
 // per tile) need to stream at HBM rate.
 // ---------------------------------------------------------------------------
-template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI>
+template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB>
 __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int BPX = 256, NWC = 8, NWL = 4;
   static_assert(WPX * WCH == NWC, "compute waves");
@@ -363,9 +483,9 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int WTPX = BPX / WPX, WTCH = BCH / WCH;
   constexpr int NTP = WTPX / 16, MTC = WTCH / 16;
   static_assert(LCH >= 1 && MTC % 2 == 0, "shape");
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + 2 * BCH * 4 + 16];
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + pg_red_bytes<BCH>()];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
-  int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 2 * BCH * 4);
+  int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 6 * BCH * 4);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -477,8 +597,9 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   }
 
   // -------------------------------------------------------------- compute
-  if (a.stats) {  // ordered before any use by the first stage barrier
-    for (int i = tid; i < 2 * BCH; i += 64 * NWC) red[i] = 0.f;
+  const bool sums = BNB || a.stats != nullptr;
+  if (sums) {  // ordered before any use by the first stage barrier
+    for (int i = tid; i < 6 * BCH; i += 64 * NWC) red[i] = 0.f;
     if (tid == 0) *red_cnt = 0;
   }
   const int wpx = wid % WPX, wch = wid / WPX;
@@ -524,59 +645,10 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
     const long long bpx = (t / ntc) * BPX;
     const int bch = (int)(t % ntc) * BCH;
     const int slot = (int)(t % ARTSBIR_NSLOT);
-#pragma unroll
-    for (int p = 0; p < MTC / 2; ++p) {
-      const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
-      const bool chok = ch0 < a.Cout;
-      float s1[8], s2[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
-#pragma unroll
-      for (int j = 0; j < NTP; ++j) {
-        const long long px = bpx + wpx * WTPX + j * 16 + fr;
-        float v[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
-        if (px < a.M && chok) {
-          if (a.stats) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
-          }
-          if (a.res_mode) {
-            long long ri = px;
-            float sc = 1.f;
-            if (a.res_mode == 2) {
-              const long long img = px / HoWo;
-              const int rem = (int)(px - img * HoWo);
-              const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-              ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
-              sc = 0.25f;
-            }
-            const Vec16<bf16> rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + ch0);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += sc * to_f(rv.v[e]);
-          }
-          Vec16<bf16> o;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
-          st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
-        }
-      }
-      if (a.stats) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
-        if (fr == 15 && chok) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            atomicAdd(red + (ch0 - bch) + e, s1[e]);
-            atomicAdd(red + BCH + (ch0 - bch) + e, s2[e]);
-          }
-        }
-      }
-    }
+    pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
     // the flushing wave zeroes red before it reaches the next stage barrier,
     // and no wave adds for tile ti+1 before passing that barrier
-    if (a.stats) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane);
+    if (sums) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane, bpx, BPX);
 #pragma unroll
     for (int i = 0; i < MTC; ++i)
 #pragma unroll
@@ -599,15 +671,23 @@ static const PgCfg kCfgs[] = {
     {256, 32, 4 * (256 + 32) * 128, 512, 0.70f},    // 4: 256 x 32, 4 stages
 };
 
-template <bool MULTI>
+template <bool MULTI, bool BNB>
 static void pg_launch_cfg(int c, const PgArgs& a, long long tiles, hipStream_t st) {
+  const dim3 g((unsigned)tiles);
   switch (c) {
-    case 0: hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 2, 2, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
-    case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, MULTI>), dim3((unsigned)tiles), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI>), dim3((unsigned)tiles), dim3(512), 0, st, a); break;
+    case 0: hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 2, 2, MULTI, BNB>), g, dim3(512), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, MULTI, BNB>), g, dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, MULTI, BNB>), g, dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, MULTI, BNB>), g, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI, BNB>), g, dim3(512), 0, st, a); break;
   }
+}
+
+template <bool MULTI, bool BNB>
+static void pstream_launch(int bch, const PgArgs& a, int grid, int ntl, hipStream_t st) {
+  if (bch == 32) hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, MULTI, BNB>), dim3(grid), dim3(768), 0, st, a, ntl);
+  else if (bch == 64) hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, MULTI, BNB>), dim3(grid), dim3(768), 0, st, a, ntl);
+  else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, MULTI, BNB>), dim3(grid), dim3(768), 0, st, a, ntl);
 }
 
 static bool pg_supported(const PgArgs& a, bool& multi) {
@@ -620,6 +700,9 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
   const long long HoWo = (long long)a.Ho * a.Wo;
   if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 > 0x7fffffffLL) return false;
   if (a.M > (1LL << 40)) return false;
+  // segments: every wave's pixels in one segment, a tile in at most two
+  if (a.seg_m > 0 && (a.seg_m % 64 != 0 || a.seg_m < 256 || a.M % a.seg_m != 0)) return false;
+  if (a.bnb && (a.stats || a.Cout % 8 != 0)) return false;
   return true;
 }
 
@@ -634,15 +717,12 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
     const int grid = (int)(nt < 256 ? nt : 256);
     const int ntl = (int)nt;
     set_last_kernel(bch == 32 ? "pstream_kernel<32>" : bch == 64 ? "pstream_kernel<64>" : "pstream_kernel<128>");
-    if (bch == 32) {
-      if (multi) hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, true>), dim3(grid), dim3(768), 0, st, a, ntl);
-      else hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, false>), dim3(grid), dim3(768), 0, st, a, ntl);
-    } else if (bch == 64) {
-      if (multi) hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, true>), dim3(grid), dim3(768), 0, st, a, ntl);
-      else hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false>), dim3(grid), dim3(768), 0, st, a, ntl);
+    if (a.bnb) {
+      if (multi) pstream_launch<true, true>(bch, a, grid, ntl, st);
+      else pstream_launch<false, true>(bch, a, grid, ntl, st);
     } else {
-      if (multi) hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, true>), dim3(grid), dim3(768), 0, st, a, ntl);
-      else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, false>), dim3(grid), dim3(768), 0, st, a, ntl);
+      if (multi) pstream_launch<true, false>(bch, a, grid, ntl, st);
+      else pstream_launch<false, false>(bch, a, grid, ntl, st);
     }
     return true;
   }
@@ -653,8 +733,13 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   static const char* names[] = {"pgemm_kernel<256,256>", "pgemm_kernel<256,128>", "pgemm_kernel<256,64>",
                                 "pgemm_kernel<128,128>", "pgemm_kernel<256,32>"};
   set_last_kernel(names[c]);
-  if (multi) pg_launch_cfg<true>(c, a, tiles, st);
-  else pg_launch_cfg<false>(c, a, tiles, st);
+  if (a.bnb) {
+    if (multi) pg_launch_cfg<true, true>(c, a, tiles, st);
+    else pg_launch_cfg<false, true>(c, a, tiles, st);
+  } else {
+    if (multi) pg_launch_cfg<true, false>(c, a, tiles, st);
+    else pg_launch_cfg<false, false>(c, a, tiles, st);
+  }
   return true;
 }
 

@@ -7,14 +7,20 @@ autograd record the backward.  Here the whole encoder forward and backward are
 sequenced explicitly over the C-ABI kernels:
 
   * activations live in HBM as NHWC tensors of the compute dtype (bf16 for
-    throughput, f32 for parity); only the raw convolution outputs y are stored,
-    BatchNorm+ReLU is re-applied on load by the consuming convolution and by
-    the weight-gradient GEMM (in_scale/in_shift/in_relu), so the normalised
-    activations are never materialised except where an AvgPool or the
-    residual join needs them;
+    throughput, f32 for parity); the raw convolution outputs y are stored and
+    BatchNorm+ReLU(+AvgPool) is applied once (act_pool / block_out), producing
+    the next convolution's input, which is also the weight-gradient operand;
   * BN batch statistics come out of the convolution epilogue (sum / sum of
     squares) and are finalised per call -> per-branch statistics exactly as the
     reference's three separate forward calls (train.py:28-30);
+  * several forward calls can run as one batch of G SEGMENTS (the triplet's
+    sketch / positive / negative, ModifiedResNet.forward_branches): every
+    GEMM runs once over G x B images, while BatchNorm statistics, running
+    statistics and the BN backward stay per segment — the same arithmetic as G
+    separate calls;
+  * the BatchNorm backward reduction (sum g, sum g*xhat) of a BN whose output
+    gradient comes out of a data-gradient GEMM is fused into that GEMM's
+    epilogue (artsbir_conv2d_dgrad_bnb), which stores g = d * relu-mask;
   * weights are re-packed from the f32 parameters (reference layout, so
     state_dicts interchange) into the kernel layouts whenever a parameter
     changes (torch version counter or an optimizer step of optim.Adam here).
@@ -25,7 +31,9 @@ native library is missing.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+import ctypes
+import os
+from dataclasses import dataclass
 
 import torch
 
@@ -35,6 +43,8 @@ from _hip import call, ptr
 NSLOT = _hip.NSLOT
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+# ARTSBIR_FUSE_BNB=0 runs the BN-backward reduction as its own pass (A/B tests)
+FUSE_BNB = os.environ.get("ARTSBIR_FUSE_BNB", "1") != "0"
 
 # bumped by optim.Adam (which updates parameters through raw pointers, invisible
 # to torch's version counters) so packed weights are rebuilt after every step
@@ -49,27 +59,45 @@ def _s():
     return _hip.stream()
 
 
+def _at(t, i):
+    """raw pointer of image i of an NHWC tensor (None -> NULL)"""
+    return None if t is None else t[i].data_ptr()
+
+
 @dataclass
 class BNState:
-    """per-call batch-norm parameters: mean, istd, scale, shift [4][C] f32"""
+    """per-call batch-norm parameters of G segments: buf [G][4][C] f32 holds the
+    mean, istd, scale, shift of each segment; count = elements per segment."""
     buf: torch.Tensor
     count: float
 
     @property
+    def G(self):
+        return self.buf.shape[0]
+
+    def seg(self, i):
+        return BNState(self.buf[i:i + 1], self.count)
+
+    @property
+    def pstride(self):
+        """floats between the parameters of consecutive segments"""
+        return 4 * self.buf.shape[2]
+
+    @property
     def mean(self):
-        return self.buf[0]
+        return self.buf[0, 0]
 
     @property
     def istd(self):
-        return self.buf[1]
+        return self.buf[0, 1]
 
     @property
     def scale(self):
-        return self.buf[2]
+        return self.buf[0, 2]
 
     @property
     def shift(self):
-        return self.buf[3]
+        return self.buf[0, 3]
 
 
 @dataclass
@@ -93,6 +121,7 @@ class Engine:
         self._packed = None
         self._packed_key = None
         self.dtype = torch.float32
+        self._G = 1
 
     # ------------------------------------------------------------------ utils
     @property
@@ -182,54 +211,80 @@ class Engine:
         y = self._empty(B, Ho, Wo, cout, device=a.t.device)
         d = self._desc(B, H, W, C, cout, R, S, stride, pad)
         bn = a.bn
+        flops = 2.0 * B * Ho * Wo * cout * R * S * C
+        if stats_buf is not None and bn is None:
+            # BN statistics per segment (one launch for all G forward calls)
+            call("artsbir_conv2d_fwd_seg", d, ptr(a.t), ptr(fw), ptr(y), self._G, ptr(stats_buf), _s(),
+                 kernel="auto", flops=flops)
+            return y
+        if bn is not None and bn.G != 1:
+            raise NotImplementedError("affine-on-load convolutions take one segment")
         call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None,
              ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None, a.relu,
-             ptr(stats_buf), _s(), kernel="auto",
-             flops=2.0 * B * Ho * Wo * cout * R * S * C)
+             ptr(stats_buf), _s(), kernel="auto", flops=flops)
         return y
 
     def _bn(self, bnmod, stats_buf, count, train):
+        """finalise the BN of every segment in order (running statistics are
+        updated once per segment, as by the reference's consecutive calls)"""
         C = bnmod.num_features
-        st = BNState(torch.empty(4, C, dtype=torch.float32, device=bnmod.weight.device), float(count))
-        call("artsbir_bn_finalize", ptr(stats_buf) if train else None, C, float(count),
-             ptr(bnmod.weight.detach()), ptr(bnmod.bias.detach()),
-             ptr(bnmod.running_mean), ptr(bnmod.running_var),
-             ptr(bnmod.num_batches_tracked) if train else None,
-             BN_MOMENTUM, BN_EPS, 1 if train else 0,
-             ptr(st.mean), ptr(st.istd), ptr(st.scale), ptr(st.shift), _s())
+        G = self._G
+        st = BNState(torch.empty(G, 4, C, dtype=torch.float32, device=bnmod.weight.device), float(count))
+        per = 2 * NSLOT * C
+        for i in range(G):
+            call("artsbir_bn_finalize", ptr(stats_buf[i * per:]) if train else None, C, float(count),
+                 ptr(bnmod.weight.detach()), ptr(bnmod.bias.detach()),
+                 ptr(bnmod.running_mean), ptr(bnmod.running_var),
+                 ptr(bnmod.num_batches_tracked) if train else None,
+                 BN_MOMENTUM, BN_EPS, 1 if train else 0,
+                 ptr(st.buf[i, 0]), ptr(st.buf[i, 1]), ptr(st.buf[i, 2]), ptr(st.buf[i, 3]), _s())
         return st
 
     def _conv_bn(self, a, conv, bnmod, fw, stride, pad, train, stats):
         cout, _, R, S = conv.weight.shape
-        sb = stats.take(cout) if train else None
+        sb = stats.take(cout * self._G) if train else None
         y = self._conv(a, fw, cout, R, S, stride, pad, sb)
         B, Ho, Wo, _ = y.shape
-        return y, self._bn(bnmod, sb, B * Ho * Wo, train)
+        return y, self._bn(bnmod, sb, (B // self._G) * Ho * Wo, train)
 
     def _act_pool(self, x, bn, relu, pool):
         B, H, W, C = x.shape
         p = max(pool, 1)
         out = self._empty(B, H // p, W // p, C, device=x.device)
-        call("artsbir_act_pool", self.dt, ptr(x), ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None,
-             relu, pool, B, H, W, C, ptr(out), _s())
+        G = bn.G if bn is not None else 1
+        Bs = B // G
+        for s in range(G):
+            sb = bn.seg(s) if bn is not None else None
+            call("artsbir_act_pool", self.dt, _at(x, s * Bs), ptr(sb.scale) if sb else None,
+                 ptr(sb.shift) if sb else None, relu, pool, Bs, H, W, C, _at(out, s * Bs), _s())
         return out
 
     # ---------------------------------------------------------------- forward
-    def forward(self, x: torch.Tensor, train: bool, save: bool):
-        if not x.is_cuda:
-            raise RuntimeError("ModifiedResNet on libartsbir_hip runs on the GPU: move model and input to cuda")
+    def forward(self, x, train: bool, save: bool):
+        """x: [B,3,R,R] or a list of G such batches (G separate reference forward
+        calls run as one batch of G BN segments).  Returns ([G*B, out], ctx)."""
+        xs = list(x) if isinstance(x, (list, tuple)) else [x]
+        for xi in xs:
+            if not xi.is_cuda:
+                raise RuntimeError("ModifiedResNet on libartsbir_hip runs on the GPU: move model and input to cuda")
+            if tuple(xi.shape) != tuple(xs[0].shape):
+                raise ValueError("forward_branches: every branch needs the same input shape")
+        G = len(xs)
+        self._G = G
         m = self.model
         pk = self.packed()
-        x = x.contiguous().float()
-        B, cin, R, R2 = x.shape
-        dev = x.device
-        nstat = 2 * NSLOT * m.total_bn_channels() if train else 0
+        Bs, cin, R, R2 = xs[0].shape
+        B = G * Bs
+        dev = xs[0].device
+        nstat = 2 * NSLOT * m.total_bn_channels() * G if train else 0
         stats = _Arena(torch.zeros(max(nstat, 1), dtype=torch.float32, device=dev), NSLOT * 2)
-        ctx = {"train": train, "B": B}
+        ctx = {"train": train, "B": B, "G": G}
 
         # stem (models.py:345-350)
         x0 = self._empty(B, R, R2, 8, device=dev)
-        call("artsbir_pack_input", self.dt, ptr(x), B, cin, R, R2, ptr(x0), _s())
+        for i, xi in enumerate(xs):
+            xi = xi.contiguous().float()
+            call("artsbir_pack_input", self.dt, ptr(xi), Bs, cin, R, R2, _at(x0, i * Bs), _s())
         (fw1, _), (fw2, _), (fw3, _) = pk["stem"]
         y1, b1 = self._conv_bn(Act(x0), m.conv1, m.bn1, fw1, 2, 1, train, stats)
         a1 = self._act_pool(y1, b1, 1, 0)
@@ -273,10 +328,16 @@ class Engine:
                 din = h
             yd, bd = self._conv_bn(Act(din), blk.downsample[1], blk.downsample[2], bp["down"][0], 1, 0, train, stats)
         out = torch.empty_like(y3)
-        rows = out.numel() // out.shape[-1]
-        call("artsbir_block_out", self.dt, ptr(y3), ptr(b3.scale), ptr(b3.shift),
-             ptr(yd), ptr(bd.scale) if bd else None, ptr(bd.shift) if bd else None,
-             None if yd is not None else ptr(h), rows, out.shape[-1], ptr(out), _s())
+        G = self._G
+        Bs = B // G
+        C = out.shape[-1]
+        rows = out[0].numel() // C * Bs
+        for g in range(G):
+            s3 = b3.seg(g)
+            sd = bd.seg(g) if bd is not None else None
+            call("artsbir_block_out", self.dt, _at(y3, g * Bs), ptr(s3.scale), ptr(s3.shift),
+                 _at(yd, g * Bs), ptr(sd.scale) if sd else None, ptr(sd.shift) if sd else None,
+                 None if yd is not None else _at(h, g * Bs), rows, C, _at(out, g * Bs), _s())
         ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, b1=b1, b2=b2, b3=b3, bd=bd)
         return out, ctx
 
@@ -318,13 +379,17 @@ class Engine:
             raise NotImplementedError("backward is implemented for train-mode BatchNorm (as in train.py)")
         m = self.model
         pk = self.packed()
+        self._G = G = ctx["G"]
         dev = dout.device
         grads = self.grad_buffer(dev)
-        ws = _Arena(torch.zeros(max(2 * NSLOT * m.total_bn_channels() * 2, 1), dtype=torch.float32, device=dev),
+        ws = _Arena(torch.zeros(max(2 * NSLOT * m.total_bn_channels() * 2 * G, 1), dtype=torch.float32, device=dev),
                     NSLOT * 2)
         dh = self._attnpool_bwd(m.attnpool, pk, ctx["attn"], dout.contiguous().float(), grads)
-        for blk, bp, c in zip(reversed(m.blocks()), reversed(pk["blocks"]), reversed(ctx["blocks"])):
-            dh = self._block_bwd(blk, bp, c, dh, grads, ws)
+        blocks, bps, cs = m.blocks(), pk["blocks"], ctx["blocks"]
+        fused = None
+        for i in reversed(range(len(blocks))):
+            prev = (blocks[i - 1], cs[i - 1]) if i > 0 else None
+            dh, fused = self._block_bwd(blocks[i], bps[i], cs[i], dh, grads, ws, fused, prev)
         self._stem_bwd(m, pk, ctx["stem"], dh, grads, ws)
         return grads
 
@@ -365,39 +430,103 @@ class Engine:
         return dh
 
     def _bn_bwd(self, kind, d, targets, bnmods, ws, grads, mask=None, mask_bn=None, pool=0, gout=None):
-        """targets: list of (y, BNState); returns list of dy tensors"""
+        """BatchNorm backward as a reduce pass + apply pass per segment.
+        targets: list of (y, BNState); returns list of dy tensors"""
+        y0 = targets[0][0]
+        B, H, W, C = y0.shape
+        G = self._G
+        Bs = B // G
+        dys = [torch.empty_like(y) for y, _ in targets]
+        for s in range(G):
+            desc = _hip.BnBwdDesc()
+            desc.dtype = self.dt
+            desc.kind = kind
+            desc.pool = pool
+            desc.d = _at(d, s * Bs)
+            desc.mask = _at(mask, s * Bs)
+            mb = mask_bn.seg(s) if mask_bn is not None else None
+            desc.mask_scale = ptr(mb.scale) if mb else None
+            desc.mask_shift = ptr(mb.shift) if mb else None
+            desc.ntarget = len(targets)
+            slots = []
+            for i, (y, st) in enumerate(targets):
+                ss = st.seg(s)
+                desc.y[i] = _at(y, s * Bs)
+                desc.mean[i] = ptr(ss.mean)
+                desc.istd[i] = ptr(ss.istd)
+                sl = ws.take(C)
+                slots.append(sl)
+                desc.slots[i] = ptr(sl)
+            desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
+            call("artsbir_bn_bwd_reduce", desc, _s())
+            self._bn_apply(desc, targets, bnmods, slots, grads, dys, s)
+            desc.gout = _at(gout, s * Bs)
+            call("artsbir_bn_bwd_apply", desc, _s())
+        return dys
+
+    def _bn_apply(self, desc, targets, bnmods, slots, grads, dys, s):
+        """finalise segment s (parameter gradients += , apply coefficients) and
+        point desc at its outputs; the caller launches the apply."""
+        C = desc.C
+        count = float(desc.B * desc.H * desc.W)
+        desc._keep = []
+        for i, ((y, st), bnm) in enumerate(zip(targets, bnmods)):
+            ss = st.seg(s)
+            coef = torch.empty(3, C, dtype=torch.float32, device=y.device)
+            call("artsbir_bn_bwd_finalize", ptr(slots[i]), C, count, ptr(bnm.weight.detach()),
+                 ptr(ss.istd), ptr(grads[bnm.weight]), ptr(grads[bnm.bias]), ptr(coef), _s())
+            desc._keep.append(coef)
+            desc.coef[i] = ptr(coef)
+            desc.dy[i] = _at(dys[i], s * desc.B)
+
+    def _bnb_fused_desc(self, kind, targets, ws, mask=None, mask_bn=None):
+        """descriptor of a BN-backward reduction fused into the data-gradient GEMM
+        that produces its input gradient (all G segments; slots [G][NSLOT][2][C])"""
         y0 = targets[0][0]
         B, H, W, C = y0.shape
         desc = _hip.BnBwdDesc()
         desc.dtype = self.dt
         desc.kind = kind
-        desc.pool = pool
-        desc.d = ptr(d)
+        desc.pool = 0
         desc.mask = ptr(mask)
-        desc.mask_scale = ptr(mask_bn.scale) if mask_bn else None
-        desc.mask_shift = ptr(mask_bn.shift) if mask_bn else None
+        desc.mask_scale = ptr(mask_bn.scale) if mask_bn is not None else None
+        desc.mask_shift = ptr(mask_bn.shift) if mask_bn is not None else None
         desc.ntarget = len(targets)
-        slots, coefs, dys = [], [], []
+        slots = []
         for i, (y, st) in enumerate(targets):
             desc.y[i] = ptr(y)
             desc.mean[i] = ptr(st.mean)
             desc.istd[i] = ptr(st.istd)
-            sl = ws.take(C)
+            sl = ws.take(C * self._G)
             slots.append(sl)
             desc.slots[i] = ptr(sl)
         desc.B, desc.H, desc.W, desc.C = B, H, W, C
-        call("artsbir_bn_bwd_reduce", desc, _s())
-        for i, ((y, st), bnm) in enumerate(zip(targets, bnmods)):
-            coef = torch.empty(3, C, dtype=torch.float32, device=y.device)
-            call("artsbir_bn_bwd_finalize", ptr(slots[i]), C, float(B * H * W), ptr(bnm.weight.detach()),
-                 ptr(st.istd), ptr(grads[bnm.weight]), ptr(grads[bnm.bias]), ptr(coef), _s())
-            coefs.append(coef)
-            dy = torch.empty_like(y)
-            dys.append(dy)
-            desc.coef[i] = ptr(coef)
-            desc.dy[i] = ptr(dy)
-        desc.gout = ptr(gout)
-        call("artsbir_bn_bwd_apply", desc, _s())
+        return desc, slots, targets
+
+    def _bn_finish(self, g, fused, bnmods, grads):
+        """apply pass of a fused BN-backward: g (masked) -> dy per target"""
+        _, slots, targets = fused
+        y0 = targets[0][0]
+        B, H, W, C = y0.shape
+        G = self._G
+        Bs = B // G
+        per = 2 * NSLOT * C
+        dys = [torch.empty_like(y) for y, _ in targets]
+        for s in range(G):
+            desc = _hip.BnBwdDesc()
+            desc.dtype = self.dt
+            desc.kind = 2
+            desc.pool = 0
+            desc.d = _at(g, s * Bs)
+            desc.ntarget = len(targets)
+            for i, (y, st) in enumerate(targets):
+                ss = st.seg(s)
+                desc.y[i] = _at(y, s * Bs)
+                desc.mean[i] = ptr(ss.mean)
+                desc.istd[i] = ptr(ss.istd)
+            desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
+            self._bn_apply(desc, targets, bnmods, [sl[s * per:] for sl in slots], grads, dys, s)
+            call("artsbir_bn_bwd_apply", desc, _s())
         return dys
 
     def _wgrad(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):
@@ -417,52 +546,95 @@ class Engine:
         if target is not g:
             call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
 
-    def _dgrad(self, dy, dw, conv, pad, out_shape, res=None, res_mode=0):
+    def _dgrad(self, dy, dw, conv, pad, out_shape, res=None, res_mode=0, fused=None):
         B, H, W, C = out_shape
         co, _, R, S = conv.weight.shape
         dx = self._empty(B, H, W, C, device=dy.device)
         d = self._desc(B, H, W, C, co, R, S, 1, pad)
-        call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
-             kernel="auto", flops=2.0 * B * H * W * C * R * S * co)
+        flops = 2.0 * B * H * W * C * R * S * co
+        if fused is None:
+            call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
+                 kernel="auto", flops=flops)
+        else:
+            call("artsbir_conv2d_dgrad_bnb", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode,
+                 ctypes.byref(fused[0]), self._G, 4 * C, _s(), kernel="auto", flops=flops)
         return dx
 
-    def _block_bwd(self, blk, bp, c, dout, grads, ws):
+    def _block_bwd(self, blk, bp, c, dout, grads, ws, fused_res=None, prev=None):
+        """backward of one Bottleneck.  dout: gradient of the block output, or —
+        when fused_res is given — g = dout * relu-mask with the block-output BN
+        reduction already done by the producing data-gradient GEMM.  prev: the
+        (Bottleneck, ctx) feeding this block, whose output BN reduction is fused
+        into this block's last data gradient.  Returns (dh, fused for prev)."""
         h, y1, y2, p2, y3, yd, pd, out = (c[k] for k in ("h", "y1", "y2", "p2", "y3", "yd", "pd", "out"))
         b1, b2, b3, bd = c["b1"], c["b2"], c["b3"], c["bd"]
         s = blk.stride
         has_ds = blk.downsample is not None
-        targets = [(y3, b3)] + ([(yd, bd)] if has_ds else [])
         bnmods = [blk.bn3] + ([blk.downsample[2]] if has_ds else [])
-        gid = None if has_ds else torch.empty_like(dout)
-        dys = self._bn_bwd(0, dout, targets, bnmods, ws, grads, mask=out, gout=gid)
+        if fused_res is not None:
+            dys = self._bn_finish(dout, fused_res, bnmods, grads)
+            gid = dout  # the identity branch's gradient is g itself
+        else:
+            targets = [(y3, b3)] + ([(yd, bd)] if has_ds else [])
+            gid = None if has_ds else torch.empty_like(dout)
+            dys = self._bn_bwd(0, dout, targets, bnmods, ws, grads, mask=out, gout=gid)
         dy3 = dys[0]
         c3in = Act(p2)
         self._wgrad(dy3, c3in, blk.conv3, 1, 0, grads)
-        dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3in.shape[:3] + (blk.conv3.weight.shape[1],))
-        dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
+        c3out = c3in.shape[:3] + (blk.conv3.weight.shape[1],)
+        if s == 1 and FUSE_BNB:
+            f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
+            g2 = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out, fused=f2)
+            dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
+        else:
+            dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out)
+            dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
         self._wgrad(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
-        da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
-        dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
+        if FUSE_BNB:
+            f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
+            g1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape, fused=f1)
+            dy1, = self._bn_finish(g1, f1, [blk.bn1], grads)
+        else:
+            da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
+            dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
         self._wgrad(dy1, Act(h), blk.conv1, 1, 0, grads)
         if has_ds:
             dyd = dys[1]
             din = pd if s > 1 else h
             dconv = blk.downsample[1]
             self._wgrad(dyd, Act(din), dconv, 1, 0, grads)
-            dpd = self._dgrad(dyd, bp["down"][1], dconv, 0, din.shape)
-            return self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=dpd, res_mode=2 if s > 1 else 1)
-        return self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=gid, res_mode=1)
+            res = self._dgrad(dyd, bp["down"][1], dconv, 0, din.shape)
+            res_mode = 2 if s > 1 else 1
+        else:
+            res, res_mode = gid, 1
+        fprev = None
+        if prev is not None and FUSE_BNB:
+            pblk, pc = prev
+            ptargets = [(pc["y3"], pc["b3"])] + ([(pc["yd"], pc["bd"])] if pblk.downsample is not None else [])
+            fprev = self._bnb_fused_desc(0, ptargets, ws, mask=pc["out"])
+        dh = self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=res, res_mode=res_mode, fused=fprev)
+        return dh, fprev
 
     def _stem_bwd(self, m, pk, c, dh, grads, ws):
         x0, y1, y2, y3, b1, b2, b3 = (c[k] for k in ("x0", "y1", "y2", "y3", "b1", "b2", "b3"))
         (_, _), (_, dw2), (_, dw3) = pk["stem"]
         dy3, = self._bn_bwd(1, dh, [(y3, b3)], [m.bn3], ws, grads, mask_bn=b3, pool=2)
         self._wgrad(dy3, Act(c["a2"]), m.conv3, 1, 1, grads)
-        da2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape)
-        dy2, = self._bn_bwd(1, da2, [(y2, b2)], [m.bn2], ws, grads, mask_bn=b2)
+        if FUSE_BNB:
+            f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
+            g2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape, fused=f2)
+            dy2, = self._bn_finish(g2, f2, [m.bn2], grads)
+        else:
+            da2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape)
+            dy2, = self._bn_bwd(1, da2, [(y2, b2)], [m.bn2], ws, grads, mask_bn=b2)
         self._wgrad(dy2, Act(c["a1"]), m.conv2, 1, 1, grads)
-        da1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape)
-        dy1, = self._bn_bwd(1, da1, [(y1, b1)], [m.bn1], ws, grads, mask_bn=b1)
+        if FUSE_BNB:
+            f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
+            g1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape, fused=f1)
+            dy1, = self._bn_finish(g1, f1, [m.bn1], grads)
+        else:
+            da1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape)
+            dy1, = self._bn_bwd(1, da1, [(y1, b1)], [m.bn1], ws, grads, mask_bn=b1)
         self._wgrad(dy1, Act(x0), m.conv1, 2, 1, grads)
 
 

@@ -126,6 +126,30 @@ class _EncoderFunction(torch.autograd.Function):
         return (None, None) + (None,) * ctx.nparams
 
 
+class _EncoderBranchesFunction(torch.autograd.Function):
+    """G forward calls of the reference (train.py:28-30) as one autograd node:
+    one batched launch per GEMM, BatchNorm statistics per branch."""
+
+    @staticmethod
+    def forward(ctx, model, nb, *args):
+        xs, params = args[:nb], args[nb:]
+        eng = model._hip_engine
+        eng.dtype = model.compute_dtype
+        out, state = eng.forward(list(xs), model.training, save=True)
+        ctx.state, ctx.model, ctx.dtype, ctx.nb, ctx.nparams = state, model, model.compute_dtype, nb, len(params)
+        return tuple(out.chunk(nb))
+
+    @staticmethod
+    def backward(ctx, *douts):
+        ref = next(d for d in douts if d is not None)
+        dout = torch.cat([d if d is not None else torch.zeros_like(ref) for d in douts])
+        eng = ctx.model._hip_engine
+        eng.dtype = ctx.dtype
+        eng.backward(ctx.state, dout)
+        ctx.state = None
+        return (None, None) + (None,) * (ctx.nb + ctx.nparams)
+
+
 class ModifiedResNet(nn.Module):
     """CLIP ModifiedResNet: 3-conv stem with avgpool, anti-aliased strided
     Bottlenecks, attention-pool head (models.py:275-360)."""
@@ -193,6 +217,24 @@ class ModifiedResNet(nn.Module):
     def forward(self, x):
         return self.encode(x)
 
+    def encode_branches(self, xs):
+        """[model(x) for x in xs] with the same arithmetic (per-call BatchNorm
+        batch statistics, running statistics updated once per call in order)
+        but every convolution launched once over all the calls' images."""
+        xs = list(xs)
+        if len(xs) == 1:
+            return [self.encode(xs[0])]
+        params = tuple(self.parameters())
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return list(_EncoderBranchesFunction.apply(self, len(xs), *xs, *params))
+        eng = self._hip_engine
+        eng.dtype = self.compute_dtype
+        return list(eng.forward(xs, self.training, save=False)[0].chunk(len(xs)))
+
+    def forward_branches(self, xs):
+        """the triplet's sketch / positive / negative forwards (train.py:28-30)"""
+        return self.encode_branches(xs)
+
 
 class ModifiedResNet_with_classification(ModifiedResNet):
     def __init__(self, layers, output_dim, heads=32, input_resolution=224, width=64, num_classes=125, num_classes2=0):
@@ -213,13 +255,18 @@ class ModifiedResNet_with_classification(ModifiedResNet):
             ps += list(self.classifier2.parameters())
         return ps
 
-    def forward(self, x):
+    def _heads(self, feature):
         import heads as _heads
-        feature = super().forward(x)
         classes = _heads.linear(feature, self.classifier.weight, self.classifier.bias)
         if self.num_classes2 == 0:
             return feature, classes
         return feature, classes, _heads.linear(feature, self.classifier2.weight, self.classifier2.bias)
+
+    def forward(self, x):
+        return self._heads(super().forward(x))
+
+    def forward_branches(self, xs):
+        return [self._heads(f) for f in self.encode_branches(xs)]
 
 
 class LayerNorm(nn.LayerNorm):

@@ -38,9 +38,14 @@ device = "cuda" if torch.cuda.is_available() else "cpu"
 
 
 def get_loss(loss_fn, model, elements):
-    s = model(elements[0])
-    p = model(elements[1])
-    n = model(elements[2])
+    # three forward calls (per-branch BatchNorm statistics, train.py:28-30), run
+    # as one batched encoder pass when the model offers it
+    if hasattr(model, "forward_branches") and elements[0].shape == elements[1].shape == elements[2].shape:
+        s, p, n = model.forward_branches(elements[:3])
+    else:
+        s = model(elements[0])
+        p = model(elements[1])
+        n = model(elements[2])
     if isinstance(s, torch.Tensor):
         return loss_fn(s, p, n)
     if len(s) == 2:

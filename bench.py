@@ -178,6 +178,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the live per-launch event timing")
     ap.add_argument("--no-retrieval", action="store_true", help="skip the 1M x 512 kNN leg")
+    ap.add_argument("--unbatched", dest="batched", action="store_false",
+                    help="three separate encoder calls per step instead of forward_branches")
     args = ap.parse_args()
 
     import _hip
@@ -214,7 +216,9 @@ def main():
     batch = [((t - mean) / std).contiguous() for t in (sketch, pos, neg)]
 
     def step():
-        outs = [model(x) for x in batch]
+        # the three branch forwards of train.py:28-30 (per-branch BN statistics),
+        # each GEMM launched once over the 3 x B images
+        outs = model.forward_branches(batch) if args.batched else [model(x) for x in batch]
         loss = loss_fn(*outs)
         opt.zero_grad(set_to_none=False)
         loss.backward()

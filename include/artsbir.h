@@ -74,6 +74,26 @@ int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void* dy, long l
 int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx,
                          const void* res, int res_mode, void* stream);
 
+/* conv2d_fwd without bias/affine, with BatchNorm statistics kept per SEGMENT:
+ * the N images are nseg equal consecutive groups, each one of the reference's
+ * separate forward calls (train.py:28-30 sketch / positive / negative), so one
+ * launch covers them while stats[s][slot][2][Cout] hold segment s only. */
+int artsbir_conv2d_fwd_seg(const artsbir_conv_desc* d, const void* x, const void* w, void* y, int nseg,
+                           float* stats, void* stream);
+
+/* conv2d_dgrad whose output is the gradient at the output of a BatchNorm2d(+ReLU)
+ * (models.py:199-210, 234-235): the BN-backward reduction is fused into it.  dx
+ * receives g = dx_raw * relu-mask (bnb->kind 1: y[0]*mask_scale+mask_shift > 0;
+ * kind 0: mask > 0, the block output) and bnb->slots[t] += (sum g, sum g*xhat_t)
+ * exactly as artsbir_bn_bwd_reduce; finish with artsbir_bn_bwd_finalize and
+ * artsbir_bn_bwd_apply of kind 2 (g given).  bnb->pool must be 0/1.  With nseg
+ * segments the per-channel BN parameters of segment s are at +s*param_stride
+ * floats and its slots at +s*ARTSBIR_NSLOT*2*C. */
+typedef struct artsbir_bn_bwd_desc artsbir_bn_bwd_desc;
+int artsbir_conv2d_dgrad_bnb(const artsbir_conv_desc* d, const void* dy, const void* wd, void* dx,
+                             const void* res, int res_mode, const artsbir_bn_bwd_desc* bnb, int nseg,
+                             long long param_stride, void* stream);
+
 /* ---- layout / parameter packing ---------------------------------------- */
 /* x.type(weight dtype) + NCHW -> NHWC8 (models.py:352); x [B][Cin<=8][H][W] f32. */
 int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, void* out, void* stream);
@@ -102,9 +122,10 @@ int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* 
                       void* out, void* stream);
 
 /* BatchNorm2d(train) backward, see elementwise.hip for the math. */
-typedef struct artsbir_bn_bwd_desc {
+struct artsbir_bn_bwd_desc {
   int dtype;
-  int kind;               /* 0: g = d*(mask>0) (block output); 1: g = up(d)*(y*mask_scale+mask_shift>0) */
+  int kind;               /* 0: g = d*(mask>0) (block output); 1: g = up(d)*(y*mask_scale+mask_shift>0);
+                             2: g = d (already masked, artsbir_conv2d_dgrad_bnb) */
   int pool;               /* kind 1: d is at 1/pool resolution (AvgPool backward) */
   const void* d;
   const void* mask;
@@ -119,7 +140,7 @@ typedef struct artsbir_bn_bwd_desc {
   void* dy[2];            /* apply outputs */
   void* gout;             /* apply: optional copy of g */
   int B, H, W, C;
-} artsbir_bn_bwd_desc;
+};
 int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
 /* dgamma += sum g*xhat, dbeta += sum g; coef = [gamma*istd, sum g/cnt, sum g*xhat/cnt]. */
 int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,

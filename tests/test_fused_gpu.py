@@ -1,0 +1,222 @@
+"""Batched branches (BN segments) and the BN-backward reduction fused into the
+data-gradient GEMM: kernel-level checks against torch fp32 (CPU), and the
+encoder-level check that forward_branches / fused backward give the same
+embeddings, running statistics and gradients as three separate calls with the
+unfused backward."""
+import copy
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import _hip
+
+pytestmark = pytest.mark.gpu
+
+CFGS = ["auto", "0", "1", "2", "3", "4", "10", "-2"]
+
+
+@pytest.fixture
+def cfg_env():
+    old = os.environ.get("ARTSBIR_PGEMM_CFG")
+    yield
+    if old is None:
+        os.environ.pop("ARTSBIR_PGEMM_CFG", None)
+    else:
+        os.environ["ARTSBIR_PGEMM_CFG"] = old
+
+
+def _set(cfg):
+    if cfg == "auto":
+        os.environ.pop("ARTSBIR_PGEMM_CFG", None)
+    else:
+        os.environ["ARTSBIR_PGEMM_CFG"] = cfg
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+SEG_CASES = [
+    # N (= nseg x images), nseg, H, W, C, Cout, R, pad
+    (6, 3, 16, 16, 64, 128, 3, 1),     # 256 px / segment
+    (12, 3, 8, 8, 256, 64, 1, 0),      # 256 px / segment
+    (6, 3, 32, 16, 32, 64, 3, 1),      # multi-tap C=32, 1024 px / segment
+    (6, 2, 7, 7, 512, 256, 3, 1),      # 147 px / segment: not a multiple of 64 -> per-segment fallback
+]
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("case", SEG_CASES)
+def test_conv_fwd_segment_stats(case, cfg, dev, cfg_env):
+    _set(cfg)
+    N, G, H, W, C, Co, R, pd = case
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, C, H, W, generator=g)
+    x[N // G:] += 0.5  # segments with different statistics
+    x = x.bfloat16().float()
+    w = (torch.randn(Co, C, R, R, generator=g) / (C * R * R) ** 0.5).bfloat16().float()
+    ref = F.conv2d(x, w, padding=pd)
+    y = torch.empty(N * H * W, Co, device=dev, dtype=torch.bfloat16)
+    stats = torch.zeros(G, _hip.NSLOT, 2, Co, device=dev)
+    d = _hip.conv_desc(torch.bfloat16, N, H, W, C, Co, R, R, 1, pd)
+    xd = _nhwc(x).to(dev, torch.bfloat16)
+    wd = w.permute(0, 2, 3, 1).contiguous().to(dev, torch.bfloat16)
+    _hip.call("artsbir_conv2d_fwd_seg", d, xd.data_ptr(), wd.data_ptr(), y.data_ptr(), G, stats.data_ptr(),
+              _hip.stream())
+    torch.cuda.synchronize()
+    out = y.float().cpu().view(N, H, W, Co).permute(0, 3, 1, 2)
+    assert torch.allclose(out, ref, atol=3e-2, rtol=1e-2), (out - ref).abs().max()
+    s = stats.sum(1).cpu()
+    for k in range(G):
+        r2 = ref[k * N // G:(k + 1) * N // G].permute(0, 2, 3, 1).reshape(-1, Co)
+        assert torch.allclose(s[k, 0], r2.sum(0), atol=5e-2, rtol=1e-3), k
+        assert torch.allclose(s[k, 1], (r2 * r2).sum(0), atol=5e-2, rtol=1e-3), k
+
+
+BNB_CASES = [
+    # N, nseg, H, W, Cin (= BN channels), Cout (of the forward conv), R, pad, kind, ntarget, res_mode
+    (4, 1, 8, 8, 64, 64, 3, 1, 1, 1, 0),       # ACT, 3x3
+    (6, 3, 16, 16, 128, 64, 1, 0, 1, 1, 0),    # ACT, segments
+    (4, 2, 16, 16, 256, 64, 1, 0, 0, 2, 1),    # RES (bn3 + downsample), residual add
+    (6, 3, 16, 16, 256, 64, 1, 0, 0, 1, 2),    # RES, avg-unpool residual
+    (4, 2, 16, 16, 32, 64, 3, 1, 1, 1, 0),     # stem-like: 64-ch dY -> 32-ch dX
+]
+
+
+def _bnb_reference(d, kind, ys, means, istds, msc, msh, mask):
+    """g = d*mask, sum g, sum g*xhat_t (f64) for one segment; tensors [n, C]"""
+    if kind == 1:
+        keep = (ys[0] * msc + msh) > 0
+    else:
+        keep = mask > 0
+    g = torch.where(keep, d, torch.zeros_like(d))
+    sums = []
+    for y, m, s in zip(ys, means, istds):
+        xhat = (y - m) * s
+        sums.append((g.sum(0), (g * xhat).sum(0)))
+    return g, sums
+
+
+@pytest.mark.parametrize("cfg", CFGS)
+@pytest.mark.parametrize("case", BNB_CASES)
+def test_dgrad_fused_bn_reduce(case, cfg, dev, cfg_env):
+    _set(cfg)
+    N, G, H, W, Ci, Co, R, pd, kind, nt, rm = case
+    g = torch.Generator().manual_seed(7)
+    dy = torch.randn(N, Co, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Co, Ci, R, R, generator=g) / (Co * R * R) ** 0.5).bfloat16().float()
+    draw = torch.nn.grad.conv2d_input((N, Ci, H, W), w, dy, stride=1, padding=pd)
+    res = None
+    if rm == 1:
+        res = torch.randn(N, Ci, H, W, generator=g).bfloat16().float()
+        draw = draw + res
+    elif rm == 2:
+        res = torch.randn(N, Ci, H // 2, W // 2, generator=g).bfloat16().float()
+        draw = draw + 0.25 * F.interpolate(res, scale_factor=2, mode="nearest")
+    ys = [torch.randn(N, Ci, H, W, generator=g).bfloat16().float() for _ in range(nt)]
+    mask = torch.randn(N, Ci, H, W, generator=g).bfloat16().float()
+    params = torch.randn(G, 4, Ci, generator=g)  # mean, istd, scale, shift per segment
+    params[:, 1] = params[:, 1].abs() + 0.5
+    params2 = torch.randn(G, 4, Ci, generator=g)
+    params2[:, 1] = params2[:, 1].abs() + 0.5
+    # device buffers
+    wdflip = w.flip(2, 3).permute(1, 2, 3, 0).contiguous().to(dev, torch.bfloat16)
+    dyd = _nhwc(dy).to(dev, torch.bfloat16)
+    resd = _nhwc(res).to(dev, torch.bfloat16) if res is not None else None
+    yds = [_nhwc(y).to(dev, torch.bfloat16) for y in ys]
+    maskd = _nhwc(mask).to(dev, torch.bfloat16)
+    pd_ = [params.to(dev), params2.to(dev)]
+    slots = [torch.zeros(G, _hip.NSLOT, 2, Ci, device=dev) for _ in range(nt)]
+    dx = torch.full((N * H * W, Ci), float("nan"), device=dev, dtype=torch.bfloat16)
+    desc = _hip.BnBwdDesc()
+    desc.dtype = _hip.DT_BF16
+    desc.kind = kind
+    desc.pool = 0
+    desc.mask = maskd.data_ptr() if kind == 0 else None
+    desc.mask_scale = pd_[0][0, 2].data_ptr() if kind == 1 else None
+    desc.mask_shift = pd_[0][0, 3].data_ptr() if kind == 1 else None
+    desc.ntarget = nt
+    for t in range(nt):
+        desc.y[t] = yds[t].data_ptr()
+        desc.mean[t] = pd_[t][0, 0].data_ptr()
+        desc.istd[t] = pd_[t][0, 1].data_ptr()
+        desc.slots[t] = slots[t].data_ptr()
+    d = _hip.conv_desc(torch.bfloat16, N, H, W, Ci, Co, R, R, 1, pd)
+    _hip.call("artsbir_conv2d_dgrad_bnb", d, dyd.data_ptr(), wdflip.data_ptr(), dx.data_ptr(),
+              resd.data_ptr() if resd is not None else None, rm, desc, G, 4 * Ci, _hip.stream())
+    torch.cuda.synchronize()
+    got = dx.float().cpu()
+    flat = lambda t: t.permute(0, 2, 3, 1).reshape(-1, Ci)  # noqa: E731
+    per = N // G * H * W
+    for s in range(G):
+        sl = slice(s * per, (s + 1) * per)
+        dseg = flat(draw)[sl]
+        yseg = [flat(y)[sl] for y in ys]
+        gref, sums = _bnb_reference(dseg, kind, yseg, [params[s, 0], params2[s, 0]], [params[s, 1], params2[s, 1]],
+                                    params[s, 2], params[s, 3], flat(mask)[sl])
+        # masks decided on identical bf16 inputs; g within bf16 rounding of the f32 GEMM
+        assert torch.allclose(got[sl], gref, atol=3e-2, rtol=1e-2), (s, (got[sl] - gref).abs().max())
+        for t in range(nt):
+            st = slots[t][s].sum(0).cpu()
+            scale = gref.abs().sum(0) + 1.0
+            assert ((st[0] - sums[t][0]).abs() / scale).max() < 2e-2, (s, t)
+            assert ((st[1] - sums[t][1]).abs() / (scale * 4)).max() < 2e-2, (s, t)
+
+
+def _models(dev, dtype):
+    import models
+    torch.manual_seed(11)
+    a = models.ModifiedResNet((1, 2, 1, 1), 32, heads=8, input_resolution=64, width=16)
+    b = copy.deepcopy(a)
+    a.compute_dtype = b.compute_dtype = dtype
+    return a.to(dev), b.to(dev)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_forward_branches_matches_separate_calls(dtype, dev):
+    import engine
+    import losses
+    batched, separate = _models(dev, dtype)
+    g = torch.Generator(device=dev).manual_seed(3)
+    xs = [torch.randn(8, 3, 64, 64, device=dev, generator=g) + i for i in range(3)]
+    loss_fn = losses.TripletMarginLoss(margin=0.2)
+    old = engine.FUSE_BNB
+    try:
+        engine.FUSE_BNB = True
+        batched.train()
+        ob = batched.forward_branches(xs)
+        lb = loss_fn(*ob)
+        lb.backward()
+        engine.FUSE_BNB = False
+        separate.train()
+        os_ = [separate(x) for x in xs]
+        ls = loss_fn(*os_)
+        ls.backward()
+    finally:
+        engine.FUSE_BNB = old
+    torch.cuda.synchronize()
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    for a, b in zip(ob, os_):
+        assert torch.allclose(a, b, atol=tol, rtol=tol), (a - b).abs().max()
+    sa, sb = batched.state_dict(), separate.state_dict()
+    for k in sa:
+        if "running" in k or "num_batches" in k:
+            assert torch.allclose(sa[k].double(), sb[k].double(), atol=tol, rtol=tol), k
+    if dtype != torch.float32:
+        return  # bf16 run-to-run gradient noise (atomic order + ReLU flips) is ~15 % on this tiny net
+    # per parameter, relative to max(|g|, 1e-4 * the largest gradient anywhere):
+    # mathematically-zero gradients (k_proj.bias, c_proj.bias of a triplet loss)
+    # are rounding noise of ~1e-8 and must not dominate a global norm
+    grads_b = {k: p.grad for k, p in batched.named_parameters()}
+    grads_s = {k: p.grad for k, p in separate.named_parameters()}
+    # BN sums use f32 atomics, so a pre-activation within ~1e-7 of zero can land
+    # on either side of a ReLU between two runs.  On this net two identical
+    # separate-call runs already differ by up to ~6e-3 (per-parameter relative
+    # L2) in a few dozen BN parameters (measured on MI355X), so the bar here is
+    # that noise level; the fused kernels themselves are checked exactly above.
+    floor = 1e-4 * max(g.norm().item() for g in grads_s.values())
+    for k, gs in grads_s.items():
+        err = (grads_b[k] - gs).norm().item() / max(gs.norm().item(), floor)
+        assert err < 2e-2, (k, err)
