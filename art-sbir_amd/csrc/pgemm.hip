@@ -161,6 +161,12 @@ __device__ __forceinline__ void stats_flush(float* red, int* cnt, int last_count
   }
 }
 
+// 8 consecutive floats by two 16-B loads
+__device__ __forceinline__ void loadf8v(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 // LDS accumulator half of the wave's segment (0: the tile's first segment)
 __device__ __forceinline__ int stats_rseg(const PgArgs& a, long long bpx, long long wave_px0) {
   if (a.seg_m <= 0) return 0;
@@ -183,7 +189,7 @@ constexpr int pg_red_bytes() {
 // up to two BN inputs t sharing g (models.py:234 bn3 + downsample BN).  The
 // per-lane sums are reduced over the 16 pixel lanes by DPP and added to the
 // tile's LDS accumulator (stats_flush writes it out).
-template <bool BNB, int BCH, int MTC, int NTP, int WTPX, int WTCH>
+template <bool BNB, int BCH, int MTC, int NTP, int WTPX, int WTCH, int EJB = 2>
 __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
                                             int wpx, int wch, int fr, int fq, float* red) {
   const int HoWo = a.Ho * a.Wo;
@@ -201,83 +207,98 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
     float s1[8], s2[8], s3[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+    // every global load below is issued unconditionally from a clamped, valid
+    // address (pixel / channel tails are masked at the store), so the loads of
+    // a batch go out together and are waited for once, not one round trip each
+    const int chc = chok ? ch0 : 0;
     // BN-backward per-channel constants: xhat_t = y * xa_t + xb_t; mask affine
     float xa0[8], xb0[8], xa1[8], xb1[8], ms[8], mh[8];
-    if (BNB && chok) {
-      const long long po = wseg * a.bnb_pstride + ch0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float is = a.bnb_istd[0][po + e];
-        xa0[e] = is;
-        xb0[e] = -a.bnb_mean[0][po + e] * is;
-        xa1[e] = 0.f; xb1[e] = 0.f; ms[e] = 0.f; mh[e] = 0.f;
-      }
+    if constexpr (BNB) {
+      const long long po = wseg * a.bnb_pstride + chc;
+      float m0[8], m1[8];
+      loadf8v(a.bnb_istd[0] + po, xa0);
+      loadf8v(a.bnb_mean[0] + po, m0);
       if (two) {
+        loadf8v(a.bnb_istd[1] + po, xa1);
+        loadf8v(a.bnb_mean[1] + po, m1);
+      } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float is = a.bnb_istd[1][po + e];
-          xa1[e] = is;
-          xb1[e] = -a.bnb_mean[1][po + e] * is;
-        }
+        for (int e = 0; e < 8; ++e) { xa1[e] = 0.f; m1[e] = 0.f; }
       }
       if (a.bnb == 1) {
+        loadf8v(a.bnb_msc + po, ms);
+        loadf8v(a.bnb_msh + po, mh);
+      } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { ms[e] = a.bnb_msc[po + e]; mh[e] = a.bnb_msh[po + e]; }
+        for (int e = 0; e < 8; ++e) { ms[e] = 0.f; mh[e] = 0.f; }
       }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { xb0[e] = -m0[e] * xa0[e]; xb1[e] = -m1[e] * xa1[e]; }
     }
+    // pixel tiles in batches of EJ: loads of the batch first, then the math
+    constexpr int EJ = NTP >= EJB ? EJB : 1;
 #pragma unroll
-    for (int j = 0; j < NTP; ++j) {
-      const long long px = wpx0 + j * 16 + fr;
-      float v[8];
+    for (int j0 = 0; j0 < NTP; j0 += EJ) {
+      Vec16<bf16> rv[EJ], y0v[EJ], mkv[EJ], y1v[EJ];
+      float rsc[EJ];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
-      if (px < a.M && chok) {
-        if (!BNB && a.stats) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
-        }
+      for (int u = 0; u < EJ; ++u) {
+        const long long px = wpx0 + (j0 + u) * 16 + fr;
+        const long long pc = px < a.M ? px : a.M - 1;
+        rsc[u] = 1.f;
         if (a.res_mode) {
-          long long ri = px;
-          float sc = 1.f;
+          long long ri = pc;
           if (a.res_mode == 2) {
-            const long long img = px / HoWo;
-            const int rem = (int)(px - img * HoWo);
+            const long long img = pc / HoWo;
+            const int rem = (int)(pc - img * HoWo);
             const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
             ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
-            sc = 0.25f;
+            rsc[u] = 0.25f;
           }
-          const Vec16<bf16> rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + ch0);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += sc * to_f(rv.v[e]);
+          rv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + chc);
         }
         if constexpr (BNB) {
-          const long long off = px * a.ldy + ch0;
-          const Vec16<bf16> y0 = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + off);
-          bool keep[8];
-          if (a.bnb == 1) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) keep[e] = to_f(y0.v[e]) * ms[e] + mh[e] > 0.f;
-          } else {
-            const Vec16<bf16> mk = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + off);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) keep[e] = to_f(mk.v[e]) > 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            v[e] = keep[e] ? v[e] : 0.f;
-            s1[e] += v[e];
-            s2[e] += v[e] * (to_f(y0.v[e]) * xa0[e] + xb0[e]);
-          }
-          if (two) {
-            const Vec16<bf16> y1 = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + off);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s3[e] += v[e] * (to_f(y1.v[e]) * xa1[e] + xb1[e]);
-          }
+          const long long off = pc * a.ldy + chc;
+          y0v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + off);
+          if (a.bnb == 2) mkv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + off);
+          if (two) y1v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + off);
         }
-        Vec16<bf16> o;
+      }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
-        st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+      for (int u = 0; u < EJ; ++u) {
+        const int j = j0 + u;
+        const long long px = wpx0 + j * 16 + fr;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+        if (px < a.M && chok) {
+          if (!BNB && a.stats) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+          }
+          if (a.res_mode) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += rsc[u] * to_f(rv[u].v[e]);
+          }
+          if constexpr (BNB) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float yv = to_f(y0v[u].v[e]);
+              const bool keep = a.bnb == 1 ? yv * ms[e] + mh[e] > 0.f : to_f(mkv[u].v[e]) > 0.f;
+              v[e] = keep ? v[e] : 0.f;
+              s1[e] += v[e];
+              s2[e] += v[e] * (yv * xa0[e] + xb0[e]);
+            }
+            if (two) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) s3[e] += v[e] * (to_f(y1v[u].v[e]) * xa1[e] + xb1[e]);
+            }
+          }
+          Vec16<bf16> o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+          st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+        }
       }
     }
     if (sums) {
@@ -645,7 +666,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
     const long long bpx = (t / ntc) * BPX;
     const int bch = (int)(t % ntc) * BCH;
     const int slot = (int)(t % ARTSBIR_NSLOT);
-    pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
+    pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH, 1>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
     // the flushing wave zeroes red before it reaches the next stage barrier,
     // and no wave adds for tile ti+1 before passing that barrier
     if (sums) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane, bpx, BPX);

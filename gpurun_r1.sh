@@ -1,13 +1,13 @@
 #!/bin/bash
-# GPU check: bench at a small batch, then full bench, then profile
+# GPU check: fused/pgemm tests, bench, kernel trace
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-retrieval --batch 32 --steps 2 --warmup 1 > gpurun_out/bench_small.json 2> gpurun_out/bench_small.err || { echo SMALL_FAILED; tail -20 gpurun_out/bench_small.err; exit 1; }
-cat gpurun_out/bench_small.json | cut -c1-300
+timeout -k 10 300 python -u -m pytest tests/test_fused_gpu.py tests/test_pgemm_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/fused_tests.log 2>&1 || { echo FUSED_TESTS_FAILED; tail -40 gpurun_out/fused_tests.log; exit 1; }
+tail -2 gpurun_out/fused_tests.log
 timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-retrieval > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
+cat gpurun_out/bench.json | cut -c1-400
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace -d $R/gpurun_out/prof2 -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-retrieval > $R/gpurun_out/bench_prof.json 2> $R/gpurun_out/bench_prof.err || { echo PROF_FAILED; tail -20 $R/gpurun_out/bench_prof.err; exit 1; }
 echo done
