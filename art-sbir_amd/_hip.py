@@ -128,11 +128,12 @@ class HipError(RuntimeError):
 
 # Optional live per-launch timing (bench.py): when PROFILE is a list, every call
 # that declares its algorithmic work is bracketed by two timing events on the
-# current stream and (kernel, flops, bytes, start, end) is appended.
+# current stream and (kernel, flops, bytes, start, end, tag) is appended.
 PROFILE = None
 
 
-def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes: float = 0.0) -> None:
+def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes: float = 0.0,
+         tag: str | None = None) -> None:
     """Invoke a status-returning entry point; map a non-zero status to HipError."""
     prof = PROFILE
     if prof is not None and kernel is not None:
@@ -143,7 +144,7 @@ def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes
         e1.record()
         if kernel == "auto":  # the variant the library chose for this call
             kernel = lib().artsbir_last_kernel().decode()
-        prof.append((kernel, flops, nbytes, e0, e1))
+        prof.append((kernel, flops, nbytes, e0, e1, tag))
     else:
         rc = getattr(lib(), name)(*args)
     if rc != 0:

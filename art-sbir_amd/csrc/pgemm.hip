@@ -41,6 +41,7 @@ namespace artsbir {
 #define PG_PRIO_OFF()
 #endif
 typedef __attribute__((address_space(3))) void* pg_lds_t;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pg_rsrc(const void* base, long long bytes) {
   if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
@@ -678,6 +679,191 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
 }
 
 // ---------------------------------------------------------------------------
+// Direct 3x3 convolution for few channels (C in {8, 32, 64} in, Cout in
+// {32, 64} out): the stem (models.py:310-317, 112x112) and the layer-1 3x3
+// convolutions, forward and data gradient.  Their im2col rows are short
+// (K = 72..576), so the LDS-staged im2col of pgemm spends its time gathering:
+// here the pixel operand is read STRAIGHT from global memory into the MFMA B
+// fragments — lane (fr, fq) of a 16-pixel tile loads 16 B (8 channels) of its
+// own input pixel, so for C = 32 one wave instruction reads one contiguous
+// 1 KB run of 16 pixels x 64 B (coalesced; the 9 tap re-reads hit L1/L2) —
+// while the whole filter bank sits in LDS (read as A fragments, XOR-swizzled
+// conflict-free).  Padding and tails come back as zeros from the buffer unit.
+// Output tile = 256 consecutive pixels x all Cout channels, 4 waves x 64
+// pixels; the epilogue (BN statistics, BN-backward fusion, segments) is
+// pgemm's.
+// ---------------------------------------------------------------------------
+// LDS image of the filters: block kk (32 k = 4 chunks of 16 B) holds COUT rows
+// of 64 B; row rho carries channel pg_perm(rho), chunk c at slot c ^ sw(rho).
+__device__ __forceinline__ int sc_sw(int rho) { return (rho ^ (rho >> 1)) & 3; }
+
+template <int C, int COUT, int STRIDE, bool BNB>
+__global__ void __launch_bounds__(256) sconv_kernel(PgArgs a, int ntiles) {
+  constexpr int K = 9 * C;
+  constexpr int NKK = (K + 31) / 32;  // 32-k MFMA steps
+  constexpr int CPT = C / 8;          // 16-B chunks per tap
+  constexpr int MTC = COUT / 16, NTP = 4, WTPX = 64, BPX = 256, BCH = COUT;
+  constexpr int PF = 2;                // k-steps of B fragments in flight ahead
+  constexpr int WB = NKK * COUT * 64;  // filter image bytes
+  __shared__ __attribute__((aligned(16))) char smem[WB + pg_red_bytes<BCH>()];
+  float* red = reinterpret_cast<float*>(smem + WB);
+  int* red_cnt = reinterpret_cast<int*>(smem + WB + 6 * BCH * 4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool sums = a.stats != nullptr || a.bnb != 0;
+  if (sums) {
+    for (int i = tid; i < 6 * BCH; i += 256) red[i] = 0.f;
+    if (tid == 0) *red_cnt = 0;
+  }
+  // ---- filters -> LDS once per (persistent) block (zero past K)
+  for (int i = tid; i < NKK * COUT * 4; i += 256) {
+    const int kk = i / (COUT * 4), rem = i - kk * COUT * 4;
+    const int rho = rem >> 2, c = rem & 3;
+    const int k = kk * 32 + c * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (k < K) v = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.w) + (long long)pg_perm(rho) * K + k);
+    *reinterpret_cast<uint4*>(smem + (kk * COUT + rho) * 64 + ((c ^ sc_sw(rho)) << 4)) = v;
+  }
+  const int HoWo = a.Ho * a.Wo;
+  const int G = gridDim.x;
+  int ti = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += G, ++ti) {
+    // filter image visible (first tile); the previous tile's statistics flush
+    // is complete before any wave adds this tile's sums
+    __syncthreads();
+    const long long bpx = (long long)tile * BPX;
+    // ---- per pixel tile: input origin and tap validity of this lane's pixel
+    const long long img0 = bpx / HoWo;
+    const __amdgpu_buffer_rsrc_t xr =
+        pg_rsrc(reinterpret_cast<const bf16*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * 2);
+    const long long wpx0 = bpx + wid * WTPX;
+    int boff[NTP];
+    unsigned vmask[NTP];
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const long long px = wpx0 + j * 16 + fr;
+      const bool valid = px < a.M;
+      const long long pc = valid ? px : bpx;
+      const long long n = pc / HoWo;
+      const int rem = (int)(pc - n * HoWo);
+      const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+      const int ih0 = oh * STRIDE - 1, iw0 = ow * STRIDE - 1;
+      boff[j] = (int)(((n - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2);
+      unsigned m = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r = t / 3, s = t % 3;
+        const bool ok = valid && ih0 + r >= 0 && ih0 + r < a.H && iw0 + s >= 0 && iw0 + s < a.W;
+        m |= (ok ? 1u : 0u) << t;
+      }
+      vmask[j] = m;
+    }
+    // B fragment of k-step kk, pixel tile j: 16 B of the lane's own input pixel
+    auto bload = [&](int kk, int j) -> uint4 {
+      const int kc = kk * 4 + fq;  // 16-B chunk of the im2col row
+      const int t = kc / CPT, cc = kc - (kc / CPT) * CPT;
+      const int r = t / 3, s = t - (t / 3) * 3;
+      const bool ok = kc < 9 * CPT && ((vmask[j] >> t) & 1u);
+      const unsigned off = (unsigned)(boff[j] + ((r * (int)a.sH + s * (int)a.sW) * 2) + cc * 16);
+      const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)off : (int)PG_OOB, 0, 0);
+      return make_uint4(v[0], v[1], v[2], v[3]);
+    };
+    f32x4 acc[MTC][NTP];
+#pragma unroll
+    for (int i = 0; i < MTC; ++i)
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // ring of PF + 1 k-steps of B fragments (fully unrolled: static indices)
+    uint4 bf[PF + 1][NTP];
+#pragma unroll
+    for (int q = 0; q < PF; ++q)
+      if (q < NKK) {
+#pragma unroll
+        for (int j = 0; j < NTP; ++j) bf[q][j] = bload(q, j);
+      }
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      if (kk + PF < NKK) {
+#pragma unroll
+        for (int j = 0; j < NTP; ++j) bf[(kk + PF) % (PF + 1)][j] = bload(kk + PF, j);
+      }
+      uint4 af[MTC];
+#pragma unroll
+      for (int i = 0; i < MTC; ++i) {
+        const int rho = i * 16 + fr;
+        af[i] = *reinterpret_cast<const uint4*>(smem + (kk * COUT + rho) * 64 + ((fq ^ sc_sw(rho)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MTC; ++i)
+#pragma unroll
+        for (int j = 0; j < NTP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
+                                                              *reinterpret_cast<const bf16x8*>(&bf[kk % (PF + 1)][j]),
+                                                              acc[i][j], 0, 0, 0);
+    }
+    const int slot = tile % ARTSBIR_NSLOT;
+    pg_epilogue<BNB, BCH, MTC, NTP, WTPX, COUT, 1>(a, acc, bpx, 0, wid, 0, fr, fq, red);
+    if (sums) stats_flush<BCH>(red, red_cnt, 4 * (ti + 1) - 1, a, 0, slot, lane, bpx, BPX);
+  }
+}
+
+// shapes the direct small-channel kernel takes
+static bool sconv_ok(const PgArgs& a) {
+  if (a.R != 3 || a.S != 3 || a.pad != 1 || a.M <= 0) return false;
+  if (a.Cout != 32 && a.Cout != 64) return false;
+  if (!((a.stride == 1 && (a.C == 32 || a.C == 64)) || (a.stride == 2 && a.C == 8 && a.Cout == 32))) return false;
+  if (a.seg_m > 0 && (a.seg_m % 64 != 0 || a.seg_m < 256 || a.M % a.seg_m != 0)) return false;
+  if (a.bnb && a.stats) return false;
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  // block-relative byte offsets in 31 bits: a 256-pixel tile spans few images
+  if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 > 0x7fffffffLL) return false;
+  return (a.M + 255) / 256 <= 0x7fffffffLL / 256;
+}
+
+// persistent grid: as many blocks as fit on the 256 CUs at once (LDS-bound)
+template <int C, int COUT>
+static int sconv_grid(int ntiles) {
+  constexpr int K = 9 * C, NKK = (K + 31) / 32;
+  constexpr int lds = NKK * COUT * 64 + 2 * 3 * COUT * 4 + 16;
+  int per_cu = (160 * 1024) / lds;
+  if (per_cu > 4) per_cu = 4;  // 4 x 256 threads: 16 waves per CU
+  const int g = 256 * per_cu;
+  return ntiles < g ? ntiles : g;
+}
+
+template <bool BNB>
+static bool sconv_dispatch(const PgArgs& a, int ntiles, hipStream_t st) {
+  if (a.stride == 1 && a.C == 32 && a.Cout == 32) {
+    set_last_kernel("sconv_kernel<32,32>");
+    hipLaunchKernelGGL((sconv_kernel<32, 32, 1, BNB>), dim3(sconv_grid<32, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
+  } else if (a.stride == 1 && a.C == 32 && a.Cout == 64) {
+    set_last_kernel("sconv_kernel<32,64>");
+    hipLaunchKernelGGL((sconv_kernel<32, 64, 1, BNB>), dim3(sconv_grid<32, 64>(ntiles)), dim3(256), 0, st, a, ntiles);
+  } else if (a.stride == 1 && a.C == 64 && a.Cout == 32) {
+    set_last_kernel("sconv_kernel<64,32>");
+    hipLaunchKernelGGL((sconv_kernel<64, 32, 1, BNB>), dim3(sconv_grid<64, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
+  } else if (a.stride == 1 && a.C == 64 && a.Cout == 64) {
+    set_last_kernel("sconv_kernel<64,64>");
+    hipLaunchKernelGGL((sconv_kernel<64, 64, 1, BNB>), dim3(sconv_grid<64, 64>(ntiles)), dim3(256), 0, st, a, ntiles);
+  } else if (a.stride == 2 && a.C == 8 && a.Cout == 32) {
+    set_last_kernel("sconv_kernel<8,32,s2>");
+    hipLaunchKernelGGL((sconv_kernel<8, 32, 2, BNB>), dim3(sconv_grid<8, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
+  } else {
+    return false;
+  }
+  return true;
+}
+
+// candidate 20: the direct small-channel kernel; false if the shape is not one
+bool sconv_launch(const PgArgs& a, hipStream_t st) {
+  if (!sconv_ok(a)) return false;
+  const int ntiles = (int)((a.M + 255) / 256);
+  if (a.bnb) return sconv_dispatch<true>(a, ntiles, st);
+  return sconv_dispatch<false>(a, ntiles, st);
+}
+
+// ---------------------------------------------------------------------------
 // launch: pick the tile shape with the best (tile utilisation x CU fill)
 // ---------------------------------------------------------------------------
 struct PgCfg {
@@ -729,6 +915,7 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
 
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
+  if (c == 20) return sconv_launch(a, st);
   bool multi;
   if (!pg_supported(a, multi)) return false;
   if (c == 10) {
@@ -766,6 +953,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
 
 // static choice (no tuning): streaming kernel for many tiles, else best-scored tile
 int pgemm_default_cfg(const PgArgs& a) {
+  if (sconv_ok(a)) return 20;
   bool multi;
   if (!pg_supported(a, multi)) return -1;
   const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;

@@ -45,6 +45,8 @@ BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 # ARTSBIR_FUSE_BNB=0 runs the BN-backward reduction as its own pass (A/B tests)
 FUSE_BNB = os.environ.get("ARTSBIR_FUSE_BNB", "1") != "0"
+# ARTSBIR_OVERLAP_WGRAD=0 keeps the weight gradients on the caller's stream
+OVERLAP_WGRAD = os.environ.get("ARTSBIR_OVERLAP_WGRAD", "1") != "0"
 
 # bumped by optim.Adam (which updates parameters through raw pointers, invisible
 # to torch's version counters) so packed weights are rebuilt after every step
@@ -215,7 +217,7 @@ class Engine:
         if stats_buf is not None and bn is None:
             # BN statistics per segment (one launch for all G forward calls)
             call("artsbir_conv2d_fwd_seg", d, ptr(a.t), ptr(fw), ptr(y), self._G, ptr(stats_buf), _s(),
-                 kernel="auto", flops=flops)
+                 kernel="auto", flops=flops, tag=f"fwd {B}x{H}x{W}x{C}->{cout} {R}x{S}/{stride}")
             return y
         if bn is not None and bn.G != 1:
             raise NotImplementedError("affine-on-load convolutions take one segment")
@@ -391,6 +393,8 @@ class Engine:
             prev = (blocks[i - 1], cs[i - 1]) if i > 0 else None
             dh, fused = self._block_bwd(blocks[i], bps[i], cs[i], dh, grads, ws, fused, prev)
         self._stem_bwd(m, pk, ctx["stem"], dh, grads, ws)
+        if OVERLAP_WGRAD:
+            torch.cuda.current_stream().wait_stream(self._side_stream(dev))
         return grads
 
     def _attnpool_bwd(self, ap, pk, c, dout, grads):
@@ -529,7 +533,30 @@ class Engine:
             call("artsbir_bn_bwd_apply", desc, _s())
         return dys
 
+    def _side_stream(self, device):
+        st = getattr(self, "_side", None)
+        if st is None or st.device != device:
+            st = self._side = torch.cuda.Stream(device=device)
+        return st
+
     def _wgrad(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):
+        """weight gradient on a second stream: it only reads dy and the layer
+        input and accumulates into its own slice of the gradient buffer, so it
+        runs concurrently with the (HBM-bound) data-gradient / BatchNorm chain
+        of the main stream; backward() joins the streams at the end."""
+        if not OVERLAP_WGRAD:
+            return self._wgrad_sync(dy, a, conv, stride, pad, grads, ci_pad)
+        main = torch.cuda.current_stream()
+        side = self._side_stream(dy.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._wgrad_sync(dy, a, conv, stride, pad, grads, ci_pad)
+        # the caching allocator must not hand these to the main stream before
+        # the side stream is done with them
+        dy.record_stream(side)
+        a.t.record_stream(side)
+
+    def _wgrad_sync(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):
         B, H, W, C = a.shape
         co, ci, R, S = conv.weight.shape
         d = self._desc(B, H, W, C, co, R, S, stride, pad)
@@ -542,7 +569,7 @@ class Engine:
         Ho, Wo = dy.shape[1], dy.shape[2]
         call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), ptr(bn.scale) if bn else None,
              ptr(bn.shift) if bn else None, a.relu, ptr(target), _s(), kernel="auto",
-             flops=2.0 * B * Ho * Wo * co * R * S * C)
+             flops=2.0 * B * Ho * Wo * co * R * S * C, tag=f"wgrad {B}x{H}x{W}x{C}->{co} {R}x{S}/{stride}")
         if target is not g:
             call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
 
@@ -554,10 +581,11 @@ class Engine:
         flops = 2.0 * B * H * W * C * R * S * co
         if fused is None:
             call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
-                 kernel="auto", flops=flops)
+                 kernel="auto", flops=flops, tag=f"dgrad {B}x{H}x{W}x{co}->{C} {R}x{S} res{res_mode}")
         else:
             call("artsbir_conv2d_dgrad_bnb", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode,
-                 ctypes.byref(fused[0]), self._G, 4 * C, _s(), kernel="auto", flops=flops)
+                 ctypes.byref(fused[0]), self._G, 4 * C, _s(), kernel="auto", flops=flops,
+                 tag=f"dgrad+bn{fused[0].kind} {B}x{H}x{W}x{co}->{C} {R}x{S} res{res_mode}")
         return dx
 
     def _block_bwd(self, blk, bp, c, dout, grads, ws, fused_res=None, prev=None):

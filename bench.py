@@ -134,7 +134,7 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1 in prof if kn == "knn_scan_kernel"]
+    scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1, *_ in prof if kn == "knn_scan_kernel"]
     scan_s = sum(s for _, s in scan) / len(scan)
     scan_fl = sum(f for f, _ in scan) / len(scan)
     rk = r.double() + 1
@@ -256,7 +256,7 @@ def main():
         roof = None
         if prof:
             agg = {}
-            for kname, fl, _, e0, e1 in prof:
+            for kname, fl, _, e0, e1, *_ in prof:
                 a = agg.setdefault(kname, [0.0, 0.0, 0])
                 a[0] += fl
                 a[1] += e0.elapsed_time(e1) / 1e3

@@ -1,11 +1,11 @@
 #!/bin/bash
-# GPU check: fused/pgemm tests, bench, kernel trace
+# GPU check: all parity tests, bench, kernel trace
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd $R
-timeout -k 10 300 python -u -m pytest tests/test_fused_gpu.py tests/test_pgemm_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/fused_tests.log 2>&1 || { echo FUSED_TESTS_FAILED; tail -40 gpurun_out/fused_tests.log; exit 1; }
-tail -2 gpurun_out/fused_tests.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/gpu_tests.log
 timeout -k 10 400 python -u bench.py --no-cpu-baseline --no-retrieval > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json | cut -c1-400
 cd /tmp && export TMPDIR=/tmp

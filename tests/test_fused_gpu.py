@@ -14,7 +14,7 @@ import _hip
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ["auto", "0", "1", "2", "3", "4", "10", "-2"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "10", "20", "-2"]
 
 
 @pytest.fixture
@@ -43,6 +43,7 @@ SEG_CASES = [
     (6, 3, 16, 16, 64, 128, 3, 1),     # 256 px / segment
     (12, 3, 8, 8, 256, 64, 1, 0),      # 256 px / segment
     (6, 3, 32, 16, 32, 64, 3, 1),      # multi-tap C=32, 1024 px / segment
+    (6, 3, 16, 16, 32, 32, 3, 1),      # stem conv2 shape family
     (6, 2, 7, 7, 512, 256, 3, 1),      # 147 px / segment: not a multiple of 64 -> per-segment fallback
 ]
 
@@ -82,6 +83,8 @@ BNB_CASES = [
     (4, 2, 16, 16, 256, 64, 1, 0, 0, 2, 1),    # RES (bn3 + downsample), residual add
     (6, 3, 16, 16, 256, 64, 1, 0, 0, 1, 2),    # RES, avg-unpool residual
     (4, 2, 16, 16, 32, 64, 3, 1, 1, 1, 0),     # stem-like: 64-ch dY -> 32-ch dX
+    (6, 3, 16, 16, 32, 32, 3, 1, 1, 1, 0),     # stem conv2 data gradient, segments
+    (3, 1, 9, 13, 64, 64, 3, 1, 1, 1, 0),      # layer-1 3x3, image-crossing tiles
 ]
 
 

@@ -20,8 +20,12 @@ CASES = [
     (1, 5, 5, 256, 96, 1, 1, 1, 0),     # partial channel tile
     (8, 28, 28, 64, 128, 3, 3, 1, 1),   # many pixel tiles
     (3, 12, 12, 512, 64, 1, 1, 2, 0),   # strided 1x1
+    (2, 12, 10, 32, 32, 3, 3, 1, 1),    # stem conv2 (direct small-channel kernel)
+    (3, 9, 13, 64, 64, 3, 3, 1, 1),     # layer-1 3x3, image-crossing pixel tiles
+    (2, 12, 10, 64, 32, 3, 3, 1, 1),
+    (3, 11, 7, 8, 32, 3, 3, 2, 1),      # stem conv1, odd sizes
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "10"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "10", "20"]
 
 
 @pytest.fixture
@@ -81,6 +85,8 @@ DG_CASES = [
     (2, 10, 6, 32, 64, 3, 1, 0),        # dY with 64 channels -> 32-channel dX (stem)
     (2, 10, 6, 32, 32, 3, 1, 0),        # 32-channel dY: multi-tap
     (8, 28, 28, 128, 128, 3, 1, 2),
+    (3, 9, 13, 64, 64, 3, 1, 0),        # layer-1 3x3 data gradient
+    (2, 12, 10, 64, 32, 3, 1, 1),
 ]
 
 
