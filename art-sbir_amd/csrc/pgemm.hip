@@ -835,19 +835,19 @@ static int sconv_grid(int ntiles) {
 template <bool BNB>
 static bool sconv_dispatch(const PgArgs& a, int ntiles, hipStream_t st) {
   if (a.stride == 1 && a.C == 32 && a.Cout == 32) {
-    set_last_kernel("sconv_kernel<32,32>");
+    set_last_kernel(BNB ? "sconv_kernel<32,32,bnb>" : "sconv_kernel<32,32>");
     hipLaunchKernelGGL((sconv_kernel<32, 32, 1, BNB>), dim3(sconv_grid<32, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 1 && a.C == 32 && a.Cout == 64) {
-    set_last_kernel("sconv_kernel<32,64>");
+    set_last_kernel(BNB ? "sconv_kernel<32,64,bnb>" : "sconv_kernel<32,64>");
     hipLaunchKernelGGL((sconv_kernel<32, 64, 1, BNB>), dim3(sconv_grid<32, 64>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 1 && a.C == 64 && a.Cout == 32) {
-    set_last_kernel("sconv_kernel<64,32>");
+    set_last_kernel(BNB ? "sconv_kernel<64,32,bnb>" : "sconv_kernel<64,32>");
     hipLaunchKernelGGL((sconv_kernel<64, 32, 1, BNB>), dim3(sconv_grid<64, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 1 && a.C == 64 && a.Cout == 64) {
-    set_last_kernel("sconv_kernel<64,64>");
+    set_last_kernel(BNB ? "sconv_kernel<64,64,bnb>" : "sconv_kernel<64,64>");
     hipLaunchKernelGGL((sconv_kernel<64, 64, 1, BNB>), dim3(sconv_grid<64, 64>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 2 && a.C == 8 && a.Cout == 32) {
-    set_last_kernel("sconv_kernel<8,32,s2>");
+    set_last_kernel(BNB ? "sconv_kernel<8,32,s2,bnb>" : "sconv_kernel<8,32,s2>");
     hipLaunchKernelGGL((sconv_kernel<8, 32, 2, BNB>), dim3(sconv_grid<8, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else {
     return false;
@@ -924,7 +924,9 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
     if (nt > 0x7fffffffLL) return false;
     const int grid = (int)(nt < 256 ? nt : 256);
     const int ntl = (int)nt;
-    set_last_kernel(bch == 32 ? "pstream_kernel<32>" : bch == 64 ? "pstream_kernel<64>" : "pstream_kernel<128>");
+    static const char* pnames[2][3] = {{"pstream_kernel<32>", "pstream_kernel<64>", "pstream_kernel<128>"},
+                                       {"pstream_kernel<32,bnb>", "pstream_kernel<64,bnb>", "pstream_kernel<128,bnb>"}};
+    set_last_kernel(pnames[a.bnb ? 1 : 0][bch == 32 ? 0 : bch == 64 ? 1 : 2]);
     if (a.bnb) {
       if (multi) pstream_launch<true, true>(bch, a, grid, ntl, st);
       else pstream_launch<false, true>(bch, a, grid, ntl, st);
@@ -938,9 +940,11 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const PgCfg& g = kCfgs[c];
   const long long tiles = ((a.M + g.bpx - 1) / g.bpx) * ((a.Cout + g.bch - 1) / g.bch);
   if (tiles > 0x7fffffffLL) return false;
-  static const char* names[] = {"pgemm_kernel<256,256>", "pgemm_kernel<256,128>", "pgemm_kernel<256,64>",
-                                "pgemm_kernel<128,128>", "pgemm_kernel<256,32>"};
-  set_last_kernel(names[c]);
+  static const char* names[2][5] = {{"pgemm_kernel<256,256>", "pgemm_kernel<256,128>", "pgemm_kernel<256,64>",
+                                      "pgemm_kernel<128,128>", "pgemm_kernel<256,32>"},
+                                     {"pgemm_kernel<256,256,bnb>", "pgemm_kernel<256,128,bnb>", "pgemm_kernel<256,64,bnb>",
+                                      "pgemm_kernel<128,128,bnb>", "pgemm_kernel<256,32,bnb>"}};
+  set_last_kernel(names[a.bnb ? 1 : 0][c]);
   if (a.bnb) {
     if (multi) pg_launch_cfg<true, true>(c, a, tiles, st);
     else pg_launch_cfg<false, true>(c, a, tiles, st);

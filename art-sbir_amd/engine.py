@@ -214,16 +214,18 @@ class Engine:
         d = self._desc(B, H, W, C, cout, R, S, stride, pad)
         bn = a.bn
         flops = 2.0 * B * Ho * Wo * cout * R * S * C
+        es = y.element_size()
+        nbytes = float(es * (B * H * W * C + cout * R * S * C + B * Ho * Wo * cout))  # algorithmic: x, w, y once
         if stats_buf is not None and bn is None:
             # BN statistics per segment (one launch for all G forward calls)
             call("artsbir_conv2d_fwd_seg", d, ptr(a.t), ptr(fw), ptr(y), self._G, ptr(stats_buf), _s(),
-                 kernel="auto", flops=flops, tag=f"fwd {B}x{H}x{W}x{C}->{cout} {R}x{S}/{stride}")
+                 kernel="auto", flops=flops, nbytes=nbytes, tag=f"fwd {B}x{H}x{W}x{C}->{cout} {R}x{S}/{stride}")
             return y
         if bn is not None and bn.G != 1:
             raise NotImplementedError("affine-on-load convolutions take one segment")
         call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None,
              ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None, a.relu,
-             ptr(stats_buf), _s(), kernel="auto", flops=flops)
+             ptr(stats_buf), _s(), kernel="auto", flops=flops, nbytes=nbytes)
         return y
 
     def _bn(self, bnmod, stats_buf, count, train):
@@ -569,7 +571,8 @@ class Engine:
         Ho, Wo = dy.shape[1], dy.shape[2]
         call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), ptr(bn.scale) if bn else None,
              ptr(bn.shift) if bn else None, a.relu, ptr(target), _s(), kernel="auto",
-             flops=2.0 * B * Ho * Wo * co * R * S * C, tag=f"wgrad {B}x{H}x{W}x{C}->{co} {R}x{S}/{stride}")
+             flops=2.0 * B * Ho * Wo * co * R * S * C, tag=f"wgrad {B}x{H}x{W}x{C}->{co} {R}x{S}/{stride}",
+             nbytes=float(dy.element_size() * (B * Ho * Wo * co + B * H * W * C) + 4 * co * R * S * C))
         if target is not g:
             call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
 
@@ -579,12 +582,19 @@ class Engine:
         dx = self._empty(B, H, W, C, device=dy.device)
         d = self._desc(B, H, W, C, co, R, S, 1, pad)
         flops = 2.0 * B * H * W * C * R * S * co
+        es = dx.element_size()
+        px = B * H * W
+        # algorithmic bytes: dy, w, dx once; residual; BN-backward operands (y_t, mask)
+        nb = px * co + co * R * S * C + px * C + (px * C if res_mode == 1 else px * C // 4 if res_mode == 2 else 0)
+        if fused is not None:
+            nb += px * C * (fused[0].ntarget + (1 if fused[0].kind == 0 else 0))
+        nbytes = float(es * nb)
         if fused is None:
             call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
-                 kernel="auto", flops=flops, tag=f"dgrad {B}x{H}x{W}x{co}->{C} {R}x{S} res{res_mode}")
+                 kernel="auto", flops=flops, nbytes=nbytes, tag=f"dgrad {B}x{H}x{W}x{co}->{C} {R}x{S} res{res_mode}")
         else:
             call("artsbir_conv2d_dgrad_bnb", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode,
-                 ctypes.byref(fused[0]), self._G, 4 * C, _s(), kernel="auto", flops=flops,
+                 ctypes.byref(fused[0]), self._G, 4 * C, _s(), kernel="auto", flops=flops, nbytes=nbytes,
                  tag=f"dgrad+bn{fused[0].kind} {B}x{H}x{W}x{co}->{C} {R}x{S} res{res_mode}")
         return dx
 

@@ -28,6 +28,7 @@ import torch.distributed as dist  # noqa: E402
 
 LAYERS, OUT_DIM, RES, WIDTH, HEADS = (3, 4, 6, 3), 512, 224, 64, 32
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s measured copy)
 # per-launch HBM bytes of each kernel from the committed rocprofv3 PMC passes
 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/summarize_pmc.py)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
@@ -255,23 +256,36 @@ def main():
         value = images / elapsed
         roof = None
         if prof:
+            # per kernel: algorithmic FLOPs and bytes (declared by the engine per
+            # launch) over the HIP-event time of its launches; the dominant kernel
+            # (most time) is priced against the roof its arithmetic intensity hits
             agg = {}
-            for kname, fl, _, e0, e1, *_ in prof:
-                a = agg.setdefault(kname, [0.0, 0.0, 0])
+            for kname, fl, nb, e0, e1, *_ in prof:
+                a = agg.setdefault(kname, [0.0, 0.0, 0, 0.0])
                 a[0] += fl
                 a[1] += e0.elapsed_time(e1) / 1e3
                 a[2] += 1
+                a[3] += nb
             dom = max(agg, key=lambda k: agg[k][1])
-            fl, secs, cnt = agg[dom]
-            peak = MFMA_PEAK_TFLOPS[args.dtype]
-            achieved = fl / secs / 1e12
-            roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                    "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom),
-                    "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT), "kernel": dom, "launches": cnt,
-                    "avg_launch_us": round(secs / cnt * 1e6, 2), "avg_launch_flops": fl / cnt,
-                    "per_kernel": {k: {"launches": v[2], "avg_us": round(v[1] / v[2] * 1e6, 2),
-                                       "tflops": round(v[0] / v[1] / 1e12, 1), "share_s": round(v[1], 4)}
-                                   for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}}
+            fl, secs, cnt, nb = agg[dom]
+            peak_fl = MFMA_PEAK_TFLOPS[args.dtype]
+            ridge = peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
+            if nb > 0 and fl / nb < ridge:
+                achieved = nb / secs / 1e9
+                roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 4)}
+            else:
+                achieved = fl / secs / 1e12
+                roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_fl, "unit": "TFLOP/s",
+                        "frac": round(achieved / peak_fl, 4)}
+            roof.update({"traffic": pmc_traffic(dom), "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT),
+                         "kernel": dom, "launches": cnt, "avg_launch_us": round(secs / cnt * 1e6, 2),
+                         "avg_launch_flops": fl / cnt, "avg_launch_bytes": nb / cnt,
+                         "intensity_flop_per_byte": round(fl / nb, 1) if nb else None,
+                         "per_kernel": {k: {"launches": v[2], "avg_us": round(v[1] / v[2] * 1e6, 2),
+                                            "tflops": round(v[0] / v[1] / 1e12, 1),
+                                            "gbs": round(v[3] / v[1] / 1e9, 1), "share_s": round(v[1], 4)}
+                                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}})
         step_flops = train_flops_per_triplet() * B
         line = {
             "metric": "triplet-images/sec embedded @224² bf16, 1→8 GPU; gallery kNN QPS @1M×512",

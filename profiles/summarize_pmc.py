@@ -3,7 +3,7 @@
 
     rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py ...
     rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py ...
-    python profiles/summarize_pmc.py gpurun_out profiles/r1_pmc_traffic.json
+    python profiles/summarize_pmc.py gpurun_out/pmc_train gpurun_out/pmc_retr profiles/r1_pmc_traffic.json
 
 Counter values are KiB.  gfx950 correction (MI355X_MICROARCH.md §HBM):
 FETCH_SIZE reports half the bytes of a wide coalesced stream -> doubled;
@@ -28,19 +28,35 @@ def short(name):
     m = re.match(r"_ZN7artsbir12wgrad_kernelIDF16bLi(\d+)ELi(\d+)E", name)
     if m:
         return f"wgrad_kernel<bf16,{m.group(1)},{m.group(2)}>"
+    bnb = ",bnb" if re.search(r"Lb1EEEv", name) else ""  # last template flag: fused BN backward
     m = re.match(r"_ZN7artsbir12pgemm_kernelILi(\d+)ELi(\d+)E", name)
     if m:
-        return f"pgemm_kernel<{m.group(1)},{m.group(2)}>"
+        return f"pgemm_kernel<{m.group(1)},{m.group(2)}{bnb}>"
     m = re.match(r"_ZN7artsbir14pstream_kernelILi(\d+)E", name)
     if m:
-        return f"pstream_kernel<{m.group(1)}>"
+        return f"pstream_kernel<{m.group(1)}{bnb}>"
     m = re.match(r"_ZN7artsbir13pwgrad_kernelILi(\d+)ELi(\d+)E", name)
     if m:
         return f"pwgrad_kernel<{m.group(1)},{m.group(2)}>"
+    m = re.match(r"_ZN7artsbir12sconv_kernelILi(\d+)ELi(\d+)ELi(\d+)E", name)
+    if m:
+        return f"sconv_kernel<{m.group(1)},{m.group(2)}{',s2' if m.group(3) == '2' else ''}{bnb}>"
     m = re.match(r"_ZN7artsbir\d+(\w+?_kernel)", name)
     if m:
         return m.group(1)
-    return name.split("(")[0].replace("artsbir::", "")
+    # demangled form: void artsbir::name<a, b, ...>(args) -> the names bench.py uses
+    m = re.match(r"(?:void )?artsbir::(\w+_kernel)<([^>]*)>", name)
+    if m:
+        k, t = m.group(1), [x.strip() for x in m.group(2).split(",")]
+        fb = ",bnb" if t[-1] == "true" and k in ("pgemm_kernel", "pstream_kernel", "sconv_kernel") else ""
+        if k in ("pgemm_kernel", "pwgrad_kernel"):
+            return f"{k}<{t[0]},{t[1]}{fb}>"
+        if k == "pstream_kernel":
+            return f"{k}<{t[0]}{fb}>"
+        if k == "sconv_kernel":
+            return f"{k}<{t[0]},{t[1]}{',s2' if t[2] == '2' else ''}{fb}>"
+        return k
+    return name.split("(")[0].replace("artsbir::", "").replace("void ", "")
 
 
 def load(path, counter):
@@ -54,7 +70,7 @@ def load(path, counter):
     return agg
 
 
-def main(src, dst):
+def summarize(src):
     fetch = load(f"{src}/pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
     write = load(f"{src}/pmc_write/run_counter_collection.csv", "WRITE_SIZE")
     out = {}
@@ -65,10 +81,21 @@ def main(src, dst):
         nw, bw = write[k]
         out[k] = {"launches": nf, "fetch_bytes_per_launch": 2.0 * bf / nf, "write_bytes_per_launch": bw / nw,
                   "hbm_bytes_per_launch": 2.0 * bf / nf + bw / nw}
+    return out
+
+
+def main(dst, *srcs):
+    """srcs: run directories (each with pmc_fetch/ and pmc_write/); a kernel is
+    taken from the first run that has it"""
+    out = {}
+    for src in srcs:
+        for k, v in summarize(src).items():
+            out.setdefault(k, v)
     out = dict(sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"]))
-    json.dump({"note": "FETCH_SIZE doubled (gfx950 correction), WRITE_SIZE as reported; bytes per launch",
+    json.dump({"note": "FETCH_SIZE doubled (gfx950 correction), WRITE_SIZE as reported; bytes per launch "
+                       "(averaged over every launch of the kernel in the profiled run, autotuning trials included)",
                "kernels": out}, open(dst, "w"), indent=1)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[-1], *sys.argv[1:-1])
