@@ -14,7 +14,7 @@ import os
 import torch  # noqa: F401  (must be imported before the library is dlopen'ed)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libartsbir_hip.so")
+LIB_PATH = os.environ.get("ARTSBIR_LIB") or os.path.join(_HERE, "libartsbir_hip.so")
 
 DT_F32 = 0
 DT_BF16 = 1

@@ -794,7 +794,7 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  static const int cands[] = {-2, 0, 1, 2, 3, 4, 10, 20};
+  static const int cands[] = {-2, 0, 1, 2, 3, 4, 10, 20, 21};
   int best = -2;
   float best_ms = 1e30f;
   for (int c : cands) {

@@ -20,6 +20,7 @@
 //  * implicit im2col: per pixel row a tap-validity mask; out-of-range (padding,
 //    tails) source offsets are 0x80000000, which the buffer unit turns into
 //    zeros written to LDS.
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -864,6 +865,300 @@ bool sconv_launch(const PgArgs& a, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
+// Halo-tiled direct 3x3 convolution (stride 1, pad 1; C in {32, 64} channels
+// in, Cout in {32, 64} out): the stem conv2/conv3 (models.py:312-317, 112x112)
+// and the layer-1 conv2 (models.py:200-201, 56x56), forward and data gradient
+// with the fused BN-backward reduction.
+//
+// An output tile is TR x TC pixels of one image (all Cout channels).  Its
+// input halo of (TR+2) x (TC+2) pixels is brought into LDS ONCE by LDS-DMA and
+// all nine taps read it there (sconv re-reads every input pixel nine times
+// through L1/L2 as fragment-shaped loads).  One loader wave streams the halo
+// of the block's next tile into the second of two halo buffers while four
+// compute waves run the MFMAs of the current one out of the first; the filter
+// bank stays in LDS for the whole persistent block.
+//
+// Halo LDS image: 1-KB blocks of PB pixels x CPT 16-B channel chunks, chunk
+// major inside a block (lane l of a DMA instruction fills chunk l / PB of
+// pixel l % PB, so one instruction reads PB whole pixels = 1 KB of contiguous
+// NHWC input).  A B fragment read (16 consecutive halo pixels of one tile row,
+// one chunk per lane quad) then hits 16 distinct 16-B bank slots in every
+// ds_read_b128 lane group, for every tap offset.
+//
+// The BN-backward operand of the epilogue (y of the BN before the ReLU) and
+// the per-channel parameters are loaded into registers before the MFMAs, so
+// their latency hides behind them.
+// ---------------------------------------------------------------------------
+#define HC_MAXSEG 4
+template <int C>
+__device__ __forceinline__ int hc_addr(int q, int c) {
+  constexpr int PB = 64 / (C / 8);
+  constexpr int PBL = PB == 16 ? 4 : 3;
+  return ((q >> PBL) << 10) + c * (PB * 16) + ((q & (PB - 1)) << 4);
+}
+
+template <int C, int COUT, int TR, int TC>
+struct HcGeom {
+  static constexpr int NWC = 4;                    // compute waves
+  static constexpr int CPT = C / 8, PB = 64 / CPT;
+  static constexpr int NKK = 9 * C / 32;           // 32-k MFMA steps
+  static constexpr int MTC = COUT / 16, NP = MTC / 2;
+  static constexpr int TCB = TC / 16;              // 16-pixel MFMA tiles per tile row
+  static constexpr int NTP = TR * TCB / NWC;       // MFMA pixel tiles per compute wave
+  static constexpr int HW = TC + 2, NQ = HW * (TR + 2);
+  static constexpr int NB = (NQ + PB - 1) / PB;    // 1-KB halo blocks
+  static constexpr int HB = NB * 1024;
+  static constexpr int WB = NKK * COUT * 64;       // filter image
+  static constexpr int PRM = HC_MAXSEG * 4 * COUT * 4;  // BN-backward parameters per segment
+  static constexpr int LDS = WB + 2 * HB + PRM + pg_red_bytes<COUT>();
+};
+
+template <int C, int COUT, int TR, int TC, bool BNB>
+__global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
+  using Gm = HcGeom<C, COUT, TR, TC>;
+  constexpr int NWC = Gm::NWC, PB = Gm::PB, NKK = Gm::NKK, MTC = Gm::MTC, NP = Gm::NP;
+  constexpr int TCB = Gm::TCB, NTP = Gm::NTP, HW = Gm::HW, NQ = Gm::NQ, NB = Gm::NB, HB = Gm::HB;
+  constexpr int WB = Gm::WB;
+  static_assert(C % 32 == 0 && COUT % 32 == 0 && TC % 16 == 0, "tile shape");
+  static_assert(NTP * NWC == TR * TCB, "pixel tiles per wave");
+  static_assert(Gm::LDS <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
+  float* prm = reinterpret_cast<float*>(smem + WB + 2 * HB);  // [seg][istd, mean, msc, msh][COUT]
+  float* red = reinterpret_cast<float*>(smem + WB + 2 * HB + Gm::PRM);
+  int* red_cnt = reinterpret_cast<int*>(smem + WB + 2 * HB + Gm::PRM + 6 * COUT * 4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int G = gridDim.x;
+  const int ntw = (a.Wo + TC - 1) / TC, nth = (a.Ho + TR - 1) / TR;
+  const int HoWo = a.Ho * a.Wo;
+  const bool sums = a.stats != nullptr || BNB;
+
+  // halo of tile t -> buffer buf (loader wave)
+  auto issue_halo = [&](int t, int buf) {
+    const int img = t / (nth * ntw), rem = t - img * (nth * ntw);
+    const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
+    const __amdgpu_buffer_rsrc_t xr =
+        pg_rsrc(reinterpret_cast<const bf16*>(a.x) + (long long)img * a.sN, (a.x_elems - (long long)img * a.sN) * 2);
+    char* hb = smem + WB + buf * HB;
+    const int c = lane / PB, ql = lane - c * PB;
+#pragma unroll 4
+    for (int b = 0; b < NB; ++b) {
+      const int q = b * PB + ql;
+      const int hr = q / HW, hc = q - (q / HW) * HW;
+      const int ih = h0 - 1 + hr, iw = w0 - 1 + hc;
+      const bool ok = q < NQ && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      glds16(xr, hb + b * 1024, ok ? (unsigned)((ih * (int)a.sH + iw * (int)a.sW) * 2 + c * 16) : PG_OOB);
+    }
+  };
+
+  if (wid == NWC) {
+    if ((int)blockIdx.x < ntiles) issue_halo(blockIdx.x, 0);
+  } else {
+    if (sums) {
+      for (int i = tid; i < 6 * COUT; i += 64 * NWC) red[i] = 0.f;
+      if (tid == 0) *red_cnt = 0;
+    }
+    if constexpr (BNB) {
+      const int nsg = a.seg_m > 0 ? (int)(a.M / a.seg_m) : 1;
+      for (int i = tid; i < nsg * 4 * COUT; i += 64 * NWC) {
+        const int sg = i / (4 * COUT), r = (i / COUT) & 3, ch = i % COUT;
+        const float* src = r == 0 ? a.bnb_istd[0] : r == 1 ? a.bnb_mean[0] : r == 2 ? a.bnb_msc : a.bnb_msh;
+        prm[i] = src[sg * a.bnb_pstride + ch];
+      }
+    }
+    // filters -> LDS (sconv's image: block kk holds COUT rows of 64 B)
+    for (int i = tid; i < NKK * COUT * 4; i += 64 * NWC) {
+      const int kk = i / (COUT * 4), rem = i - kk * COUT * 4;
+      const int rho = rem >> 2, c = rem & 3;
+      const uint4 v =
+          *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(a.w) + (long long)pg_perm(rho) * a.K + kk * 32 + c * 8);
+      *reinterpret_cast<uint4*>(smem + (kk * COUT + rho) * 64 + ((c ^ sc_sw(rho)) << 4)) = v;
+    }
+  }
+
+  int k = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
+    if (wid == NWC) vm_wait<0>();  // this tile's halo has landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // halo k visible; buffer (k+1)&1 and the statistics accumulator free
+    asm volatile("" ::: "memory");
+    if (wid == NWC) {
+      if (tile + G < ntiles) issue_halo(tile + G, (k + 1) & 1);
+      continue;
+    }
+    const int img = tile / (nth * ntw), rem = tile - img * (nth * ntw);
+    const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
+    const long long pimg = (long long)img * HoWo;
+    // per MFMA pixel tile j: this lane's output pixel and its halo position
+    long long px[NTP];
+    bool pv[NTP];
+    int qb[NTP];
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const int m = wid * NTP + j, row = m / TCB, cb = m - (m / TCB) * TCB;
+      const int oh = h0 + row, ow = w0 + cb * 16 + fr;
+      pv[j] = oh < a.Ho && ow < a.Wo;
+      px[j] = pv[j] ? pimg + oh * a.Wo + ow : pimg;
+      qb[j] = row * HW + cb * 16 + fr;
+    }
+    const long long wseg = a.seg_m > 0 ? pimg / a.seg_m : 0;
+    // ---- epilogue operands ahead of the MFMAs
+    Vec16<bf16> yp[NP][NTP];
+    if constexpr (BNB) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p)
+#pragma unroll
+        for (int j = 0; j < NTP; ++j)
+          yp[p][j] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + px[j] * a.ldy + 32 * p + 8 * fq);
+    }
+    // ---- MFMAs: filters (A) and halo (B) from LDS
+    const char* hb = smem + WB + (k & 1) * HB;
+    f32x4 acc[MTC][NTP];
+#pragma unroll
+    for (int i = 0; i < MTC; ++i)
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int KPT = C / 32;  // 32-k steps per tap
+    // taps fully unrolled where the registers allow (no spills), else by rows
+    constexpr int TUN = (NTP <= 2 || (C == 32 && MTC * NTP <= 8)) ? 9 : 3;
+#pragma unroll TUN
+    for (int t = 0; t < 9; ++t) {
+      const int toff = (t / 3) * HW + (t % 3);
+      int qa[NTP];
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) qa[j] = qb[j] + toff;
+#pragma unroll
+    for (int h = 0; h < KPT; ++h) {
+      const int kk = t * KPT + h, c = h * 4 + fq;
+      uint4 af[MTC], bv[NTP];
+#pragma unroll
+      for (int i = 0; i < MTC; ++i) {
+        const int rho = i * 16 + fr;
+        af[i] = *reinterpret_cast<const uint4*>(smem + (kk * COUT + rho) * 64 + ((fq ^ sc_sw(rho)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(hb + hc_addr<C>(qa[j], c));
+#pragma unroll
+      for (int i = 0; i < MTC; ++i)
+#pragma unroll
+        for (int j = 0; j < NTP; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
+                                                              *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j], 0, 0, 0);
+    }
+    }
+    // ---- epilogue: BN statistics or the fused BN-backward reduction, bf16 stores
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int ch0 = 32 * p + 8 * fq;
+      float s1[8], s2[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+      float xa[8], xm[8], ms[8], mh[8];
+      if constexpr (BNB) {
+        const float* pp = prm + wseg * 4 * COUT + ch0;
+        loadf8v(pp, xa);
+        loadf8v(pp + COUT, xm);
+        loadf8v(pp + 2 * COUT, ms);
+        loadf8v(pp + 3 * COUT, mh);
+      }
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+        if (pv[j]) {
+          if constexpr (BNB) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float yv = to_f(yp[p][j].v[e]);
+              v[e] = yv * ms[e] + mh[e] > 0.f ? v[e] : 0.f;
+              s1[e] += v[e];
+              s2[e] += v[e] * ((yv - xm[e]) * xa[e]);
+            }
+          } else if (sums) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += v[e]; s2[e] += v[e] * v[e]; }
+          }
+          Vec16<bf16> o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+          st16<bf16>(reinterpret_cast<bf16*>(a.y) + px[j] * a.ldy + ch0, o);
+        }
+      }
+      if (sums) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
+        if (fr == 15) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            atomicAdd(red + ch0 + e, s1[e]);
+            atomicAdd(red + COUT + ch0 + e, s2[e]);
+          }
+        }
+      }
+    }
+    if (sums) stats_flush<COUT>(red, red_cnt, NWC * (k + 1) - 1, a, 0, tile % ARTSBIR_NSLOT, lane, pimg, 1);
+  }
+  if (wid == NWC) vm_wait<0>();
+}
+
+// shapes the halo-tiled kernel takes
+static bool hconv_ok(const PgArgs& a) {
+  if (a.R != 3 || a.S != 3 || a.pad != 1 || a.stride != 1 || a.M <= 0) return false;
+  if ((a.C != 32 && a.C != 64) || (a.Cout != 32 && a.Cout != 64) || a.K != 9 * a.C) return false;
+  if (a.res_mode || (a.bnb && (a.bnb != 1 || a.bnb_nt != 1 || a.stats))) return false;
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  if (a.Ho != a.H || a.Wo != a.W || a.M % HoWo) return false;
+  // statistics segments are whole images (a tile never spans two)
+  if (a.seg_m > 0 && (a.seg_m % HoWo || a.M % a.seg_m)) return false;
+  if (a.bnb && a.seg_m > 0 && a.M / a.seg_m > HC_MAXSEG) return false;
+  if (a.sW < a.C || a.sN * 2 > 0x7fffffffLL || (long long)a.H * a.sH * 2 > 0x7fffffffLL) return false;
+  const long long nt = (a.M / HoWo) * ((a.Ho + 15) / 16) * ((a.Wo + 15) / 16) * 2;
+  return nt < 0x7fffffffLL;
+}
+
+template <int C, int COUT, int TR, int TC, bool BNB>
+static void hconv_go(const PgArgs& a, hipStream_t st) {
+  using Gm = HcGeom<C, COUT, TR, TC>;
+  const int ntiles = (int)((a.M / ((long long)a.Ho * a.Wo)) * ((a.Ho + TR - 1) / TR) * ((a.Wo + TC - 1) / TC));
+  int per_cu = (160 * 1024) / Gm::LDS;
+  if (per_cu > 4) per_cu = 4;
+  const int g = 256 * per_cu < ntiles ? 256 * per_cu : ntiles;
+  static const char* nm = nullptr;
+  static char buf[64];
+  if (!nm) {
+    snprintf(buf, sizeof buf, "hconv_kernel<%d,%d,%dx%d%s>", C, COUT, TR, TC, BNB ? ",bnb" : "");
+    nm = buf;
+  }
+  set_last_kernel(nm);
+  hipLaunchKernelGGL((hconv_kernel<C, COUT, TR, TC, BNB>), dim3(g), dim3(320), 0, st, a, ntiles);
+}
+
+template <int C, int COUT, bool BNB>
+static void hconv_tiles(const PgArgs& a, hipStream_t st) {
+  // 16 x 16 tiles when the image splits evenly (stem, 112 x 112), else 8 x 16
+  if (a.Ho % 16 == 0 && a.Wo % 16 == 0) hconv_go<C, COUT, 16, 16, BNB>(a, st);
+  else hconv_go<C, COUT, 8, 16, BNB>(a, st);
+}
+
+template <bool BNB>
+static void hconv_dispatch(const PgArgs& a, hipStream_t st) {
+  if (a.C == 32 && a.Cout == 32) hconv_tiles<32, 32, BNB>(a, st);
+  else if (a.C == 32) hconv_tiles<32, 64, BNB>(a, st);
+  else if (a.Cout == 32) hconv_tiles<64, 32, BNB>(a, st);
+  else hconv_tiles<64, 64, BNB>(a, st);
+}
+
+// candidate 21: the halo-tiled small-channel kernel
+bool hconv_launch(const PgArgs& a, hipStream_t st) {
+  if (!hconv_ok(a)) return false;
+  if (a.bnb) hconv_dispatch<true>(a, st);
+  else hconv_dispatch<false>(a, st);
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // launch: pick the tile shape with the best (tile utilisation x CU fill)
 // ---------------------------------------------------------------------------
 struct PgCfg {
@@ -916,6 +1211,7 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (c == 20) return sconv_launch(a, st);
+  if (c == 21) return hconv_launch(a, st);
   bool multi;
   if (!pg_supported(a, multi)) return false;
   if (c == 10) {

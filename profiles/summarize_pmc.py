@@ -41,6 +41,9 @@ def short(name):
     m = re.match(r"_ZN7artsbir12sconv_kernelILi(\d+)ELi(\d+)ELi(\d+)E", name)
     if m:
         return f"sconv_kernel<{m.group(1)},{m.group(2)}{',s2' if m.group(3) == '2' else ''}{bnb}>"
+    m = re.match(r"_ZN7artsbir12hconv_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])E", name)
+    if m:
+        return f"hconv_kernel<{m.group(1)},{m.group(2)},{m.group(3)}x{m.group(4)}{',bnb' if m.group(5) == '1' else ''}>"
     m = re.match(r"_ZN7artsbir\d+(\w+?_kernel)", name)
     if m:
         return m.group(1)
@@ -53,6 +56,8 @@ def short(name):
             return f"{k}<{t[0]},{t[1]}{fb}>"
         if k == "pstream_kernel":
             return f"{k}<{t[0]}{fb}>"
+        if k == "hconv_kernel":
+            return f"{k}<{t[0]},{t[1]},{t[2]}x{t[3]}{',bnb' if t[4] == 'true' else ''}>"
         if k == "sconv_kernel":
             return f"{k}<{t[0]},{t[1]}{',s2' if t[2] == '2' else ''}{fb}>"
         return k

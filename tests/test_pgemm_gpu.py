@@ -24,8 +24,11 @@ CASES = [
     (3, 9, 13, 64, 64, 3, 3, 1, 1),     # layer-1 3x3, image-crossing pixel tiles
     (2, 12, 10, 64, 32, 3, 3, 1, 1),
     (3, 11, 7, 8, 32, 3, 3, 2, 1),      # stem conv1, odd sizes
+    (2, 32, 48, 64, 64, 3, 3, 1, 1),    # halo-tiled kernel, 16 x 16 tiles
+    (2, 32, 16, 32, 64, 3, 3, 1, 1),    # halo-tiled, 16 x 16 tiles, 32 -> 64 channels
+    (3, 17, 23, 64, 32, 3, 3, 1, 1),    # halo-tiled, 8 x 16 tiles with row and column tails
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "10", "20"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "10", "20", "21"]
 
 
 @pytest.fixture
@@ -87,6 +90,7 @@ DG_CASES = [
     (8, 28, 28, 128, 128, 3, 1, 2),
     (3, 9, 13, 64, 64, 3, 1, 0),        # layer-1 3x3 data gradient
     (2, 12, 10, 64, 32, 3, 1, 1),
+    (2, 16, 32, 32, 64, 3, 1, 0),       # halo-tiled data gradient, 16 x 16 tiles
 ]
 
 
