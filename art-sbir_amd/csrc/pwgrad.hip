@@ -270,6 +270,207 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Halo-tiled weight gradient of a 3x3 stride-1 pad-1 convolution with few
+// channels (C in {32, 64} in, Cout in {32, 64} out: stem conv2/conv3,
+// models.py:312-317, and layer-1 conv2, models.py:200-201).  For im2col rows
+// this short the pipelined kernel above gathers every input pixel nine times;
+// here an output tile of TR x 16 pixels of one image brings its dY tile and
+// its (TR+2) x 18 input halo into LDS once (LDS-DMA, loader wave, double
+// buffer) and all nine taps read the halo there.  Each persistent block keeps
+// the whole dW (Cout x 9 x C) in registers across its tiles — compute wave w
+// owns the (input-channel tile, tap) pairs w, w+4, ... for all Cout — and adds
+// it into dW with one round of f32 atomics at the end.  Both operand images
+// use the transposing-read layout of pwgrad_kernel (rows of C or Cout bf16).
+// ---------------------------------------------------------------------------
+template <int C, int COUT, int TR>
+struct HwGeom {
+  static constexpr int NWC = 4, TC = 16, NPX = TR * TC, HW = TC + 2, NQ = HW * (TR + 2);
+  static constexpr int SX = 2 * C, SD = 2 * COUT;        // LDS row bytes (halo pixel, dY pixel)
+  static constexpr int XI = (NQ * SX + 1023) / 1024;     // 1-KB halo DMA instructions
+  static constexpr int DI = NPX * SD / 1024;             // 1-KB dY tile DMA instructions
+  static constexpr int XB = XI * 1024, DB = DI * 1024, STAGE = XB + DB;
+  static constexpr int NJ = C / 16, MTC = COUT / 16, NPAIR = NJ * 9, PPW = (NPAIR + NWC - 1) / NWC;
+};
+
+// transposing read of rows r0 + q (q = t >> 2), 4 columns from byte column cb
+// + 8 (t & 3), of a plain row-major LDS image with `S`-byte rows: the lane's
+// constant part is folded into `lb`, the rest is an immediate offset
+__device__ __forceinline__ pw_v4s hw_tr(const char* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_v4s)(pw_lds_t)(base + off));
+}
+
+template <int C, int COUT, int TR>
+__global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
+  using Gm = HwGeom<C, COUT, TR>;
+  constexpr int NWC = Gm::NWC, TC = Gm::TC, NPX = Gm::NPX, HW = Gm::HW, NQ = Gm::NQ;
+  constexpr int SX = Gm::SX, SD = Gm::SD, XI = Gm::XI, DI = Gm::DI, XB = Gm::XB, STAGE = Gm::STAGE;
+  constexpr int NJ = Gm::NJ, MTC = Gm::MTC, NPAIR = Gm::NPAIR, PPW = Gm::PPW;
+  static_assert(2 * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int ntw = (a.Wo + TC - 1) / TC, nth = (a.Ho + TR - 1) / TR;
+  const int HoWo = a.Ho * a.Wo;
+
+  // operands of tile t -> stage buf (loader wave): row-major images, lane l
+  // of DMA instruction g moves bytes g * 1024 + 16 l .. + 15
+  auto issue = [&](int t, int buf) {
+    const int img = t / (nth * ntw), rem = t - img * (nth * ntw);
+    const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
+    char* xs = smem + buf * STAGE;
+    char* ds = xs + XB;
+    const __amdgpu_buffer_rsrc_t xr =
+        pw_rsrc(reinterpret_cast<const bf16*>(a.x) + (long long)img * a.sN, (a.x_elems - (long long)img * a.sN) * 2);
+#pragma unroll 4
+    for (int g = 0; g < XI; ++g) {
+      const int b = g * 1024 + lane * 16;
+      const int q = b / SX, ci = (b - (b / SX) * SX) >> 1;
+      const int hr = q / HW, hc = q - (q / HW) * HW;
+      const int ih = h0 - 1 + hr, iw = w0 - 1 + hc;
+      const bool ok = q < NQ && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
+      pw_glds16(xr, xs + g * 1024, ok ? (unsigned)((ih * (int)a.sH + iw * (int)a.sW + ci) * 2) : PW_OOB);
+    }
+    const long long pimg = (long long)img * HoWo;
+    const __amdgpu_buffer_rsrc_t dr =
+        pw_rsrc(reinterpret_cast<const bf16*>(a.dy) + pimg * a.ldd, (a.dy_elems - pimg * a.ldd) * 2);
+#pragma unroll 4
+    for (int g = 0; g < DI; ++g) {
+      const int b = g * 1024 + lane * 16;
+      const int m = b / SD, co = (b - (b / SD) * SD) >> 1;
+      const int oh = h0 + m / TC, ow = w0 + m % TC;
+      const bool ok = oh < a.Ho && ow < a.Wo;
+      pw_glds16(dr, ds + g * 1024, ok ? (unsigned)(((oh * a.Wo + ow) * (int)a.ldd + co) * 2) : PW_OOB);
+    }
+  };
+
+  const int t = lane & 15, g = lane >> 4;
+  // lane constants of the transposing reads: row t >> 2, byte column 8 (t & 3)
+  const int la = (t >> 2) * SD + 8 * (t & 3);
+  const int lb = (t >> 2) * SX + 8 * (t & 3);
+  // this wave's (channel tile, tap) pairs as halo byte offsets (uniform);
+  // pairs past NPAIR (uneven split) repeat the last one and are dropped
+  int pofs[PPW];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) {
+    int pi = wid + NWC * p;
+    if (pi >= NPAIR) pi = NPAIR - 1;
+    const int tap = pi / NJ;
+    pofs[p] = ((tap / 3) * HW + tap % 3) * SX + 32 * (pi % NJ);
+  }
+  f32x4 acc[PPW][MTC];
+#pragma unroll
+  for (int p = 0; p < PPW; ++p)
+#pragma unroll
+    for (int i = 0; i < MTC; ++i) acc[p][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (wid == NWC && (int)blockIdx.x < ntiles) issue(blockIdx.x, 0);
+  int k = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
+    if (wid == NWC) pw_vm_wait<0>();  // this tile's operands have landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();      // tile k visible; the other buffer is free
+    asm volatile("" ::: "memory");
+    if (wid == NWC) {
+      if (tile + G < ntiles) issue(tile + G, (k + 1) & 1);
+      continue;
+    }
+    const char* xs = smem + (k & 1) * STAGE;
+    const char* ds = xs + XB;
+#pragma unroll 1
+    for (int ks = 0; ks < NPX / 32; ++ks) {
+      // this lane's 8 pixels m = mb .. mb + 7 lie in one tile row
+      const int mb = ks * 32 + 8 * g;
+      const int row = mb / TC, col0 = mb - (mb / TC) * TC;
+      const char* da = ds + mb * SD + la;
+      bf16x8 af[MTC];
+#pragma unroll
+      for (int i = 0; i < MTC; ++i) {
+        const pw_v4s lo = hw_tr(da, 32 * i);
+        const pw_v4s hi = hw_tr(da, 4 * SD + 32 * i);
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+      const char* xa = xs + (row * HW + col0) * SX + lb;
+#pragma unroll
+      for (int p = 0; p < PPW; ++p) {
+        const pw_v4s lo = hw_tr(xa, pofs[p]);
+        const pw_v4s hi = hw_tr(xa, pofs[p] + 4 * SX);
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < MTC; ++i) acc[p][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bv, acc[p][i], 0, 0, 0);
+      }
+    }
+  }
+  if (wid == NWC) {
+    pw_vm_wait<0>();
+    return;
+  }
+  // acc[p][i][r]: co = 16 i + 4 g + r, input channel 16 j + t of tap `tap`
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) {
+    const int pi = wid + NWC * p;
+    if (pi >= NPAIR) continue;
+    const int j = pi % NJ, tap = pi / NJ;
+#pragma unroll
+    for (int i = 0; i < MTC; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        atomicAdd(a.dw + (long long)(16 * i + 4 * g + r) * a.K + tap * C + 16 * j + t, acc[p][i][r]);
+  }
+}
+
+static bool hwgrad_ok(const PwArgs& a) {
+  if (a.dense || a.R != 3 || a.S != 3 || a.pad != 1 || a.stride != 1 || a.M <= 0) return false;
+  if ((a.C != 32 && a.C != 64) || (a.Cout != 32 && a.Cout != 64) || a.K != 9 * a.C) return false;
+  if (a.Ho != a.H || a.Wo != a.W || a.M % ((long long)a.Ho * a.Wo)) return false;
+  if (a.sW < a.C || a.ldd < a.Cout) return false;
+  if (a.sN * 2 > 0x7fffffffLL || (long long)a.Ho * a.Wo * a.ldd * 2 > 0x7fffffffLL) return false;
+  const long long nt = (a.M / ((long long)a.Ho * a.Wo)) * ((a.Ho + 7) / 8) * ((a.Wo + 15) / 16);
+  return nt < 0x7fffffffLL;
+}
+
+template <int C, int COUT, int TR>
+static void hwgrad_go(const PwArgs& a, hipStream_t st) {
+  using Gm = HwGeom<C, COUT, TR>;
+  const int ntiles = (int)((a.M / ((long long)a.Ho * a.Wo)) * ((a.Ho + TR - 1) / TR) * ((a.Wo + 15) / 16));
+  int per_cu = (160 * 1024) / (2 * Gm::STAGE);
+  if (per_cu > 2) per_cu = 2;
+  const int g = 256 * per_cu < ntiles ? 256 * per_cu : ntiles;
+  hipLaunchKernelGGL((hwgrad_kernel<C, COUT, TR>), dim3(g), dim3(320), 0, st, a, ntiles);
+}
+
+template <int C, int COUT>
+static void hwgrad_tiles(const PwArgs& a, hipStream_t st) {
+  if (a.Ho % 16 == 0 && a.Wo % 16 == 0) hwgrad_go<C, COUT, 16>(a, st);
+  else hwgrad_go<C, COUT, 8>(a, st);
+}
+
+static bool hwgrad_launch(const PwArgs& a, hipStream_t st) {
+  if (!hwgrad_ok(a)) return false;
+  static const char* names[2][2] = {{"hwgrad_kernel<32,32>", "hwgrad_kernel<32,64>"},
+                                    {"hwgrad_kernel<64,32>", "hwgrad_kernel<64,32>x2"}};
+  set_last_kernel(names[a.C == 64][a.Cout == 64]);
+  if (a.C == 32 && a.Cout == 32) {
+    hwgrad_tiles<32, 32>(a, st);
+  } else if (a.C == 32) {
+    hwgrad_tiles<32, 64>(a, st);
+  } else if (a.Cout == 32) {
+    hwgrad_tiles<64, 32>(a, st);
+  } else {
+    // 64 -> 64: two passes over the output-channel halves (the whole dW of
+    // one block would not fit the registers of four waves)
+    PwArgs b = a;
+    b.Cout = 32;
+    b.dy_elems -= 32;
+    hwgrad_tiles<64, 32>(b, st);
+    b.dy = reinterpret_cast<const bf16*>(a.dy) + 32;
+    b.dw = a.dw + 32LL * a.K;
+    hwgrad_tiles<64, 32>(b, st);
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
 // tile configurations (BCO x BKK output tile, waves WCO x WKK, LDS stages)
 struct PwCfg {
   int bco, bkk, threads;
@@ -305,11 +506,14 @@ static const int kSplitTarget[] = {1536, 512, 256};
 static const int kSplitMinSteps[] = {8, 24, 64};
 constexpr int kNumLevels = 3;
 
-int pwgrad_num_cfgs() { return kNumPw * kNumLevels; }
+// candidates: kNumPw tile configurations x kNumLevels split levels, then the
+// halo-tiled small-channel kernel
+int pwgrad_num_cfgs() { return kNumPw * kNumLevels + 1; }
 
 // candidate c = cfg + kNumPw * level of the pipelined wgrad; false (nothing
 // launched) if not applicable
 bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
+  if (cand == kNumPw * kNumLevels) return hwgrad_launch(a, st);
   if (cand < 0 || cand >= kNumPw * kNumLevels) return false;
   const int c = cand % kNumPw, level = cand / kNumPw;
   if (a.Cout % 8 || a.K % 8 || a.M <= 0) return false;

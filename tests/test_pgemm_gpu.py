@@ -134,10 +134,13 @@ WG_CASES = [
     (4, 28, 28, 64, 64, 3, 3, 1, 1),     # many K-steps, split over workgroups
     (3, 12, 12, 512, 64, 1, 1, 2, 0),    # strided 1x1 (not dense)
     (1, 5, 5, 256, 96, 1, 1, 1, 0),      # partial Cout tile
+    (2, 32, 48, 32, 32, 3, 3, 1, 1),     # halo-tiled wgrad, 16 x 16 tiles
+    (3, 17, 23, 64, 64, 3, 3, 1, 1),     # halo-tiled, 8 x 16 tiles with tails, two output-channel passes
+    (2, 16, 16, 64, 32, 3, 3, 1, 1),
 ]
 
 
-@pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "4", "5", "6", "9", "16", "auto"])
+@pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "4", "5", "6", "9", "16", "21", "auto"])
 @pytest.mark.parametrize("case", WG_CASES)
 def test_wgrad_accumulates(case, cfg, dev):
     old = os.environ.get("ARTSBIR_WGRAD_CFG")
