@@ -977,16 +977,25 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
     }
   }
 
+  // the loader and the compute waves run separate loops with one barrier per
+  // tile each (a role branch inside one loop makes the compiler merge and copy
+  // the accumulators every tile)
+  if (wid == NWC) {
+    int k = 0;
+    for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
+      vm_wait<0>();  // this tile's halo has landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (tile + G < ntiles) issue_halo(tile + G, (k + 1) & 1);
+    }
+    vm_wait<0>();
+    return;
+  }
   int k = 0;
   for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
-    if (wid == NWC) vm_wait<0>();  // this tile's halo has landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();   // halo k visible; buffer (k+1)&1 and the statistics accumulator free
     asm volatile("" ::: "memory");
-    if (wid == NWC) {
-      if (tile + G < ntiles) issue_halo(tile + G, (k + 1) & 1);
-      continue;
-    }
     const int img = tile / (nth * ntw), rem = tile - img * (nth * ntw);
     const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
     const long long pimg = (long long)img * HoWo;
@@ -1100,7 +1109,6 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
     }
     if (sums) stats_flush<COUT>(red, red_cnt, NWC * (k + 1) - 1, a, 0, tile % ARTSBIR_NSLOT, lane, pimg, 1);
   }
-  if (wid == NWC) vm_wait<0>();
 }
 
 // shapes the halo-tiled kernel takes

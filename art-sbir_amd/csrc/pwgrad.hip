@@ -270,51 +270,58 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Halo-tiled weight gradient of a 3x3 stride-1 pad-1 convolution with few
-// channels (C in {32, 64} in, Cout in {32, 64} out: stem conv2/conv3,
-// models.py:312-317, and layer-1 conv2, models.py:200-201).  For im2col rows
-// this short the pipelined kernel above gathers every input pixel nine times;
-// here an output tile of TR x 16 pixels of one image brings its dY tile and
-// its (TR+2) x 18 input halo into LDS once (LDS-DMA, loader wave, double
-// buffer) and all nine taps read the halo there.  Each persistent block keeps
-// the whole dW (Cout x 9 x C) in registers across its tiles — compute wave w
-// owns the (input-channel tile, tap) pairs w, w+4, ... for all Cout — and adds
-// it into dW with one round of f32 atomics at the end.  Both operand images
-// use the transposing-read layout of pwgrad_kernel (rows of C or Cout bf16).
+// Halo-tiled weight gradient of a 3x3 stride-1 pad-1 convolution: the stem
+// conv2/conv3 (models.py:312-317) and the Bottleneck conv2 of every stage
+// (models.py:200-201).  The pipelined kernel above gathers every input pixel
+// nine times (implicit im2col) and re-streams dY once per 128-wide k tile;
+// here a workgroup owns one (CT input-channel x OT output-channel) slice of dW
+// for all nine taps, kept in registers across a persistent run of TR x 16
+// output-pixel tiles: per tile the dY slice and the (TR+2) x 18 input-halo
+// slice come into LDS once (LDS-DMA by one loader wave, double buffer) and all
+// nine taps read the halo there.  One round of f32 atomics adds the block's
+// slice into dW at the end.  Compute wave w owns the (16-channel input tile,
+// tap) pairs w, w + NWC, ... for all OT output channels.  LDS images are plain
+// row-major (one halo / output pixel per row); the MFMA fragments, 8
+// consecutive pixels per lane, come from the transposing read
+// ds_read_b64_tr_b16 (2-way bank conflicts at most for every tap offset).
+// Workgroups are numbered so that the NPC channel slices of one pixel-tile
+// group run on the same XCD at the same time and share dY / input through L2.
 // ---------------------------------------------------------------------------
-template <int C, int COUT, int TR>
+template <int CT, int OT, int TR, int NWC>
 struct HwGeom {
-  static constexpr int NWC = 4, TC = 16, NPX = TR * TC, HW = TC + 2, NQ = HW * (TR + 2);
-  static constexpr int SX = 2 * C, SD = 2 * COUT;        // LDS row bytes (halo pixel, dY pixel)
+  static constexpr int TC = 16, NPX = TR * TC, HW = TC + 2, NQ = HW * (TR + 2);
+  static constexpr int SX = 2 * CT, SD = 2 * OT;         // LDS row bytes (halo pixel, dY pixel)
   static constexpr int XI = (NQ * SX + 1023) / 1024;     // 1-KB halo DMA instructions
   static constexpr int DI = NPX * SD / 1024;             // 1-KB dY tile DMA instructions
   static constexpr int XB = XI * 1024, DB = DI * 1024, STAGE = XB + DB;
-  static constexpr int NJ = C / 16, MTC = COUT / 16, NPAIR = NJ * 9, PPW = (NPAIR + NWC - 1) / NWC;
+  static constexpr int NJ = CT / 16, MTC = OT / 16, NPAIR = NJ * 9, PPW = (NPAIR + NWC - 1) / NWC;
 };
 
-// transposing read of rows r0 + q (q = t >> 2), 4 columns from byte column cb
-// + 8 (t & 3), of a plain row-major LDS image with `S`-byte rows: the lane's
-// constant part is folded into `lb`, the rest is an immediate offset
 __device__ __forceinline__ pw_v4s hw_tr(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_v4s)(pw_lds_t)(base + off));
 }
 
-template <int C, int COUT, int TR>
-__global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
-  using Gm = HwGeom<C, COUT, TR>;
-  constexpr int NWC = Gm::NWC, TC = Gm::TC, NPX = Gm::NPX, HW = Gm::HW, NQ = Gm::NQ;
+template <int CT, int OT, int TR, int NWC>
+__global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int ntiles, int npc) {
+  using Gm = HwGeom<CT, OT, TR, NWC>;
+  constexpr int TC = Gm::TC, NPX = Gm::NPX, HW = Gm::HW, NQ = Gm::NQ;
   constexpr int SX = Gm::SX, SD = Gm::SD, XI = Gm::XI, DI = Gm::DI, XB = Gm::XB, STAGE = Gm::STAGE;
   constexpr int NJ = Gm::NJ, MTC = Gm::MTC, NPAIR = Gm::NPAIR, PPW = Gm::PPW;
   static_assert(2 * STAGE <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = gridDim.x;
+  // (pixel-tile group, channel slice): the npc slices of a group share an XCD
+  const int G = gridDim.x / npc;  // groups; gridDim.x is a multiple of 8 * npc
+  const int xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+  const int grp = xcd + 8 * (loc / npc), pc = loc % npc;
+  const int nci = a.C / CT;
+  const int ci0 = (pc % nci) * CT, co0 = (pc / nci) * OT;
   const int ntw = (a.Wo + TC - 1) / TC, nth = (a.Ho + TR - 1) / TR;
   const int HoWo = a.Ho * a.Wo;
 
-  // operands of tile t -> stage buf (loader wave): row-major images, lane l
-  // of DMA instruction g moves bytes g * 1024 + 16 l .. + 15
+  // operands of tile t -> stage buf (loader wave): lane l of DMA instruction
+  // g moves bytes g * 1024 + 16 l .. + 15 of the row-major image
   auto issue = [&](int t, int buf) {
     const int img = t / (nth * ntw), rem = t - img * (nth * ntw);
     const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
@@ -329,7 +336,7 @@ __global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
       const int hr = q / HW, hc = q - (q / HW) * HW;
       const int ih = h0 - 1 + hr, iw = w0 - 1 + hc;
       const bool ok = q < NQ && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W;
-      pw_glds16(xr, xs + g * 1024, ok ? (unsigned)((ih * (int)a.sH + iw * (int)a.sW + ci) * 2) : PW_OOB);
+      pw_glds16(xr, xs + g * 1024, ok ? (unsigned)((ih * (int)a.sH + iw * (int)a.sW + ci0 + ci) * 2) : PW_OOB);
     }
     const long long pimg = (long long)img * HoWo;
     const __amdgpu_buffer_rsrc_t dr =
@@ -340,7 +347,7 @@ __global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
       const int m = b / SD, co = (b - (b / SD) * SD) >> 1;
       const int oh = h0 + m / TC, ow = w0 + m % TC;
       const bool ok = oh < a.Ho && ow < a.Wo;
-      pw_glds16(dr, ds + g * 1024, ok ? (unsigned)(((oh * a.Wo + ow) * (int)a.ldd + co) * 2) : PW_OOB);
+      pw_glds16(dr, ds + g * 1024, ok ? (unsigned)(((oh * a.Wo + ow) * (int)a.ldd + co0 + co) * 2) : PW_OOB);
     }
   };
 
@@ -364,17 +371,26 @@ __global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
 #pragma unroll
     for (int i = 0; i < MTC; ++i) acc[p][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (wid == NWC && (int)blockIdx.x < ntiles) issue(blockIdx.x, 0);
-  int k = 0;
-  for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
-    if (wid == NWC) pw_vm_wait<0>();  // this tile's operands have landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();      // tile k visible; the other buffer is free
-    asm volatile("" ::: "memory");
-    if (wid == NWC) {
+  // the two roles run separate loops with one barrier per tile each (one loop
+  // with a role branch would merge the accumulators of both paths and copy
+  // them every tile)
+  if (wid == NWC) {
+    if (grp < ntiles) issue(grp, 0);
+    int k = 0;
+    for (int tile = grp; tile < ntiles; tile += G, ++k) {
+      pw_vm_wait<0>();  // this tile's operands have landed
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
       if (tile + G < ntiles) issue(tile + G, (k + 1) & 1);
-      continue;
     }
+    pw_vm_wait<0>();
+    return;
+  }
+  int k = 0;
+  for (int tile = grp; tile < ntiles; tile += G, ++k) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile k visible; the other buffer is free
+    asm volatile("" ::: "memory");
     const char* xs = smem + (k & 1) * STAGE;
     const char* ds = xs + XB;
 #pragma unroll 1
@@ -401,11 +417,13 @@ __global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
       }
     }
   }
-  if (wid == NWC) {
-    pw_vm_wait<0>();
-    return;
-  }
-  // acc[p][i][r]: co = 16 i + 4 g + r, input channel 16 j + t of tap `tap`
+  // acc[p][i][r]: co = co0 + 16 i + 4 g + r, input channel ci0 + 16 j + t of tap `tap`.
+  // The lane offset passes through an opaque statement here so that the
+  // compiler cannot hoist all the atomic addresses above the tile loop (they
+  // are loop invariant) and hold them in registers through it.
+  int lo = (co0 + 4 * g) * a.K + ci0 + t;
+  asm volatile("" : "+v"(lo));
+  float* dwl = a.dw + lo;
 #pragma unroll
   for (int p = 0; p < PPW; ++p) {
     const int pi = wid + NWC * p;
@@ -414,58 +432,60 @@ __global__ void __launch_bounds__(320) hwgrad_kernel(PwArgs a, int ntiles) {
 #pragma unroll
     for (int i = 0; i < MTC; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        atomicAdd(a.dw + (long long)(16 * i + 4 * g + r) * a.K + tap * C + 16 * j + t, acc[p][i][r]);
+      for (int r = 0; r < 4; ++r) atomicAdd(dwl + (16 * i + r) * a.K + tap * a.C + 16 * j, acc[p][i][r]);
   }
 }
 
 static bool hwgrad_ok(const PwArgs& a) {
   if (a.dense || a.R != 3 || a.S != 3 || a.pad != 1 || a.stride != 1 || a.M <= 0) return false;
-  if ((a.C != 32 && a.C != 64) || (a.Cout != 32 && a.Cout != 64) || a.K != 9 * a.C) return false;
-  if (a.Ho != a.H || a.Wo != a.W || a.M % ((long long)a.Ho * a.Wo)) return false;
+  const bool small = (a.C == 32 || a.C == 64) && (a.Cout == 32 || a.Cout == 64) && !(a.C == 64 && a.Cout == 64);
+  const bool tiled = a.C % 64 == 0 && a.Cout % 64 == 0;
+  if (!small && !tiled) return false;
+  if (a.K != 9 * a.C || a.Ho != a.H || a.Wo != a.W || a.M % ((long long)a.Ho * a.Wo)) return false;
+  if (a.Ho < 8 || a.Wo < 8) return false;  // tiles mostly padding: the pipelined kernel
   if (a.sW < a.C || a.ldd < a.Cout) return false;
   if (a.sN * 2 > 0x7fffffffLL || (long long)a.Ho * a.Wo * a.ldd * 2 > 0x7fffffffLL) return false;
   const long long nt = (a.M / ((long long)a.Ho * a.Wo)) * ((a.Ho + 7) / 8) * ((a.Wo + 15) / 16);
   return nt < 0x7fffffffLL;
 }
 
-template <int C, int COUT, int TR>
+template <int CT, int OT, int TR, int NWC>
 static void hwgrad_go(const PwArgs& a, hipStream_t st) {
-  using Gm = HwGeom<C, COUT, TR>;
+  using Gm = HwGeom<CT, OT, TR, NWC>;
   const int ntiles = (int)((a.M / ((long long)a.Ho * a.Wo)) * ((a.Ho + TR - 1) / TR) * ((a.Wo + 15) / 16));
+  const int npc = (a.C / CT) * (a.Cout / OT);
   int per_cu = (160 * 1024) / (2 * Gm::STAGE);
   if (per_cu > 2) per_cu = 2;
-  const int g = 256 * per_cu < ntiles ? 256 * per_cu : ntiles;
-  hipLaunchKernelGGL((hwgrad_kernel<C, COUT, TR>), dim3(g), dim3(320), 0, st, a, ntiles);
+  // pixel-tile groups: fill the chip once, a multiple of 8 (one XCD per group)
+  int groups = (256 * per_cu / npc) / 8 * 8;
+  if (groups < 8) groups = 8;
+  const int need = (ntiles + 7) / 8 * 8;
+  if (groups > need) groups = need;
+  hipLaunchKernelGGL((hwgrad_kernel<CT, OT, TR, NWC>), dim3(groups * npc), dim3(64 * (NWC + 1)), 0, st, a, ntiles,
+                     npc);
 }
 
-template <int C, int COUT>
+template <int CT, int OT, int NWC>
 static void hwgrad_tiles(const PwArgs& a, hipStream_t st) {
-  if (a.Ho % 16 == 0 && a.Wo % 16 == 0) hwgrad_go<C, COUT, 16>(a, st);
-  else hwgrad_go<C, COUT, 8>(a, st);
+  if (a.Ho % 16 == 0 && a.Wo % 16 == 0) hwgrad_go<CT, OT, 16, NWC>(a, st);
+  else hwgrad_go<CT, OT, 8, NWC>(a, st);
 }
 
 static bool hwgrad_launch(const PwArgs& a, hipStream_t st) {
   if (!hwgrad_ok(a)) return false;
-  static const char* names[2][2] = {{"hwgrad_kernel<32,32>", "hwgrad_kernel<32,64>"},
-                                    {"hwgrad_kernel<64,32>", "hwgrad_kernel<64,32>x2"}};
-  set_last_kernel(names[a.C == 64][a.Cout == 64]);
   if (a.C == 32 && a.Cout == 32) {
-    hwgrad_tiles<32, 32>(a, st);
+    set_last_kernel("hwgrad_kernel<32,32>");
+    hwgrad_tiles<32, 32, 4>(a, st);
   } else if (a.C == 32) {
-    hwgrad_tiles<32, 64>(a, st);
+    set_last_kernel("hwgrad_kernel<32,64>");
+    hwgrad_tiles<32, 64, 4>(a, st);
   } else if (a.Cout == 32) {
-    hwgrad_tiles<64, 32>(a, st);
+    set_last_kernel("hwgrad_kernel<64,32>");
+    hwgrad_tiles<64, 32, 4>(a, st);
   } else {
-    // 64 -> 64: two passes over the output-channel halves (the whole dW of
-    // one block would not fit the registers of four waves)
-    PwArgs b = a;
-    b.Cout = 32;
-    b.dy_elems -= 32;
-    hwgrad_tiles<64, 32>(b, st);
-    b.dy = reinterpret_cast<const bf16*>(a.dy) + 32;
-    b.dw = a.dw + 32LL * a.K;
-    hwgrad_tiles<64, 32>(b, st);
+    // 64-channel slices of input and output channels, 8 compute waves
+    set_last_kernel("hwgrad_kernel<64,64>");
+    hwgrad_tiles<64, 64, 8>(a, st);
   }
   return true;
 }

@@ -172,8 +172,20 @@ __global__ void __launch_bounds__(256) knn_scan_kernel(KnnScanArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int ntq = (a.Nq + BM - 1) / BM;
-  const int chunk = blockIdx.x / ntq;
-  const int qt = blockIdx.x % ntq;
+  // XCD-aware order: the hardware deals consecutive workgroups round-robin to
+  // the 8 XCDs; remap so that the query tiles of one gallery chunk run on ONE
+  // XCD at the same time and share each gallery tile through its L2 (instead
+  // of every query tile fetching the whole chunk from HBM)
+  int lid = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x;
+    if (nwg >= 8) {
+      const int q8 = nwg / 8, r8 = nwg % 8, x = lid % 8;
+      lid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + lid / 8;
+    }
+  }
+  const int chunk = lid / ntq;
+  const int qt = lid % ntq;
   const int bm = qt * BM;
   const int tile0 = chunk * a.tiles_per_chunk;
   int ntiles = (a.Ng + BN - 1) / BN - tile0;

@@ -227,6 +227,11 @@ def main():
         opt.step()
         return loss
 
+    # the step's own stream: high priority over the side stream the weight
+    # gradients overlap on (ARTSBIR_STEP_PRIO, default 0 = the caller's stream)
+    prio = int(os.environ.get("ARTSBIR_STEP_PRIO", "0"))
+    if prio:
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=prio))
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()

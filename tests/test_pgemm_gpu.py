@@ -137,6 +137,7 @@ WG_CASES = [
     (2, 32, 48, 32, 32, 3, 3, 1, 1),     # halo-tiled wgrad, 16 x 16 tiles
     (3, 17, 23, 64, 64, 3, 3, 1, 1),     # halo-tiled, 8 x 16 tiles with tails, two output-channel passes
     (2, 16, 16, 64, 32, 3, 3, 1, 1),
+    (3, 14, 14, 128, 192, 3, 3, 1, 1),   # halo-tiled, 64-channel slices of input and output
 ]
 
 
