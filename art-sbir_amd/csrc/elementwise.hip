@@ -132,7 +132,8 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
 template <typename T>
 __global__ void block_out_kernel(const T* __restrict__ y3, const float* __restrict__ sc3, const float* __restrict__ sh3,
                                  const T* __restrict__ yd, const float* __restrict__ scd, const float* __restrict__ shd,
-                                 const T* __restrict__ idn, long long rows, int C, T* __restrict__ out) {
+                                 const T* __restrict__ idn, long long rows, int C, T* __restrict__ out,
+                                 unsigned char* __restrict__ bits) {
   const int CG = C / 8;
   const long long n = rows * CG;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -155,6 +156,12 @@ __global__ void block_out_kernel(const T* __restrict__ y3, const float* __restri
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * s[e] + h[e] + r[e], 0.f);
     store8<T>(out + off, a);
+    if (bits) {  // ReLU mask of the stored values, one bit per channel
+      unsigned m = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m |= (to_f(from_f<T>(a[e])) > 0.f ? 1u : 0u) << e;
+      bits[i] = (unsigned char)m;
+    }
   }
 }
 
@@ -212,6 +219,11 @@ __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, lo
     load8<T>(reinterpret_cast<const T*>(a.mask) + offs[0], m);
 #pragma unroll
     for (int e = 0; e < 8; ++e) g[0][e] = m[e] > 0.f ? g[0][e] : 0.f;
+  } else if constexpr (KIND == 3) {
+    load8<T>(reinterpret_cast<const T*>(a.d) + offs[0], g[0]);
+    const unsigned m = reinterpret_cast<const unsigned char*>(a.mask)[(long long)u * (a.C / 8) + cg];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[0][e] = (m >> e) & 1u ? g[0][e] : 0.f;
   } else if constexpr (KIND == 2) {
     load8<T>(reinterpret_cast<const T*>(a.d) + offs[0], g[0]);  // g given (masked upstream)
   } else {
@@ -527,17 +539,23 @@ extern "C" int artsbir_act_pool(int dtype, const void* x, const float* scale, co
   return 0;
 }
 
-extern "C" int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
-                                 const float* scd, const float* shd, const void* identity, long long rows, int C,
-                                 void* out, void* stream) {
+extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
+                                      const float* scd, const float* shd, const void* identity, long long rows, int C,
+                                      void* out, unsigned char* mask_bits, void* stream) {
   if (C % 8) { set_error("block_out: C %% 8 != 0"); return -1; }
   if (!yd && !identity) { set_error("block_out: need downsample or identity input"); return -1; }
   long long n = rows * (C / 8);
   DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)y3, sc3, sh3, (const T*)yd, scd, shd, (const T*)identity, rows, C,
-                                       (T*)out));
+                                       (T*)out, mask_bits));
   ARTSBIR_CHECK_LAUNCH("block_out");
   return 0;
+}
+
+extern "C" int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
+                                 const float* scd, const float* shd, const void* identity, long long rows, int C,
+                                 void* out, void* stream) {
+  return artsbir_block_out_mask(dtype, y3, sc3, sh3, yd, scd, shd, identity, rows, C, out, nullptr, stream);
 }
 
 static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
@@ -548,7 +566,7 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
   if (d->ntarget < 1 || d->ntarget > 2) { set_error("bn_bwd: ntarget must be 1 or 2"); return -1; }
   if (d->kind == 1 && d->pool > 2) { set_error("bn_bwd: pool must be <= 2"); return -1; }
   if (d->kind == 1 && d->pool == 2 && (d->H % 2 || d->W % 2)) { set_error("bn_bwd: odd H/W with pool"); return -1; }
-  if (d->kind < 0 || d->kind > 2) { set_error("bn_bwd: kind must be 0, 1 or 2"); return -1; }
+  if (d->kind < 0 || d->kind > 3) { set_error("bn_bwd: kind must be 0 .. 3"); return -1; }
   if (d->kind != 1 && d->pool > 1) { set_error("bn_bwd: pool only with kind 1"); return -1; }
   if ((long long)d->B * d->H * d->W >= (1LL << 31)) { set_error("bn_bwd: too many pixels"); return -1; }
   a.kind = d->kind; a.pool = d->pool; a.d = d->d; a.mask = d->mask; a.msc = d->mask_scale; a.msh = d->mask_shift;
@@ -578,6 +596,7 @@ static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
   } while (0)
   if (a.kind == 0) BNB_LAUNCH(0, 1);
   else if (a.kind == 2) BNB_LAUNCH(2, 1);
+  else if (a.kind == 3) BNB_LAUNCH(3, 1);
   else if (P == 2) BNB_LAUNCH(1, 2);
   else BNB_LAUNCH(1, 1);
 #undef BNB_LAUNCH

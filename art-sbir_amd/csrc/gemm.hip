@@ -742,7 +742,8 @@ static int bnb_reduce_pass(const ConvArgs& a, const artsbir_bn_bwd_desc* bd, hip
     d.pool = 0;
     d.d = reinterpret_cast<const char*>(a.y) + eo;
     d.gout = reinterpret_cast<char*>(a.y) + eo;
-    if (bd->mask) d.mask = reinterpret_cast<const char*>(bd->mask) + eo;
+    if (bd->mask)  // kind 3: one mask byte per 8 channels
+      d.mask = reinterpret_cast<const char*>(bd->mask) + (bd->kind == 3 ? s * seg_m * (a.Cout / 8) : eo);
     if (bd->mask_scale) { d.mask_scale = bd->mask_scale + po; d.mask_shift = bd->mask_shift + po; }
     for (int t = 0; t < bd->ntarget; ++t) {
       d.y[t] = reinterpret_cast<const char*>(bd->y[t]) + eo;
@@ -833,7 +834,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     p.seg_m = a.nseg > 1 ? a.M / a.nseg : 0;
     p.seg_stride = (long long)ARTSBIR_NSLOT * 2 * a.Cout;
     if (bd) {
-      p.bnb = bd->kind == 1 ? 1 : 2;
+      p.bnb = bd->kind == 1 ? 1 : bd->kind == 3 ? 3 : 2;
       p.bnb_nt = bd->ntarget;
       for (int t = 0; t < bd->ntarget; ++t) {
         p.bnb_y[t] = bd->y[t];
@@ -942,13 +943,20 @@ extern "C" int artsbir_conv2d_dgrad_bnb(const artsbir_conv_desc* d, const void* 
                                         const void* res, int res_mode, const artsbir_bn_bwd_desc* bnb, int nseg,
                                         long long param_stride, void* stream) {
   if (!bnb) { set_error("conv2d_dgrad_bnb: no BN descriptor"); return -1; }
-  if (bnb->kind != 0 && bnb->kind != 1) { set_error("conv2d_dgrad_bnb: kind must be 0 or 1"); return -1; }
+  if (bnb->kind != 0 && bnb->kind != 1 && bnb->kind != 3) {
+    set_error("conv2d_dgrad_bnb: kind must be 0, 1 or 3");
+    return -1;
+  }
+  if (bnb->kind == 3 && (d->dtype != ARTSBIR_DT_BF16 || d->C % 8)) {
+    set_error("conv2d_dgrad_bnb: bit masks (kind 3) need bf16 and C %% 8 == 0");
+    return -1;
+  }
   if (bnb->kind == 1 && bnb->pool > 1) { set_error("conv2d_dgrad_bnb: pooled BN inputs are not fused"); return -1; }
   if (bnb->ntarget < 1 || bnb->ntarget > 2 || (bnb->kind == 1 && bnb->ntarget != 1)) {
     set_error("conv2d_dgrad_bnb: bad target count %d", bnb->ntarget);
     return -1;
   }
-  if (bnb->kind == 0 ? !bnb->mask : (!bnb->mask_scale || !bnb->mask_shift)) {
+  if (bnb->kind != 1 ? !bnb->mask : (!bnb->mask_scale || !bnb->mask_shift)) {
     set_error("conv2d_dgrad_bnb: missing ReLU mask");
     return -1;
   }

@@ -26,7 +26,8 @@ struct PgArgs {
   // fused BatchNorm-backward reduction (data gradient only, no stats): the
   // output d is the gradient at a BN(+ReLU) output; g = d * mask is stored and
   // sum g, sum g * xhat_t are added to bnb_slots[t] ([nseg][NSLOT][2][Cout])
-  int bnb;                // 0 off; 1: mask y_0 * msc + msh > 0; 2: mask bnb_mask > 0
+  int bnb;                // 0 off; 1: mask y_0 * msc + msh > 0; 2: mask bnb_mask > 0;
+                          // 3: bnb_mask holds one bit per channel ([M][Cout/8] bytes)
   int bnb_nt;             // BN inputs sharing g (1 or 2)
   const void* bnb_y[2];   // bf16 [M][ldy] BN inputs (pre-BN convolution outputs)
   const float* bnb_mean[2];

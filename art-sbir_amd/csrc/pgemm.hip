@@ -242,6 +242,7 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
 #pragma unroll
     for (int j0 = 0; j0 < NTP; j0 += EJ) {
       Vec16<bf16> rv[EJ], y0v[EJ], mkv[EJ], y1v[EJ];
+      unsigned mbits[EJ];
       float rsc[EJ];
 #pragma unroll
       for (int u = 0; u < EJ; ++u) {
@@ -263,6 +264,7 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
           const long long off = pc * a.ldy + chc;
           y0v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + off);
           if (a.bnb == 2) mkv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + off);
+          if (a.bnb == 3) mbits[u] = reinterpret_cast<const unsigned char*>(a.bnb_mask)[pc * (a.Cout >> 3) + (chc >> 3)];
           if (two) y1v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + off);
         }
       }
@@ -286,7 +288,9 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float yv = to_f(y0v[u].v[e]);
-              const bool keep = a.bnb == 1 ? yv * ms[e] + mh[e] > 0.f : to_f(mkv[u].v[e]) > 0.f;
+              const bool keep = a.bnb == 1   ? yv * ms[e] + mh[e] > 0.f
+                                : a.bnb == 3 ? ((mbits[u] >> e) & 1u) != 0u
+                                             : to_f(mkv[u].v[e]) > 0.f;
               v[e] = keep ? v[e] : 0.f;
               s1[e] += v[e];
               s2[e] += v[e] * (yv * xa0[e] + xb0[e]);

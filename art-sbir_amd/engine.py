@@ -47,6 +47,9 @@ BN_MOMENTUM = 0.1
 FUSE_BNB = os.environ.get("ARTSBIR_FUSE_BNB", "1") != "0"
 # ARTSBIR_OVERLAP_WGRAD=0 keeps the weight gradients on the caller's stream
 OVERLAP_WGRAD = os.environ.get("ARTSBIR_OVERLAP_WGRAD", "1") != "0"
+# ARTSBIR_MASK_BITS=0 makes the fused backward re-read the block output for its
+# ReLU mask instead of the bit mask written by the forward
+MASK_BITS = os.environ.get("ARTSBIR_MASK_BITS", "1") != "0"
 
 # bumped by optim.Adam (which updates parameters through raw pointers, invisible
 # to torch's version counters) so packed weights are rebuilt after every step
@@ -336,13 +339,20 @@ class Engine:
         Bs = B // G
         C = out.shape[-1]
         rows = out[0].numel() // C * Bs
+        # bf16 training: the ReLU mask of the block output as bits for the fused
+        # backward (kind 3), 1/16 of re-reading `out` there
+        bits = None
+        if train and FUSE_BNB and MASK_BITS and self.dt == _hip.DT_BF16:
+            bits = torch.empty(out.numel() // 8, dtype=torch.uint8, device=out.device)
         for g in range(G):
             s3 = b3.seg(g)
             sd = bd.seg(g) if bd is not None else None
-            call("artsbir_block_out", self.dt, _at(y3, g * Bs), ptr(s3.scale), ptr(s3.shift),
+            call("artsbir_block_out_mask", self.dt, _at(y3, g * Bs), ptr(s3.scale), ptr(s3.shift),
                  _at(yd, g * Bs), ptr(sd.scale) if sd else None, ptr(sd.shift) if sd else None,
-                 None if yd is not None else _at(h, g * Bs), rows, C, _at(out, g * Bs), _s())
-        ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, b1=b1, b2=b2, b3=b3, bd=bd)
+                 None if yd is not None else _at(h, g * Bs), rows, C, _at(out, g * Bs),
+                 (bits.data_ptr() + g * rows * (C // 8)) if bits is not None else None, _s())
+        ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, bits=bits, b1=b1, b2=b2, b3=b3,
+                   bd=bd)
         return out, ctx
 
     def _attnpool_fwd(self, ap, pk, h):
@@ -587,7 +597,7 @@ class Engine:
         # algorithmic bytes: dy, w, dx once; residual; BN-backward operands (y_t, mask)
         nb = px * co + co * R * S * C + px * C + (px * C if res_mode == 1 else px * C // 4 if res_mode == 2 else 0)
         if fused is not None:
-            nb += px * C * (fused[0].ntarget + (1 if fused[0].kind == 0 else 0))
+            nb += px * C * (fused[0].ntarget + {0: 1.0, 3: 1.0 / 16}.get(fused[0].kind, 0.0))
         nbytes = float(es * nb)
         if fused is None:
             call("artsbir_conv2d_dgrad", d, ptr(dy), ptr(dw), ptr(dx), ptr(res), res_mode, _s(),
@@ -649,7 +659,10 @@ class Engine:
         if prev is not None and FUSE_BNB:
             pblk, pc = prev
             ptargets = [(pc["y3"], pc["b3"])] + ([(pc["yd"], pc["bd"])] if pblk.downsample is not None else [])
-            fprev = self._bnb_fused_desc(0, ptargets, ws, mask=pc["out"])
+            if pc.get("bits") is not None:
+                fprev = self._bnb_fused_desc(3, ptargets, ws, mask=pc["bits"])
+            else:
+                fprev = self._bnb_fused_desc(0, ptargets, ws, mask=pc["out"])
         dh = self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=res, res_mode=res_mode, fused=fprev)
         return dh, fprev
 

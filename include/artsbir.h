@@ -84,7 +84,8 @@ int artsbir_conv2d_fwd_seg(const artsbir_conv_desc* d, const void* x, const void
 /* conv2d_dgrad whose output is the gradient at the output of a BatchNorm2d(+ReLU)
  * (models.py:199-210, 234-235): the BN-backward reduction is fused into it.  dx
  * receives g = dx_raw * relu-mask (bnb->kind 1: y[0]*mask_scale+mask_shift > 0;
- * kind 0: mask > 0, the block output) and bnb->slots[t] += (sum g, sum g*xhat_t)
+ * kind 0: mask > 0, the block output; kind 3: the block output's mask bits, bf16
+ * only) and bnb->slots[t] += (sum g, sum g*xhat_t)
  * exactly as artsbir_bn_bwd_reduce; finish with artsbir_bn_bwd_finalize and
  * artsbir_bn_bwd_apply of kind 2 (g given).  bnb->pool must be 0/1.  With nseg
  * segments the per-channel BN parameters of segment s are at +s*param_stride
@@ -120,12 +121,19 @@ int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* 
 int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
                       const float* scd, const float* shd, const void* identity, long long rows, int C,
                       void* out, void* stream);
+/* The same, also writing the block output's ReLU mask as bits: mask_bits[row][C/8],
+ * bit e of byte c = out[row][8c+e] > 0 (the backward's kind-3 mask: 1/16 of the
+ * bytes of re-reading out). */
+int artsbir_block_out_mask(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
+                           const float* scd, const float* shd, const void* identity, long long rows, int C,
+                           void* out, unsigned char* mask_bits, void* stream);
 
 /* BatchNorm2d(train) backward, see elementwise.hip for the math. */
 struct artsbir_bn_bwd_desc {
   int dtype;
   int kind;               /* 0: g = d*(mask>0) (block output); 1: g = up(d)*(y*mask_scale+mask_shift>0);
-                             2: g = d (already masked, artsbir_conv2d_dgrad_bnb) */
+                             2: g = d (already masked, artsbir_conv2d_dgrad_bnb);
+                             3: as 0 with mask = mask bits of artsbir_block_out_mask (reduce, dgrad_bnb) */
   int pool;               /* kind 1: d is at 1/pool resolution (AvgPool backward) */
   const void* d;
   const void* mask;

@@ -102,11 +102,20 @@ def _bnb_reference(d, kind, ys, means, istds, msc, msh, mask):
     return g, sums
 
 
+def _pack_bits(mask_nhwc):
+    """[..., C] -> uint8 [..., C/8]: bit e of byte c = mask[..., 8c+e] > 0"""
+    m = (mask_nhwc > 0).to(torch.uint8).reshape(*mask_nhwc.shape[:-1], -1, 8)
+    return (m << torch.arange(8, dtype=torch.uint8, device=m.device)).sum(-1).to(torch.uint8)
+
+
+@pytest.mark.parametrize("bits", [False, True])
 @pytest.mark.parametrize("cfg", CFGS)
 @pytest.mark.parametrize("case", BNB_CASES)
-def test_dgrad_fused_bn_reduce(case, cfg, dev, cfg_env):
+def test_dgrad_fused_bn_reduce(case, cfg, bits, dev, cfg_env):
     _set(cfg)
     N, G, H, W, Ci, Co, R, pd, kind, nt, rm = case
+    if bits and kind != 0:
+        pytest.skip("mask bits replace the block-output mask (kind 0) only")
     g = torch.Generator().manual_seed(7)
     dy = torch.randn(N, Co, H, W, generator=g).bfloat16().float()
     w = (torch.randn(Co, Ci, R, R, generator=g) / (Co * R * R) ** 0.5).bfloat16().float()
@@ -135,9 +144,10 @@ def test_dgrad_fused_bn_reduce(case, cfg, dev, cfg_env):
     dx = torch.full((N * H * W, Ci), float("nan"), device=dev, dtype=torch.bfloat16)
     desc = _hip.BnBwdDesc()
     desc.dtype = _hip.DT_BF16
-    desc.kind = kind
+    desc.kind = 3 if bits else kind
     desc.pool = 0
-    desc.mask = maskd.data_ptr() if kind == 0 else None
+    maskb = _pack_bits(maskd) if bits else None
+    desc.mask = (maskb.data_ptr() if bits else maskd.data_ptr()) if kind == 0 else None
     desc.mask_scale = pd_[0][0, 2].data_ptr() if kind == 1 else None
     desc.mask_shift = pd_[0][0, 3].data_ptr() if kind == 1 else None
     desc.ntarget = nt
@@ -223,3 +233,27 @@ def test_forward_branches_matches_separate_calls(dtype, dev):
     for k, gs in grads_s.items():
         err = (grads_b[k] - gs).norm().item() / max(gs.norm().item(), floor)
         assert err < 2e-2, (k, err)
+
+
+@pytest.mark.parametrize("C", [64, 256])
+def test_block_out_mask_bits(C, dev):
+    """artsbir_block_out_mask: the same output as artsbir_block_out plus its
+    ReLU mask as bits (the fused backward's kind-3 mask)"""
+    g = torch.Generator(device=dev).manual_seed(3)
+    rows = 3 * 7 * 5
+    y3 = torch.randn(rows, C, device=dev, generator=g).bfloat16()
+    idn = torch.randn(rows, C, device=dev, generator=g).bfloat16()
+    sc = torch.randn(C, device=dev, generator=g)
+    sh = torch.randn(C, device=dev, generator=g)
+    out0 = torch.empty_like(y3)
+    out1 = torch.empty_like(y3)
+    bits = torch.full((rows, C // 8), 77, dtype=torch.uint8, device=dev)
+    _hip.call("artsbir_block_out", _hip.DT_BF16, y3.data_ptr(), sc.data_ptr(), sh.data_ptr(), None, None, None,
+              idn.data_ptr(), rows, C, out0.data_ptr(), _hip.stream())
+    _hip.call("artsbir_block_out_mask", _hip.DT_BF16, y3.data_ptr(), sc.data_ptr(), sh.data_ptr(), None, None, None,
+              idn.data_ptr(), rows, C, out1.data_ptr(), bits.data_ptr(), _hip.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out0, out1)
+    ref = torch.relu(y3.float() * sc + sh + idn.float()).bfloat16()
+    assert torch.allclose(out1.float(), ref.float(), atol=3e-2, rtol=1e-2)
+    assert torch.equal(bits, _pack_bits(out1))
