@@ -795,13 +795,17 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
+  // time the candidates on a quiet device: work queued on other streams (the
+  // caller's overlapped weight gradients) would otherwise share the chip with
+  // some trials and not others and make the choice noisy
+  (void)hipDeviceSynchronize();
   static const int cands[] = {-2, 0, 1, 2, 3, 4, 10, 20, 21};
   int best = -2;
   float best_ms = 1e30f;
   for (int c : cands) {
     if (!run_candidate(c, at, pt, st)) continue;  // also the warm-up
     float ms = 1e30f;
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(e0, st);
       run_candidate(c, at, pt, st);
       hipEventRecord(e1, st);
@@ -1100,12 +1104,13 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
+  (void)hipDeviceSynchronize();  // quiet device (see tune_conv)
   int best = -1;
   float best_ms = 1e30f;
   for (int c = -1; c < pwgrad_num_cfgs(); ++c) {
     if (!run_wg_candidate(c, at, st)) continue;
     float ms = 1e30f;
-    for (int rep = 0; rep < 2; ++rep) {
+    for (int rep = 0; rep < 3; ++rep) {
       hipEventRecord(e0, st);
       run_wg_candidate(c, at, st);
       hipEventRecord(e1, st);

@@ -55,6 +55,19 @@ def get_loss(loss_fn, model, elements):
 
 def triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
                   stale_eval=False):
+    # the training loop runs on a high-priority stream, so the dispatcher serves
+    # the data-gradient / BatchNorm chain ahead of the weight gradients that the
+    # engine overlaps on its side stream
+    if torch.device(device).type == "cuda":
+        with torch.cuda.stream(torch.cuda.Stream(device=device, priority=-1)):
+            return _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer,
+                                  with_classification, stale_eval)
+    return _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
+                          stale_eval)
+
+
+def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
+                   stale_eval=False):
     start_time = timer()
     train_losses, test_losses, itrain_losses, itest_losses = [], [], [], []
     iteration_loss_frequency = 10000 // train_dataloader.batch_size if epochs <= 6 else 0

@@ -227,9 +227,10 @@ def main():
         opt.step()
         return loss
 
-    # the step's own stream: high priority over the side stream the weight
-    # gradients overlap on (ARTSBIR_STEP_PRIO, default 0 = the caller's stream)
-    prio = int(os.environ.get("ARTSBIR_STEP_PRIO", "0"))
+    # the step runs on a high-priority stream: the dispatcher then serves the
+    # HBM-bound data-gradient / BatchNorm chain first and the weight gradients
+    # of the side stream (engine.py) fill in (ARTSBIR_STEP_PRIO=0: torch's stream)
+    prio = int(os.environ.get("ARTSBIR_STEP_PRIO", "-1"))
     if prio:
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=prio))
     for _ in range(args.warmup):
