@@ -66,6 +66,9 @@ SIGNATURES = {
     "artsbir_act_pool": [_c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp],
     "artsbir_block_out_mask": [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
+    "artsbir_layernorm_fwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp],
+    "artsbir_quickgelu": [_c_int, _vp, _c_ll, _vp, _vp],
+    "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_bn_bwd_reduce": [_PB, _vp],
     "artsbir_bn_bwd_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp],
     "artsbir_bn_bwd_apply": [_PB, _vp],

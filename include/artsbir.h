@@ -165,6 +165,20 @@ int artsbir_attnpool_fwd(int dtype, const float* q, const void* kv, int B, int C
 int artsbir_attnpool_bwd(int dtype, const float* q, const void* kv, const float* p, const float* dout,
                          int B, int C, int heads, int T, void* dq, void* dkv, void* stream);
 
+/* ---- transformer block (models.py:382-417; SURVEY a7, forward) --------- */
+/* LayerNorm computed in fp32 whatever the storage dtype (models.py:382-388):
+ * y[r] = (x[r] - mean) / sqrt(var + eps) * gamma + beta, rows of C. */
+int artsbir_layernorm_fwd(int dtype, const void* x, const float* gamma, const float* beta, long long rows, int C,
+                          float eps, void* y, void* stream);
+/* QuickGELU (models.py:391-393): y = x * sigmoid(1.702 x), n elements. */
+int artsbir_quickgelu(int dtype, const void* x, long long n, void* y, void* stream);
+/* Self-attention core of nn.MultiheadAttention (models.py:399,409-411), seq-first:
+ * qkv [L*N][3E] (the in-projection output, rows (position, batch)), out [L*N][E] =
+ * softmax(q k^T / sqrt(64) + mask) v per head; head_dim 64, L <= 256, mask
+ * [L][L] additive f32 or NULL. */
+int artsbir_mha_fwd(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out,
+                    void* stream);
+
 /* ---- loss and optimizer (train.py:158,169) ------------------------------ */
 int artsbir_triplet_fwd(const float* a, const float* p, const float* n, int B, int D, float margin, float eps,
                         float* dist, float* loss, void* stream);

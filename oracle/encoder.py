@@ -5,6 +5,8 @@ Follows /root/reference/models.py:
   AttentionPool2d       models.py:239-272  (F.multi_head_attention_forward, q = token 0)
   ModifiedResNet        models.py:275-360  (3-conv stem, avgpool anti-aliasing, attnpool head)
   ..._with_classification models.py:363-379
+  LayerNorm / QuickGELU / ResidualAttentionBlock models.py:382-417 (block only;
+                        no reference model builds it)
 State-dict keys are identical to the reference so checkpoints interchange.
 No torchvision: the PIL ``transform`` of models.py:289-295 is not part of the
 compute path (synthetic tensors are fed directly).
@@ -138,6 +140,42 @@ class ModifiedResNet_with_classification(ModifiedResNet):
 # golden fixtures and for every parity test: the same seed gives the same
 # weights on any machine and in the HIP path.
 # ---------------------------------------------------------------------------
+def layernorm_fp32(x, weight, bias, eps=1e-5):
+    """models.py:382-388: LayerNorm evaluated in fp32, result cast back to x's dtype"""
+    xf = x.float()
+    mu = xf.mean(-1, keepdim=True)
+    var = ((xf - mu) ** 2).mean(-1, keepdim=True)
+    return ((xf - mu) / torch.sqrt(var + eps) * weight + bias).to(x.dtype)
+
+
+def quick_gelu(x):
+    """models.py:391-393"""
+    return x * torch.sigmoid(1.702 * x)
+
+
+def residual_attention_block(x, sd, n_head, attn_mask=None, eps=1e-5):
+    """models.py:396-417 on a state dict with the reference keys (attn.in_proj_*,
+    attn.out_proj.*, ln_1.*, mlp.c_fc.*, mlp.c_proj.*, ln_2.*): x [L, N, E],
+    seq-first; self-attention of nn.MultiheadAttention written out (q scaled by
+    1/sqrt(head_dim), additive float mask, softmax over keys)."""
+    L, N, E = x.shape
+    hd = E // n_head
+    h = layernorm_fp32(x, sd["ln_1.weight"], sd["ln_1.bias"], eps)
+    qkv = h @ sd["attn.in_proj_weight"].t() + sd["attn.in_proj_bias"]
+    q, k, v = qkv.split(E, dim=-1)
+
+    def heads(t):  # [L, N, E] -> [N, heads, L, hd]
+        return t.reshape(L, N, n_head, hd).permute(1, 2, 0, 3)
+    s = (heads(q) / hd ** 0.5) @ heads(k).transpose(-1, -2)
+    if attn_mask is not None:
+        s = s + attn_mask
+    o = (torch.softmax(s, dim=-1) @ heads(v)).permute(2, 0, 1, 3).reshape(L, N, E)
+    x = x + (o @ sd["attn.out_proj.weight"].t() + sd["attn.out_proj.bias"])
+    h = layernorm_fp32(x, sd["ln_2.weight"], sd["ln_2.bias"], eps)
+    f = quick_gelu(h @ sd["mlp.c_fc.weight"].t() + sd["mlp.c_fc.bias"])
+    return x + (f @ sd["mlp.c_proj.weight"].t() + sd["mlp.c_proj.bias"])
+
+
 def init_params(model: nn.Module, seed: int = 1234) -> None:
     rng = np.random.Generator(np.random.PCG64(seed))
     with torch.no_grad():
