@@ -69,6 +69,10 @@ SIGNATURES = {
     "artsbir_layernorm_fwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp],
     "artsbir_quickgelu": [_c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_bn_finalize_seg": [_vp, _c_int, _c_ll, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float,
+                                _c_float, _c_int, _vp, _vp],
+    "artsbir_bn_bwd_finalize_seg": [_vp, _c_int, _c_ll, _c_int, ctypes.c_double, _vp, _vp, _c_ll, _vp, _vp, _vp,
+                                    _vp],
     "artsbir_bn_bwd_reduce": [_PB, _vp],
     "artsbir_bn_bwd_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp],
     "artsbir_bn_bwd_apply": [_PB, _vp],

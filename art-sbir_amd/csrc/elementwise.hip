@@ -90,6 +90,43 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int C, doubl
   shift[c] = beta[c] - (float)mean * sc;
 }
 
+// all nseg BN segments of one layer in one launch: per channel the segments in
+// order (running statistics updated once per segment, as the reference's
+// consecutive forward calls do); out[s] = {mean, istd, scale, shift}[C]
+__global__ void bn_finalize_seg_kernel(const float* __restrict__ stats, int nseg, long long seg_stride, int C,
+                                       double count, const float* gamma, const float* beta, float* rmean, float* rvar,
+                                       long long* nbt, float momentum, float eps, int train, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && train && nbt) nbt[0] += nseg;
+  if (c >= C) return;
+  for (int s = 0; s < nseg; ++s) {
+    double mean, var;
+    if (train) {
+      const float* st = stats + s * seg_stride;
+      double s1 = 0, s2 = 0;
+      for (int k = 0; k < ARTSBIR_NSLOT; ++k) {
+        s1 += st[(long long)k * 2 * C + c];
+        s2 += st[(long long)k * 2 * C + C + c];
+      }
+      mean = s1 / count;
+      var = s2 / count - mean * mean;
+      if (var < 0) var = 0;
+      if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+      if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * count / (count > 1 ? count - 1 : 1));
+    } else {
+      mean = rmean[c];
+      var = rvar[c];
+    }
+    const float is = (float)(1.0 / sqrt(var + (double)eps));
+    const float sc = gamma[c] * is;
+    float* o = out + (long long)s * 4 * C;
+    o[c] = (float)mean;
+    o[C + c] = is;
+    o[2 * C + c] = sc;
+    o[3 * C + c] = beta[c] - (float)mean * sc;
+  }
+}
+
 // ------------------------------------------------ affine(+relu)(+avgpool 2x2)
 // out = pool?( act(x) ), act = x*sc+sh then ReLU (sc==NULL: identity, no relu)
 template <typename T>
@@ -353,6 +390,30 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
   }
 }
 
+// all segments of one BN backward in one launch: slots of segment s at
+// + s * seg_stride, its istd at + s * istd_stride; dgamma/dbeta accumulate the
+// segments in order; coef[s] = {c1, c2, c3}[C]
+__global__ void bn_bwd_finalize_seg_kernel(const float* __restrict__ slots, int nseg, long long seg_stride, int C,
+                                           double count, const float* gamma, const float* istd, long long istd_stride,
+                                           float* dgamma, float* dbeta, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  for (int s = 0; s < nseg; ++s) {
+    const float* sl = slots + s * seg_stride;
+    double s1 = 0, s2 = 0;
+    for (int k = 0; k < ARTSBIR_NSLOT; ++k) {
+      s1 += sl[(long long)k * 2 * C + c];
+      s2 += sl[(long long)k * 2 * C + C + c];
+    }
+    if (dbeta) dbeta[c] += (float)s1;
+    if (dgamma) dgamma[c] += (float)s2;
+    float* co = coef + (long long)s * 3 * C;
+    co[c] = gamma[c] * istd[s * istd_stride + c];
+    co[C + c] = (float)(s1 / count);
+    co[2 * C + c] = (float)(s2 / count);
+  }
+}
+
 // slots -> dgamma, dbeta (written into the parameter-gradient buffers) and the
 // apply coefficients c1 = gamma*istd, c2 = sum(g)/cnt, c3 = sum(g*xhat)/cnt
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ slots, int C, double count, const float* gamma,
@@ -527,6 +588,20 @@ extern "C" int artsbir_bn_finalize(const float* stats, int C, double count, cons
   return 0;
 }
 
+extern "C" int artsbir_bn_finalize_seg(const float* stats, int nseg, long long seg_stride, int C, double count,
+                                       const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                       long long* num_batches_tracked, float momentum, float eps, int train,
+                                       float* out, void* stream) {
+  if (nseg < 1) { set_error("bn_finalize_seg: nseg=%d", nseg); return -1; }
+  if (train && !stats) { set_error("bn_finalize: train mode needs stats"); return -1; }
+  if (!train && (!running_mean || !running_var)) { set_error("bn_finalize: eval mode needs running stats"); return -1; }
+  hipLaunchKernelGGL(bn_finalize_seg_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, stats, nseg,
+                     seg_stride, C, count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+                     train, out);
+  ARTSBIR_CHECK_LAUNCH("bn_finalize_seg");
+  return 0;
+}
+
 extern "C" int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* shift, int relu, int pool,
                                 int B, int H, int W, int C, void* out, void* stream) {
   if (C % 8) { set_error("act_pool: C %% 8 != 0"); return -1; }
@@ -615,6 +690,16 @@ extern "C" int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream) 
   if (fill_bnb(a, d)) return -1;
   DISPATCH_T(d->dtype, launch_bnb<T>(a, false, (hipStream_t)stream));
   ARTSBIR_CHECK_LAUNCH("bn_bwd_apply");
+  return 0;
+}
+
+extern "C" int artsbir_bn_bwd_finalize_seg(const float* slots, int nseg, long long seg_stride, int C, double count,
+                                           const float* gamma, const float* istd, long long istd_stride,
+                                           float* dgamma, float* dbeta, float* coef, void* stream) {
+  if (nseg < 1) { set_error("bn_bwd_finalize_seg: nseg=%d", nseg); return -1; }
+  hipLaunchKernelGGL(bn_bwd_finalize_seg_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, slots, nseg,
+                     seg_stride, C, count, gamma, istd, istd_stride, dgamma, dbeta, coef);
+  ARTSBIR_CHECK_LAUNCH("bn_bwd_finalize_seg");
   return 0;
 }
 

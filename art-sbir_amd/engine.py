@@ -237,14 +237,10 @@ class Engine:
         C = bnmod.num_features
         G = self._G
         st = BNState(torch.empty(G, 4, C, dtype=torch.float32, device=bnmod.weight.device), float(count))
-        per = 2 * NSLOT * C
-        for i in range(G):
-            call("artsbir_bn_finalize", ptr(stats_buf[i * per:]) if train else None, C, float(count),
-                 ptr(bnmod.weight.detach()), ptr(bnmod.bias.detach()),
-                 ptr(bnmod.running_mean), ptr(bnmod.running_var),
-                 ptr(bnmod.num_batches_tracked) if train else None,
-                 BN_MOMENTUM, BN_EPS, 1 if train else 0,
-                 ptr(st.buf[i, 0]), ptr(st.buf[i, 1]), ptr(st.buf[i, 2]), ptr(st.buf[i, 3]), _s())
+        call("artsbir_bn_finalize_seg", ptr(stats_buf) if train else None, G, 2 * NSLOT * C, C, float(count),
+             ptr(bnmod.weight.detach()), ptr(bnmod.bias.detach()), ptr(bnmod.running_mean), ptr(bnmod.running_var),
+             ptr(bnmod.num_batches_tracked) if train else None, BN_MOMENTUM, BN_EPS, 1 if train else 0,
+             ptr(st.buf), _s())
         return st
 
     def _conv_bn(self, a, conv, bnmod, fw, stride, pad, train, stats):
@@ -453,7 +449,10 @@ class Engine:
         G = self._G
         Bs = B // G
         dys = [torch.empty_like(y) for y, _ in targets]
-        for s in range(G):
+        per = 2 * NSLOT * C
+        slots = [ws.take(C * G) for _ in targets]  # [G][NSLOT][2][C] per target
+        descs = []
+        for s in range(G):  # every segment's reduction first ...
             desc = _hip.BnBwdDesc()
             desc.dtype = self.dt
             desc.kind = kind
@@ -464,36 +463,37 @@ class Engine:
             desc.mask_scale = ptr(mb.scale) if mb else None
             desc.mask_shift = ptr(mb.shift) if mb else None
             desc.ntarget = len(targets)
-            slots = []
             for i, (y, st) in enumerate(targets):
                 ss = st.seg(s)
                 desc.y[i] = _at(y, s * Bs)
                 desc.mean[i] = ptr(ss.mean)
                 desc.istd[i] = ptr(ss.istd)
-                sl = ws.take(C)
-                slots.append(sl)
-                desc.slots[i] = ptr(sl)
+                desc.slots[i] = ptr(slots[i][s * per:])
             desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
             call("artsbir_bn_bwd_reduce", desc, _s())
-            self._bn_apply(desc, targets, bnmods, slots, grads, dys, s)
+            descs.append(desc)
+        # ... then one finalisation per target for all segments, then the applies
+        coefs = self._bn_coefs(targets, bnmods, slots, grads, float(Bs * H * W))
+        for s, desc in enumerate(descs):
+            for i in range(len(targets)):
+                desc.coef[i] = ptr(coefs[i][s])
+                desc.dy[i] = _at(dys[i], s * Bs)
             desc.gout = _at(gout, s * Bs)
             call("artsbir_bn_bwd_apply", desc, _s())
         return dys
 
-    def _bn_apply(self, desc, targets, bnmods, slots, grads, dys, s):
-        """finalise segment s (parameter gradients += , apply coefficients) and
-        point desc at its outputs; the caller launches the apply."""
-        C = desc.C
-        count = float(desc.B * desc.H * desc.W)
-        desc._keep = []
+    def _bn_coefs(self, targets, bnmods, slots, grads, count):
+        """parameter gradients (+=) and apply coefficients [G][3][C] of every
+        segment, one launch per BN target"""
+        coefs = []
         for i, ((y, st), bnm) in enumerate(zip(targets, bnmods)):
-            ss = st.seg(s)
-            coef = torch.empty(3, C, dtype=torch.float32, device=y.device)
-            call("artsbir_bn_bwd_finalize", ptr(slots[i]), C, count, ptr(bnm.weight.detach()),
-                 ptr(ss.istd), ptr(grads[bnm.weight]), ptr(grads[bnm.bias]), ptr(coef), _s())
-            desc._keep.append(coef)
-            desc.coef[i] = ptr(coef)
-            desc.dy[i] = _at(dys[i], s * desc.B)
+            C = y.shape[-1]
+            coef = torch.empty(self._G, 3, C, dtype=torch.float32, device=y.device)
+            call("artsbir_bn_bwd_finalize_seg", ptr(slots[i]), self._G, 2 * NSLOT * C, C, count,
+                 ptr(bnm.weight.detach()), ptr(st.buf[0, 1]), 4 * C, ptr(grads[bnm.weight]), ptr(grads[bnm.bias]),
+                 ptr(coef), _s())
+            coefs.append(coef)
+        return coefs
 
     def _bnb_fused_desc(self, kind, targets, ws, mask=None, mask_bn=None):
         """descriptor of a BN-backward reduction fused into the data-gradient GEMM
@@ -526,8 +526,8 @@ class Engine:
         B, H, W, C = y0.shape
         G = self._G
         Bs = B // G
-        per = 2 * NSLOT * C
         dys = [torch.empty_like(y) for y, _ in targets]
+        coefs = self._bn_coefs(targets, bnmods, slots, grads, float(Bs * H * W))
         for s in range(G):
             desc = _hip.BnBwdDesc()
             desc.dtype = self.dt
@@ -540,8 +540,9 @@ class Engine:
                 desc.y[i] = _at(y, s * Bs)
                 desc.mean[i] = ptr(ss.mean)
                 desc.istd[i] = ptr(ss.istd)
+                desc.coef[i] = ptr(coefs[i][s])
+                desc.dy[i] = _at(dys[i], s * Bs)
             desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
-            self._bn_apply(desc, targets, bnmods, [sl[s * per:] for sl in slots], grads, dys, s)
             call("artsbir_bn_bwd_apply", desc, _s())
         return dys
 

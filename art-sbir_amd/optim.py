@@ -50,6 +50,21 @@ class Adam(torch.optim.Optimizer):
         return entry
 
     @torch.no_grad()
+    def zero_grad(self, set_to_none: bool = True):
+        """torch semantics; with set_to_none=False and every gradient a view of
+        one flat buffer (the engine's GradBuffer) that holds nothing else, the
+        buffer is cleared by ONE fill instead of one launch per parameter"""
+        grads = [p.grad for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if set_to_none or not grads:
+            return super().zero_grad(set_to_none=set_to_none)
+        base = grads[0]._base
+        if (base is not None and base.is_contiguous() and all(g._base is base for g in grads)
+                and sum(g.numel() for g in grads) == base.numel()):
+            base.zero_()
+            return None
+        return super().zero_grad(set_to_none=False)
+
+    @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:

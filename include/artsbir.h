@@ -114,6 +114,13 @@ int artsbir_bn_finalize(const float* stats, int C, double count, const float* ga
                         float* running_mean, float* running_var, long long* num_batches_tracked,
                         float momentum, float eps, int train, float* mean, float* istd, float* scale,
                         float* shift, void* stream);
+/* artsbir_bn_finalize for the nseg BN segments of one layer in one launch
+ * (segment s: stats + s*seg_stride; running statistics updated once per segment,
+ * in order; num_batches_tracked += nseg); out[s][4][C] = mean, istd, scale, shift. */
+int artsbir_bn_finalize_seg(const float* stats, int nseg, long long seg_stride, int C, double count,
+                            const float* gamma, const float* beta, float* running_mean, float* running_var,
+                            long long* num_batches_tracked, float momentum, float eps, int train, float* out,
+                            void* stream);
 /* out = avgpool_pool( relu?(x*scale+shift) ) (scale == NULL: no affine). */
 int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* shift, int relu, int pool,
                      int B, int H, int W, int C, void* out, void* stream);
@@ -153,6 +160,11 @@ int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
 /* dgamma += sum g*xhat, dbeta += sum g; coef = [gamma*istd, sum g/cnt, sum g*xhat/cnt]. */
 int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,
                             float* dgamma, float* dbeta, float* coef, void* stream);
+/* the same for nseg segments in one launch: slots + s*seg_stride, istd + s*istd_stride,
+ * dgamma/dbeta accumulate the segments in order, coef[s][3][C]. */
+int artsbir_bn_bwd_finalize_seg(const float* slots, int nseg, long long seg_stride, int C, double count,
+                                const float* gamma, const float* istd, long long istd_stride, float* dgamma,
+                                float* dbeta, float* coef, void* stream);
 int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream);
 /* out[c] += sum_r x[r*ld + c]  (bias / positional-embedding gradients). */
 int artsbir_colsum(int dtype, const void* x, long long rows, long long ld, long long C, float* out, void* stream);
