@@ -101,8 +101,10 @@ def test_triplet_step_f32(cfg, dev):
             outliers.append((k, e_mine, e_ref))
             assert e_mine <= 2e-2, (k, e_mine, e_ref)
     assert len(outliers) <= 6, outliers
-    flat_ref = torch.cat([g.flatten() for g in g64.values()])
-    flat = torch.cat([grads[k].double().flatten() for k in g64])
+    # the rest of the gradient vector (the flip outliers are bounded above)
+    flipped = {k for k, _, _ in outliers}
+    flat_ref = torch.cat([g.flatten() for k, g in g64.items() if k not in flipped])
+    flat = torch.cat([grads[k].double().flatten() for k in g64 if k not in flipped])
     assert ((flat - flat_ref).norm() / flat_ref.norm()).item() < 1e-3
     # parameters after one Adam step: the HIP Adam vs the float64 restatement of
     # torch.optim.Adam applied to the same gradients (first-step Adam is ~lr*sign(g),
