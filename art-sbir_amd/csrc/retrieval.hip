@@ -138,6 +138,7 @@ struct KnnScanArgs {
   const void* g;  // [Ng][D] compute dtype
   const float* qsq;
   const float* gsq;
+  float gsq_max;  // knn_scan_v2: max |g|^2 (prefilter slack)
   int Nq, Ng, D;
   int tiles_per_chunk;
   int nchunks;
@@ -345,6 +346,309 @@ __global__ void __launch_bounds__(256) knn_scan_kernel(KnnScanArgs a) {
       }
     }
   }
+}
+
+// ------------------------------------- register-resident scan (bf16, v2)
+// One workgroup = 8 waves = 256 queries x one gallery chunk.  Each wave holds
+// the MFMA A fragments of its 32 queries over the whole of D in registers
+// (KB = Dp/16 uint4 per lane) and streams the chunk in 32-row gallery tiles
+// that all 8 waves read from LDS: one v_mfma_f32_32x32x16_bf16 per k-block
+// needs one ds_read_b128 (its B fragment) and no A traffic, and no tile is
+// re-fetched per query tile of the workgroup.
+//
+// Gallery rows are stored AUGMENTED: [Ng][Dp + 8] bf16 whose columns Dp..Dp+1
+// carry the f32 |g|^2 (artsbir_rows_prep_aug).  A 32-row tile is then one
+// contiguous block of 32 * (2 Dp + 16) bytes, copied by LDS-DMA into a 3-stage
+// ring, and the odd row pitch in 16-B slots (2 KB + 1) makes the B-fragment
+// reads conflict-free (lanes r = 0..31 of a group hit slots r + const mod 16)
+// with no swizzle.
+//
+// Epilogue per tile, in registers (32x32 accumulator: column = lane & 31 =
+// gallery row, rows (e & 3) + 8 (e >> 2) + 4 (lane >> 5) = queries):
+//   d2 = |q|^2 + |g|^2 - 2 q.g; any lane with d2 <= crit[row] (crit =
+//   max(16th smallest of the chunk so far, rank band hi)) sends the wave into a
+//   slow path that stages the tile's values in LDS, builds per-row hit masks by
+//   ballot, counts "certainly closer" items by popcount and queues uncertain
+//   ones; owner lanes (lane r < 32 owns row r) then insert their hits into a
+//   sorted 16-entry register list.  Same candidate lists, counts and queue as
+//   knn_scan_kernel (same d2 formula, same (value, index) order).
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((address_space(3))) void* r_lds_t;
+
+// LDS-DMA of 16 B per lane to lds + 16 * lane (inline asm on purpose: the
+// compiler does not track it, so it neither drains it before every ds_read nor
+// at barriers; completion is counted by hand with rvm_wait).  M0 is written and
+// restored inside the statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void rdma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(r_lds_t)lds);
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(base), "s"(r)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void rvm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void rvm_wait_n(int n) {
+  switch (n) {
+    case 1: rvm_wait<1>(); break;
+    case 2: rvm_wait<2>(); break;
+    case 3: rvm_wait<3>(); break;
+    case 4: rvm_wait<4>(); break;
+    case 5: rvm_wait<5>(); break;
+    default: rvm_wait<0>(); break;
+  }
+}
+
+constexpr int V2_ROWS = 32;  // gallery rows per tile
+constexpr int V2_WAVES = 8;  // 8 x 32 = 256 queries per workgroup
+
+template <int KB>
+struct V2 {
+  static constexpr int RB = 32 * KB + 16;               // augmented row bytes (Dp bf16 + 16)
+  static constexpr int SLOTS = V2_ROWS * RB / 16;       // 16-B slots per tile
+  static constexpr int NI = (SLOTS + 63) / 64;          // DMA instructions per tile
+  static constexpr int STAGE = NI * 1024;
+  static constexpr int NST = 3;
+  static constexpr int SP = 33;                          // staging pitch (floats)
+  static constexpr int STG = V2_WAVES * 32 * SP * 4;
+  static constexpr int ROWS = V2_WAVES * 32;
+  static constexpr int LDS = NST * STAGE + STG + 5 * ROWS * 4;
+  static_assert((NI + V2_WAVES - 1) / V2_WAVES <= 5, "rvm_wait_n covers at most 5 DMA per wave");
+};
+
+template <int KB>
+__global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
+  using C = V2<KB>;
+  __shared__ __attribute__((aligned(16))) char smem[C::LDS];
+  float* s_stage = reinterpret_cast<float*>(smem + C::NST * C::STAGE);
+  float* s_thr = s_stage + V2_WAVES * 32 * C::SP;  // [256] 16th smallest so far (-INF: row unused)
+  float* s_crit = s_thr + C::ROWS;                 // [256] max(thr, band hi)
+  float* s_lo = s_crit + C::ROWS;                  // [256] rank band (hi < 0: no band)
+  float* s_hi = s_lo + C::ROWS;
+  float* s_qsq = s_hi + C::ROWS;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntq = (a.Nq + C::ROWS - 1) / C::ROWS;
+  int lid = (int)blockIdx.x;
+  {  // the query tiles of one gallery chunk on one XCD at the same time (shared L2)
+    const int nwg = (int)gridDim.x;
+    if (nwg >= 8) {
+      const int q8 = nwg / 8, r8 = nwg % 8, x = lid % 8;
+      lid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + lid / 8;
+    }
+  }
+  const int chunk = lid / ntq, qt = lid % ntq;
+  const int qb = qt * C::ROWS;
+  const int rows_per_chunk = a.tiles_per_chunk * 128;
+  const int g0 = chunk * rows_per_chunk;
+  const int nrows = min(a.Ng - g0, rows_per_chunk);
+  if (nrows <= 0) return;
+  const int ntiles = (nrows + V2_ROWS - 1) / V2_ROWS;
+
+  const __amdgpu_buffer_rsrc_t gr =
+      rrsrc(reinterpret_cast<const char*>(a.g) + (long long)g0 * C::RB, (long long)(a.Ng - g0) * C::RB);
+  const int my_ni = wid < C::NI ? (C::NI - wid + V2_WAVES - 1) / V2_WAVES : 0;
+  auto issue_tile = [&](int t) {
+    char* st = smem + (t % C::NST) * C::STAGE;
+    const unsigned gb = (unsigned)(t * V2_ROWS * C::RB);
+    for (int i = wid; i < C::NI; i += V2_WAVES) rdma16(gr, st + i * 1024, gb + (unsigned)((i * 64 + lane) * 16));
+  };
+  issue_tile(0);
+  if (ntiles > 1) issue_tile(1);
+
+  const float* band_lo = a.lo;
+  const float* band_hi = a.hi;
+  if (tid < C::ROWS) {
+    const int q = qb + tid;
+    const bool ok = q < a.Nq;
+    s_thr[tid] = ok ? INFINITY : -INFINITY;
+    s_crit[tid] = ok ? INFINITY : -INFINITY;
+    s_lo[tid] = (band_lo && ok) ? band_lo[q] : -1.f;
+    s_hi[tid] = (band_lo && ok) ? band_hi[q] : -1.f;
+    s_qsq[tid] = ok ? a.qsq[q] : 0.f;
+  }
+  const int r32 = lane & 31, h = lane >> 5;
+  const __amdgpu_buffer_rsrc_t qr = rrsrc(reinterpret_cast<const bf16*>(a.q) + (long long)qb * (16 * KB),
+                                          (long long)(a.Nq - qb) * (32 * KB));
+  uint4 af[KB];
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb)
+    af[kb] = rload(qr, (unsigned)(((wid * 32 + r32) * 16 * KB + kb * 16 + 8 * h) * 2));
+  // owner state: lane r < 32 owns row r of the wave (its e and half in the accumulator)
+  const int orow = lane & 31;
+  const int oe = (orow & 3) + 4 * (orow >> 3), oh = (orow >> 2) & 1;
+  const int R_own = wid * 32 + orow;
+  float lst_d[KT];
+  int lst_i[KT];
+#pragma unroll
+  for (int i = 0; i < KT; ++i) { lst_d[i] = INFINITY; lst_i[i] = -1; }
+  int mycnt = 0;
+  rvm_wait<0>();
+  __syncthreads();
+  // prefilter: t = |g|^2 - 2 q.g <= crit - |q|^2 + slack, a superset of
+  // d2 = (|q|^2 + |g|^2) - 2 q.g <= crit whatever the rounding of either form
+  // (every magnitude is <= 2 (|q|^2 + gsq_max), each rounding <= 2^-24 of it)
+  const float gmax = a.gsq_max;
+  float critp[16];
+  auto load_crit = [&]() {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int R = wid * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const float qs = s_qsq[R];
+      critp[e] = (s_crit[R] - qs) + 0x1p-18f * (qs + gmax);
+    }
+  };
+  load_crit();
+  float* stg = s_stage + wid * 32 * C::SP;
+
+  for (int t = 0; t < ntiles; ++t) {
+    if (t + 2 < ntiles) issue_tile(t + 2);
+    const char* st = smem + (t % C::NST) * C::STAGE;
+    const char* bp = st + r32 * C::RB + h * 16;
+    // B fragments two groups of 4 deep (the scheduler would otherwise hoist
+    // all KB reads ahead of the MFMAs and run out of registers)
+    f32x16 acc = {};
+    uint4 bq[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bq[0][j] = *reinterpret_cast<const uint4*>(bp + j * 32);
+#pragma unroll
+    for (int g = 0; g < KB / 4; ++g) {
+      if (g + 1 < KB / 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bq[(g + 1) & 1][j] = *reinterpret_cast<const uint4*>(bp + ((g + 1) * 4 + j) * 32);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[g * 4 + j]),
+                                                      *reinterpret_cast<const bf16x8*>(&bq[g & 1][j]), acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int bn = g0 + t * V2_ROWS;
+    const bool cvalid = bn + r32 < a.Ng;
+    const float gsq = cvalid ? *reinterpret_cast<const float*>(st + r32 * C::RB + 32 * KB) : INFINITY;
+    bool any = false;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[e], gsq) <= critp[e];
+    bool atom = false;
+    if (__builtin_amdgcn_ballot_w64(any)) {
+      // stage the raw dot products of every row with a prefilter hit; the owner
+      // of each row re-evaluates its hits exactly (d2 with the same formula as
+      // knn_scan_kernel): list insertion, certainly-closer count, uncertain queue
+      unsigned mymask = 0;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(fmaf(-2.f, acc[e], gsq) <= critp[e]);
+        if (m) {
+          stg[((e & 3) + 8 * (e >> 2) + 4 * h) * C::SP + r32] = acc[e];
+          if (oe == e) mymask = oh ? (unsigned)(m >> 32) : (unsigned)m;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      bool changed = false;
+      if (lane < 32 && mymask) {
+        const float qs = s_qsq[R_own], lo = s_lo[R_own], hi = s_hi[R_own];
+        const float* srow = stg + orow * C::SP;
+        float thr = s_thr[R_own];
+        while (mymask) {
+          const int c = __builtin_ctz(mymask);
+          mymask &= mymask - 1;
+          const bool valid = bn + c < a.Ng;
+          const float g2 = valid ? *reinterpret_cast<const float*>(st + c * C::RB + 32 * KB) : INFINITY;
+          const float d2 = fmaf(-2.f, srow[c], qs + g2);
+          if (d2 < thr) {
+            float x = d2;
+            int xi = bn + c;
+#pragma unroll
+            for (int i = 0; i < KT; ++i) {  // compare-swap down the sorted list
+              const bool sw = x < lst_d[i] || (x == lst_d[i] && xi < lst_i[i] && lst_i[i] >= 0);
+              const float td = lst_d[i];
+              const int ti = lst_i[i];
+              lst_d[i] = sw ? x : td;
+              lst_i[i] = sw ? xi : ti;
+              x = sw ? td : x;
+              xi = sw ? ti : xi;
+            }
+            thr = lst_d[KT - 1];
+            changed = true;
+          }
+          if (hi >= 0.f && valid) {
+            if (d2 < lo) {
+              ++mycnt;
+            } else if (d2 <= hi) {
+              const int k = atomicAdd(a.unc + 2 * a.unc_cap, 1);
+              if (k < a.unc_cap) { a.unc[2 * k] = qb + R_own; a.unc[2 * k + 1] = bn + c; }
+              atom = true;
+            }
+          }
+        }
+        if (changed) {
+          s_thr[R_own] = thr;
+          s_crit[R_own] = fmaxf(thr, hi);
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(changed)) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        load_crit();
+      }
+    }
+    if (t + 1 < ntiles) {
+      // stage t+1 landed (this wave's DMAs; the barrier publishes everyone's)
+      if (t + 2 < ntiles && !__builtin_amdgcn_ballot_w64(atom))
+        rvm_wait_n(my_ni);
+      else
+        rvm_wait<0>();
+    }
+    __syncthreads();
+  }
+  if (lane < 32) {
+    const int q = qb + R_own;
+    if (q < a.Nq) {
+      if (mycnt) atomicAdd(a.cnt + q, mycnt);
+      const long long o = ((long long)q * a.nchunks + chunk) * KT;
+#pragma unroll
+      for (int i = 0; i < KT; ++i) {
+        a.cand_d[o + i] = lst_d[i];
+        a.cand_i[o + i] = lst_i[i];
+      }
+    }
+  }
+}
+
+// augmented bf16 rows for knn_scan_v2: [n][Dp + 8], columns Dp..Dp+1 = f32 |x|^2
+__global__ void rows_prep_aug_kernel(const float* __restrict__ x, int n, int D, int Dp, float* __restrict__ sq,
+                                     bf16* __restrict__ xa) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= n) return;
+  const float* r = x + (long long)row * D;
+  bf16* o = xa + (long long)row * (Dp + 8);
+  float s = 0.f;
+  for (int d = lane; d < Dp; d += 64) {
+    const float v = d < D ? r[d] : 0.f;
+    s += v * v;
+    o[d] = (bf16)v;
+  }
+  s = warp_sum(s);
+  if (lane < 8) {
+    const unsigned bits = __float_as_uint(s);
+    unsigned short v = 0;
+    if (lane == 0) v = (unsigned short)(bits & 0xffffu);
+    if (lane == 1) v = (unsigned short)(bits >> 16);
+    reinterpret_cast<unsigned short*>(o)[Dp + lane] = v;
+  }
+  if (lane == 0) sq[row] = s;
 }
 
 // ------------------------------------------------------------ exact merge
@@ -599,5 +903,43 @@ extern "C" int artsbir_knn_exact_all(const float* q, const float* g, int D, int 
   if (grid > 65536) grid = 65536;
   hipLaunchKernelGGL(knn_exact_all_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, q, g, D, n, out);
   ARTSBIR_CHECK_LAUNCH("knn_exact_all");
+  return 0;
+}
+
+extern "C" int artsbir_rows_prep_aug(const float* x, int n, int D, int Dp, float* sq, void* xa, void* stream) {
+  if (Dp < D || Dp % 16) { set_error("rows_prep_aug: Dp=%d must be >= D=%d and a multiple of 16", Dp, D); return -1; }
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rows_prep_aug_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, n, D, Dp,
+                     sq, (bf16*)xa);
+  ARTSBIR_CHECK_LAUNCH("rows_prep_aug");
+  return 0;
+}
+
+extern "C" int artsbir_knn_scan_aug_supported(int Dp) { return Dp == 64 || Dp == 128 || Dp == 256 || Dp == 512; }
+
+extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float* qsq, float gsq_max, int nq, int ng,
+                                    int Dp, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc,
+                                    int unc_cap, float* cand_d, int* cand_i, void* stream) {
+  if (!artsbir_knn_scan_aug_supported(Dp)) { set_error("knn_scan_aug: Dp=%d not in {64,128,256,512}", Dp); return -1; }
+  if (tiles_per_chunk <= 0 || (long long)tiles_per_chunk * 128 * (2LL * Dp + 16) > 0x7fffffffLL) {
+    set_error("knn_scan_aug: tiles_per_chunk=%d out of range", tiles_per_chunk);
+    return -1;
+  }
+  if (nq <= 0 || ng <= 0) return 0;
+  KnnScanArgs a;
+  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.Nq = nq; a.Ng = ng; a.D = Dp;
+  a.tiles_per_chunk = tiles_per_chunk;
+  const int tiles = (ng + 127) / 128;
+  a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
+  a.lo = lo; a.hi = hi; a.cnt = cnt; a.unc = unc; a.unc_cap = unc_cap; a.cand_d = cand_d; a.cand_i = cand_i;
+  const unsigned grid = (unsigned)(a.nchunks * ((nq + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  switch (Dp) {
+    case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, s, a); break;
+    case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, s, a); break;
+    case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, s, a); break;
+    default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, s, a); break;
+  }
+  ARTSBIR_CHECK_LAUNCH("knn_scan_aug");
   return 0;
 }

@@ -32,7 +32,7 @@ def _s():
 
 def knn(queries: torch.Tensor, gallery: torch.Tensor, k: int = 10, positives: torch.Tensor | None = None,
         compute: str = "bf16", g_base: int = 0, dpos: torch.Tensor | None = None,
-        tiles_per_chunk: int = TILES_PER_CHUNK):
+        tiles_per_chunk: int = TILES_PER_CHUNK, scan: str = "auto"):
     """Exact top-k and rank of the positive.
 
     queries [Q, D], gallery [N, D] (float, CUDA).  positives: int64 [Q] global
@@ -40,7 +40,9 @@ def knn(queries: torch.Tensor, gallery: torch.Tensor, k: int = 10, positives: to
     (idx int64 [Q, k] global indices, dist float64 [Q, k], rank int64 [Q] or None,
     dpos float64 [Q] or None).  With g_base/dpos this is one shard of a larger
     gallery: dpos must then hold the exact positive distance (or -1) for rows
-    whose positive lives in another shard.
+    whose positive lives in another shard.  scan: "auto" (the register-resident
+    bf16 scan knn_scan_v2 on an augmented gallery copy when D pads to 64, 128,
+    256 or 512, else knn_scan_kernel), "v1" (always knn_scan_kernel).
     """
     if not (queries.is_cuda and gallery.is_cuda):
         raise RuntimeError("knn on libartsbir_hip needs CUDA tensors")
@@ -62,10 +64,15 @@ def knn(queries: torch.Tensor, gallery: torch.Tensor, k: int = 10, positives: to
     gsq = torch.empty(N, dtype=torch.float32, device=dev)
     step = 64 if dt == _hip.DT_BF16 else 32
     Dp = (D + step - 1) // step * step  # MFMA scan: zero-padded compute copies
+    use_v2 = (scan == "auto" and dt == _hip.DT_BF16 and bool(_hip.lib().artsbir_knn_scan_aug_supported(Dp)))
     qc = torch.empty(Q, Dp, dtype=tdt, device=dev)
-    gc = torch.empty(N, Dp, dtype=tdt, device=dev)
     call("artsbir_rows_prep", dt, ptr(q), Q, D, ptr(qsq), ptr(qc), Dp, _s())
-    call("artsbir_rows_prep", dt, ptr(g), N, D, ptr(gsq), ptr(gc), Dp, _s())
+    if use_v2:  # [N][Dp + 8] bf16 rows carrying their f32 |g|^2 (one DMA block per tile)
+        gc = torch.empty(N, Dp + 8, dtype=tdt, device=dev)
+        call("artsbir_rows_prep_aug", ptr(g), N, D, Dp, ptr(gsq), ptr(gc), _s())
+    else:
+        gc = torch.empty(N, Dp, dtype=tdt, device=dev)
+        call("artsbir_rows_prep", dt, ptr(g), N, D, ptr(gsq), ptr(gc), Dp, _s())
     gsq_max = float(gsq.max().item()) if N else 0.0
 
     lo = hi = pos = None
@@ -85,9 +92,14 @@ def knn(queries: torch.Tensor, gallery: torch.Tensor, k: int = 10, positives: to
     nchunks = ncand // 16
     cand_d = torch.empty(Q, ncand, dtype=torch.float32, device=dev)
     cand_i = torch.empty(Q, ncand, dtype=torch.int32, device=dev)
-    call("artsbir_knn_scan", dt, ptr(qc), ptr(gc), ptr(qsq), ptr(gsq), Q, N, Dp, tiles_per_chunk, ptr(lo), ptr(hi),
-         ptr(cnt), ptr(unc), UNC_CAP, ptr(cand_d), ptr(cand_i), _s(), kernel="knn_scan_kernel",
-         flops=2.0 * Q * N * D)
+    if use_v2:
+        call("artsbir_knn_scan_aug", ptr(qc), ptr(gc), ptr(qsq), gsq_max, Q, N, Dp, tiles_per_chunk, ptr(lo),
+             ptr(hi), ptr(cnt), ptr(unc), UNC_CAP, ptr(cand_d), ptr(cand_i), _s(), kernel="knn_scan_v2_kernel",
+             flops=2.0 * Q * N * D)
+    else:
+        call("artsbir_knn_scan", dt, ptr(qc), ptr(gc), ptr(qsq), ptr(gsq), Q, N, Dp, tiles_per_chunk, ptr(lo),
+             ptr(hi), ptr(cnt), ptr(unc), UNC_CAP, ptr(cand_d), ptr(cand_i), _s(), kernel="knn_scan_kernel",
+             flops=2.0 * Q * N * D)
     out_i = torch.empty(Q, k, dtype=torch.int64, device=dev)
     out_d = torch.empty(Q, k, dtype=torch.float64, device=dev)
     flag = torch.empty(Q, dtype=torch.int32, device=dev)

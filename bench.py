@@ -135,7 +135,8 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1, *_ in prof if kn == "knn_scan_kernel"]
+    scan_kernel = next((kn for kn, *_ in prof if kn.startswith("knn_scan")), "knn_scan_kernel")
+    scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1, *_ in prof if kn == scan_kernel]
     scan_s = sum(s for _, s in scan) / len(scan)
     scan_fl = sum(f for f, _ in scan) / len(scan)
     rk = r.double() + 1
@@ -144,11 +145,11 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
             "unit": "queries/s", "ms": round(el * 1e3, 3), "N": N, "D": D, "Q": Q, "k": k, "n_gpus": world,
             "scaling": "strong", "compute": "bf16 MFMA scan + exact f64 rerank", "map@10": round(map10, 6),
             "mrr": round(float((1.0 / rk).mean()), 6),
-            "roofline": {"bound": "mfma", "kernel": "knn_scan_kernel", "achieved": round(scan_fl / scan_s / 1e12, 2),
+            "roofline": {"bound": "mfma", "kernel": scan_kernel, "achieved": round(scan_fl / scan_s / 1e12, 2),
                          "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
                          "frac": round(scan_fl / scan_s / 1e12 / MFMA_PEAK_TFLOPS["bf16"], 4),
                          "avg_launch_us": round(scan_s * 1e6, 2), "avg_launch_flops": scan_fl,
-                         "traffic": pmc_traffic("knn_scan_kernel")}}
+                         "traffic": pmc_traffic(scan_kernel)}}
 
 
 def cpu_retrieval_baseline(N=1_000_000, D=512, nq=8):

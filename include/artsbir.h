@@ -227,6 +227,18 @@ int artsbir_knn_candidates_per_query(int ng, int tiles_per_chunk);
 int artsbir_knn_scan(int dtype, const void* qc, const void* gc, const float* qsq, const float* gsq, int nq,
                      int ng, int D, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc,
                      int unc_cap, float* cand_d, int* cand_i, void* stream);
+/* augmented bf16 gallery rows for artsbir_knn_scan_aug: xa is [n][Dp + 8] bf16, row i
+ * = x[i] zero-padded to Dp columns, then the f32 bits of ||x[i]||^2 in columns
+ * Dp..Dp+1 and zeros; sq[i] = ||x[i]||^2. */
+int artsbir_rows_prep_aug(const float* x, int n, int D, int Dp, float* sq, void* xa, void* stream);
+/* 1 if artsbir_knn_scan_aug has a kernel for this padded width (64, 128, 256, 512). */
+int artsbir_knn_scan_aug_supported(int Dp);
+/* the same candidate lists / counts / uncertain queue as artsbir_knn_scan (bf16), from
+ * qc [nq][Dp] bf16 and the augmented gallery ga [ng][Dp + 8]: register-resident query
+ * fragments, 32-row gallery tiles by LDS-DMA, 32x32x16 MFMA (inference.py:30-69). */
+int artsbir_knn_scan_aug(const void* qc, const void* ga, const float* qsq, float gsq_max, int nq, int ng,
+                         int Dp, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc, int unc_cap,
+                         float* cand_d, int* cand_i, void* stream);
 /* exact f64 top-k by (distance, index) from the candidates; flag[q] = 1 when a
  * chunk list could have dropped a true top-k item (caller re-runs exhaustively). */
 int artsbir_knn_merge(const float* q, const float* g, int D, int nq, int nchunks, const float* cand_d,

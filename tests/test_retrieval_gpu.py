@@ -19,13 +19,14 @@ def _oracle(g, qs, pos, k):
     return np.array(idx), np.array(dist), np.array(ranks)
 
 
-@pytest.mark.parametrize("compute", ["bf16", "f32"])
+@pytest.mark.parametrize("compute,scan", [("bf16", "auto"), ("bf16", "v1"), ("f32", "auto")])
 @pytest.mark.parametrize("N,D,Q,k", [(5000, 64, 300, 10), (20000, 512, 200, 10), (300, 128, 50, 10)])
-def test_knn_matches_oracle(compute, N, D, Q, k, dev):
+def test_knn_matches_oracle(compute, scan, N, D, Q, k, dev):
+    """scan "auto" = the register-resident knn_scan_v2 (bf16, D padded to 64/128/256/512), "v1" = knn_scan_kernel."""
     import knn
     g, qs, pos = oret.synthetic_gallery(N, D, Q)
     idx, dist, rank, _ = knn.knn(torch.from_numpy(qs).to(dev), torch.from_numpy(g).to(dev), k,
-                                 torch.from_numpy(pos).to(dev), compute=compute)
+                                 torch.from_numpy(pos).to(dev), compute=compute, scan=scan)
     ri, rd, rr = _oracle(g, qs, pos, k)
     np.testing.assert_array_equal(idx.cpu().numpy(), ri)
     np.testing.assert_allclose(dist.cpu().numpy(), rd, rtol=1e-12)
@@ -72,3 +73,74 @@ def test_pairwise_l2_matches_torch(dev):
     c = torch.randn(777, 256)
     assert torch.allclose(utils.euclidean_distance(b.to(dev), c.to(dev)).cpu(),
                           torch.nn.PairwiseDistance(p=2)(b, c), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("scan", ["auto", "v1"])
+@pytest.mark.parametrize("N,D,Q,tpc", [(5000, 100, 300, 1), (9000, 256, 520, 2), (20, 64, 3, 64), (1000, 512, 257, 1)])
+def test_knn_chunks_ragged(scan, N, D, Q, tpc, dev):
+    """many gallery chunks (small tiles_per_chunk), ragged D (zero-padded), partial query tiles
+    (Q not a multiple of 256 / 128) and a gallery smaller than one 32-row tile."""
+    import knn
+    g, qs, pos = oret.synthetic_gallery(N, D, Q, noise=1.5)
+    pos = pos.copy()
+    pos[::5] = -1
+    idx, dist, rank, _ = knn.knn(torch.from_numpy(qs).to(dev), torch.from_numpy(g).to(dev), min(10, N),
+                                 torch.from_numpy(pos).to(dev), scan=scan, tiles_per_chunk=tpc)
+    ri, rd, rr = _oracle(g, qs, pos, min(10, N))
+    np.testing.assert_array_equal(idx.cpu().numpy(), ri)
+    np.testing.assert_allclose(dist.cpu().numpy(), rd, rtol=1e-12)
+    r = rank.cpu().numpy()
+    np.testing.assert_array_equal(r[pos >= 0], rr[pos >= 0])
+
+
+def test_knn_scan_v2_candidates_equal_v1(dev):
+    """the two scans produce the same per-(query, chunk) candidate lists and counts (same
+    d2 formula and (value, index) order) — compared through the C-ABI directly."""
+    import _hip
+    from _hip import call, ptr
+    N, D, Q, tpc = 6000, 512, 300, 4
+    g, qs, pos = oret.synthetic_gallery(N, D, Q, noise=2.0)
+    q = torch.from_numpy(qs).to(dev)
+    gg = torch.from_numpy(g).to(dev)
+    qsq = torch.empty(Q, device=dev)
+    gsq = torch.empty(N, device=dev)
+    qc = torch.empty(Q, D, dtype=torch.bfloat16, device=dev)
+    gc = torch.empty(N, D, dtype=torch.bfloat16, device=dev)
+    ga = torch.empty(N, D + 8, dtype=torch.bfloat16, device=dev)
+    call("artsbir_rows_prep", _hip.DT_BF16, ptr(q), Q, D, ptr(qsq), ptr(qc), D, _hip.stream())
+    call("artsbir_rows_prep", _hip.DT_BF16, ptr(gg), N, D, ptr(gsq), ptr(gc), D, _hip.stream())
+    gsq2 = torch.empty(N, device=dev)
+    call("artsbir_rows_prep_aug", ptr(gg), N, D, D, ptr(gsq2), ptr(ga), _hip.stream())
+    assert torch.equal(gsq, gsq2)
+    assert torch.equal(ga[:, :D], gc)
+    assert torch.equal(ga[:, D:D + 2].contiguous().view(torch.float32).flatten(), gsq)
+    ncand = _hip.lib().artsbir_knn_candidates_per_query(N, tpc)
+    # rank band around the 30th-nearest item's approximate distance: exercises counts and the queue
+    d2 = (qsq[:, None] + gsq[None, :] - 2.0 * (qc.float() @ gc.float().T))
+    lo = d2.kthvalue(30, dim=1).values - 5.0
+    hi = lo + 10.0
+    out = []
+    for v2 in (False, True):
+        cnt = torch.zeros(Q, dtype=torch.int32, device=dev)
+        unc = torch.zeros(2 * 4096 + 1, dtype=torch.int32, device=dev)
+        cd = torch.empty(Q, ncand, device=dev)
+        ci = torch.empty(Q, ncand, dtype=torch.int32, device=dev)
+        if v2:
+            call("artsbir_knn_scan_aug", ptr(qc), ptr(ga), ptr(qsq), float(gsq.max()), Q, N, D, tpc, ptr(lo), ptr(hi),
+                 ptr(cnt), ptr(unc), 4096, ptr(cd), ptr(ci), _hip.stream())
+        else:
+            call("artsbir_knn_scan", _hip.DT_BF16, ptr(qc), ptr(gc), ptr(qsq), ptr(gsq), Q, N, D, tpc, ptr(lo),
+                 ptr(hi), ptr(cnt), ptr(unc), 4096, ptr(cd), ptr(ci), _hip.stream())
+        n = int(unc[-1])
+        pairs = sorted(map(tuple, unc[:2 * min(n, 4096)].view(-1, 2).cpu().tolist()))
+        out.append((cd.cpu(), ci.cpu(), cnt.cpu(), n, pairs))
+    (cd1, ci1, c1, n1, p1), (cd2, ci2, c2, n2, p2) = out
+    # the two MFMA shapes sum the dot products in different orders (f32 rounding), so a
+    # near-tie may land on the other side of a list end or band edge; otherwise equal
+    same_lists = (ci1.view(Q, -1, 16) == ci2.view(Q, -1, 16)).all(dim=2).float().mean().item()
+    assert same_lists >= 0.99, same_lists
+    assert (c1 == c2).float().mean().item() >= 0.99
+    assert n1 > 0 and abs(n1 - n2) <= max(2, n1 // 100)
+    assert len(set(p1) ^ set(p2)) <= max(2, n1 // 50)
+    m = ci1 == ci2
+    np.testing.assert_allclose(cd1[m].numpy(), cd2[m].numpy(), rtol=1e-5, atol=1e-3)
