@@ -95,8 +95,8 @@ SIGNATURES = {
                          _vp, _vp, _vp],
     "artsbir_rows_prep_aug": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_knn_scan_aug_supported": [_c_int],
-    "artsbir_knn_scan_aug": [_vp, _vp, _vp, _c_float, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int,
-                             _vp, _vp, _vp],
+    "artsbir_knn_scan_aug": [_vp, _vp, _vp, _c_float, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int, _c_float,
+                             _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp],
     "artsbir_knn_merge": [_vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_float, _c_float, _c_ll, _c_int, _vp,
                           _vp, _vp, _vp],
     "artsbir_knn_uncertain": [_vp, _vp, _c_int, _vp, _c_int, _vp, _vp, _c_ll, _vp, _vp],

@@ -139,6 +139,10 @@ struct KnnScanArgs {
   const float* qsq;
   const float* gsq;
   float gsq_max;  // knn_scan_v2: max |g|^2 (prefilter slack)
+  const float* thr0;  // knn_scan_v2: optional per-query initial list threshold (see knn.py)
+  unsigned* kb;       // knn_scan_v2: optional [Nq] shared k-th bound (kb_enc of an approx d2), atomicMin
+  int kq;             //   k of the final top-k (1..KT)
+  float rel;          //   error bound factor of the approximate d2 (eps = rel |q| max|g| + 1e-3)
   int Nq, Ng, D;
   int tiles_per_chunk;
   int nchunks;
@@ -408,6 +412,22 @@ __device__ __forceinline__ void rvm_wait_n(int n) {
   }
 }
 
+// order-preserving unsigned encoding of a float (atomicMin on the shared bound)
+__device__ __forceinline__ unsigned kb_enc(float f) {
+  const unsigned b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float kb_dec(unsigned u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+// a list threshold every chunk may use: some chunk's k-th smallest approximate d2
+// U >= the gallery's k-th smallest a_k, so U + 2 eps (+ rounding margin) >= the
+// exact merge's cut a_k + 2 eps: no item at or above it can reach the top k
+__device__ __forceinline__ float kb_bound(unsigned u, float eps) {
+  const float v = kb_dec(u);
+  return (v + 2.f * eps) * (1.f + 0x1p-18f) + 1e-3f;
+}
+
 constexpr int V2_ROWS = 32;  // gallery rows per tile
 constexpr int V2_WAVES = 8;  // 8 x 32 = 256 queries per workgroup
 
@@ -471,11 +491,13 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
   if (tid < C::ROWS) {
     const int q = qb + tid;
     const bool ok = q < a.Nq;
-    s_thr[tid] = ok ? INFINITY : -INFINITY;
-    s_crit[tid] = ok ? INFINITY : -INFINITY;
+    float t0 = (ok && a.thr0) ? a.thr0[q] : INFINITY;
+    if (ok && a.kb) t0 = fminf(t0, kb_bound(a.kb[q], a.rel * sqrtf(a.qsq[q] * a.gsq_max) * 1.001f + 1e-3f));
+    s_thr[tid] = ok ? t0 : -INFINITY;
     s_lo[tid] = (band_lo && ok) ? band_lo[q] : -1.f;
     s_hi[tid] = (band_lo && ok) ? band_hi[q] : -1.f;
     s_qsq[tid] = ok ? a.qsq[q] : 0.f;
+    s_crit[tid] = ok ? fmaxf(t0, s_hi[tid]) : -INFINITY;
   }
   const int r32 = lane & 31, h = lane >> 5;
   const __amdgpu_buffer_rsrc_t qr = rrsrc(reinterpret_cast<const bf16*>(a.q) + (long long)qb * (16 * KB),
@@ -494,6 +516,11 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
   for (int i = 0; i < KT; ++i) { lst_d[i] = INFINITY; lst_i[i] = -1; }
   int mycnt = 0;
   rvm_wait<0>();
+  // the A fragments are resident from here on: launder them through an empty asm
+  // so that the compiler's vmcnt tracking does not wait on (our hand-counted
+  // DMAs behind) their loads inside the tile loop
+#pragma unroll
+  for (int kb = 0; kb < KB; ++kb) asm volatile("" : "+v"(af[kb].x), "+v"(af[kb].y), "+v"(af[kb].z), "+v"(af[kb].w));
   __syncthreads();
   // prefilter: t = |g|^2 - 2 q.g <= crit - |q|^2 + slack, a superset of
   // d2 = (|q|^2 + |g|^2) - 2 q.g <= crit whatever the rounding of either form
@@ -510,27 +537,27 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
   };
   load_crit();
   float* stg = s_stage + wid * 32 * C::SP;
+  const int q_own = qb + R_own;
+  const float eps_own = q_own < a.Nq ? a.rel * sqrtf(a.qsq[q_own] * gmax) * 1.001f + 1e-3f : 0.f;
+  float thr_g = s_thr[R_own];  // best shared bound seen (with thr0)
 
   for (int t = 0; t < ntiles; ++t) {
     if (t + 2 < ntiles) issue_tile(t + 2);
     const char* st = smem + (t % C::NST) * C::STAGE;
     const char* bp = st + r32 * C::RB + h * 16;
-    // B fragments two groups of 4 deep (the scheduler would otherwise hoist
-    // all KB reads ahead of the MFMAs and run out of registers)
+    // B fragments PF reads ahead of their MFMA, pinned in that order (left
+    // alone, the scheduler either hoists all KB reads and runs out of registers
+    // or issues each read just one MFMA before its use and exposes the LDS latency)
+    constexpr int PF = KB < 6 ? KB : 6;
     f32x16 acc = {};
-    uint4 bq[2][4];
+    uint4 bq[KB];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bq[0][j] = *reinterpret_cast<const uint4*>(bp + j * 32);
+    for (int j = 0; j < PF; ++j) bq[j] = *reinterpret_cast<const uint4*>(bp + j * 32);
 #pragma unroll
-    for (int g = 0; g < KB / 4; ++g) {
-      if (g + 1 < KB / 4) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bq[(g + 1) & 1][j] = *reinterpret_cast<const uint4*>(bp + ((g + 1) * 4 + j) * 32);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[g * 4 + j]),
-                                                      *reinterpret_cast<const bf16x8*>(&bq[g & 1][j]), acc, 0, 0, 0);
+    for (int kb = 0; kb < KB; ++kb) {
+      if (kb + PF < KB) bq[kb + PF] = *reinterpret_cast<const uint4*>(bp + (kb + PF) * 32);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[kb]),
+                                                    *reinterpret_cast<const bf16x8*>(&bq[kb]), acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     const int bn = g0 + t * V2_ROWS;
@@ -571,7 +598,8 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
             int xi = bn + c;
 #pragma unroll
             for (int i = 0; i < KT; ++i) {  // compare-swap down the sorted list
-              const bool sw = x < lst_d[i] || (x == lst_d[i] && xi < lst_i[i] && lst_i[i] >= 0);
+              // branch-free (the short-circuit form compiles to an exec-mask branch per step)
+              const bool sw = (int)(x < lst_d[i]) | ((int)(x == lst_d[i]) & (int)(xi < lst_i[i]) & (int)(lst_i[i] >= 0));
               const float td = lst_d[i];
               const int ti = lst_i[i];
               lst_d[i] = sw ? x : td;
@@ -579,7 +607,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
               x = sw ? td : x;
               xi = sw ? ti : xi;
             }
-            thr = lst_d[KT - 1];
+            thr = fminf(lst_d[KT - 1], thr_g);
             changed = true;
           }
           if (hi >= 0.f && valid) {
@@ -595,9 +623,45 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
         if (changed) {
           s_thr[R_own] = thr;
           s_crit[R_own] = fmaxf(thr, hi);
+          if (a.kb) {  // publish this chunk's k-th smallest
+            float kth = INFINITY;
+#pragma unroll
+            for (int i = 0; i < KT; ++i) kth = (i == a.kq - 1 && lst_i[i] >= 0) ? lst_d[i] : kth;
+            if (kth < INFINITY) {
+              const float g = kb_bound(kb_enc(kth), eps_own);
+              if (g < thr_g) {
+                thr_g = g;
+                atomicMin(a.kb + q_own, kb_enc(kth));
+                atom = true;
+              }
+            }
+          }
         }
       }
       if (__builtin_amdgcn_ballot_w64(changed)) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        load_crit();
+      }
+    }
+    if (a.kb && (t & 7) == 7 && t + 1 < ntiles) {
+      // every 8 tiles: tighten the thresholds with the bounds other chunks published
+      bool upd = false;
+      if (lane < 32 && q_own < a.Nq) {
+        const unsigned u = __hip_atomic_load(a.kb + q_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float g = kb_bound(u, eps_own);
+        if (g < thr_g) {
+          thr_g = g;
+          const float cur = s_thr[R_own];
+          if (g < cur) {
+            s_thr[R_own] = g;
+            s_crit[R_own] = fmaxf(g, s_hi[R_own]);
+            upd = true;
+          }
+        }
+      }
+      atom = true;  // the compiler waited for this load with vmcnt(0) anyway
+      if (__builtin_amdgcn_ballot_w64(upd)) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         load_crit();
@@ -862,7 +926,7 @@ extern "C" int artsbir_knn_scan(int dtype, const void* qc, const void* gc, const
   if (D % (8 * EPC)) { set_error("knn_scan: D=%d must be a multiple of %d", D, 8 * EPC); return -1; }
   if (nq <= 0 || ng <= 0) return 0;
   KnnScanArgs a;
-  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.Nq = nq; a.Ng = ng; a.D = D;
+  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.thr0 = nullptr; a.kb = nullptr; a.kq = 0; a.rel = 0.f; a.Nq = nq; a.Ng = ng; a.D = D;
   a.tiles_per_chunk = tiles_per_chunk;
   const int tiles = (ng + 127) / 128;
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
@@ -918,16 +982,18 @@ extern "C" int artsbir_rows_prep_aug(const float* x, int n, int D, int Dp, float
 extern "C" int artsbir_knn_scan_aug_supported(int Dp) { return Dp == 64 || Dp == 128 || Dp == 256 || Dp == 512; }
 
 extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float* qsq, float gsq_max, int nq, int ng,
-                                    int Dp, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc,
-                                    int unc_cap, float* cand_d, int* cand_i, void* stream) {
+                                    int Dp, int tiles_per_chunk, const float* thr0, unsigned* kbound, int k, float rel,
+                                    const float* lo, const float* hi, int* cnt, int* unc, int unc_cap, float* cand_d,
+                                    int* cand_i, void* stream) {
   if (!artsbir_knn_scan_aug_supported(Dp)) { set_error("knn_scan_aug: Dp=%d not in {64,128,256,512}", Dp); return -1; }
   if (tiles_per_chunk <= 0 || (long long)tiles_per_chunk * 128 * (2LL * Dp + 16) > 0x7fffffffLL) {
     set_error("knn_scan_aug: tiles_per_chunk=%d out of range", tiles_per_chunk);
     return -1;
   }
+  if (kbound && (k < 1 || k > KT)) { set_error("knn_scan_aug: k=%d must be in 1..%d with a shared bound", k, KT); return -1; }
   if (nq <= 0 || ng <= 0) return 0;
   KnnScanArgs a;
-  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.Nq = nq; a.Ng = ng; a.D = Dp;
+  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.thr0 = thr0; a.kb = kbound; a.kq = k; a.rel = rel; a.Nq = nq; a.Ng = ng; a.D = Dp;
   a.tiles_per_chunk = tiles_per_chunk;
   const int tiles = (ng + 127) / 128;
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;

@@ -135,7 +135,7 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    scan_kernel = next((kn for kn, *_ in prof if kn.startswith("knn_scan")), "knn_scan_kernel")
+    scan_kernel = "knn_scan_v2_kernel" if any(kn == "knn_scan_v2_kernel" for kn, *_ in prof) else "knn_scan_kernel"
     scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1, *_ in prof if kn == scan_kernel]
     scan_s = sum(s for _, s in scan) / len(scan)
     scan_fl = sum(f for f, _ in scan) / len(scan)

@@ -235,10 +235,17 @@ int artsbir_rows_prep_aug(const float* x, int n, int D, int Dp, float* sq, void*
 int artsbir_knn_scan_aug_supported(int Dp);
 /* the same candidate lists / counts / uncertain queue as artsbir_knn_scan (bf16), from
  * qc [nq][Dp] bf16 and the augmented gallery ga [ng][Dp + 8]: register-resident query
- * fragments, 32-row gallery tiles by LDS-DMA, 32x32x16 MFMA (inference.py:30-69). */
+ * fragments, 32-row gallery tiles by LDS-DMA, 32x32x16 MFMA (inference.py:30-69).  thr0 (may be
+ * NULL) seeds each query's list threshold: only items with approximate d^2 < thr0[q] enter
+ * the lists (a valid seed is >= the k-th smallest approximate d^2 of the gallery + 2 eps).
+ * kbound (may be NULL): [nq] shared bound, initialised to 0xFF800000 (+inf encoded); every
+ * chunk publishes its k-th smallest approximate d^2 there (atomicMin of an order-preserving
+ * encoding) and reads the others' every 8 tiles, using bound + 2 eps (eps = rel |q| max|g|
+ * + 1e-3) as its list threshold: items at or above it cannot reach the exact top k. */
 int artsbir_knn_scan_aug(const void* qc, const void* ga, const float* qsq, float gsq_max, int nq, int ng,
-                         int Dp, int tiles_per_chunk, const float* lo, const float* hi, int* cnt, int* unc, int unc_cap,
-                         float* cand_d, int* cand_i, void* stream);
+                         int Dp, int tiles_per_chunk, const float* thr0, unsigned* kbound, int k, float rel,
+                         const float* lo, const float* hi, int* cnt, int* unc, int unc_cap, float* cand_d,
+                         int* cand_i, void* stream);
 /* exact f64 top-k by (distance, index) from the candidates; flag[q] = 1 when a
  * chunk list could have dropped a true top-k item (caller re-runs exhaustively). */
 int artsbir_knn_merge(const float* q, const float* g, int D, int nq, int nchunks, const float* cand_d,

@@ -75,7 +75,7 @@ def test_pairwise_l2_matches_torch(dev):
                           torch.nn.PairwiseDistance(p=2)(b, c), rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("scan", ["auto", "v1"])
+@pytest.mark.parametrize("scan", ["auto", "auto-noshare", "v1"])
 @pytest.mark.parametrize("N,D,Q,tpc", [(5000, 100, 300, 1), (9000, 256, 520, 2), (20, 64, 3, 64), (1000, 512, 257, 1)])
 def test_knn_chunks_ragged(scan, N, D, Q, tpc, dev):
     """many gallery chunks (small tiles_per_chunk), ragged D (zero-padded), partial query tiles
@@ -85,7 +85,8 @@ def test_knn_chunks_ragged(scan, N, D, Q, tpc, dev):
     pos = pos.copy()
     pos[::5] = -1
     idx, dist, rank, _ = knn.knn(torch.from_numpy(qs).to(dev), torch.from_numpy(g).to(dev), min(10, N),
-                                 torch.from_numpy(pos).to(dev), scan=scan, tiles_per_chunk=tpc)
+                                 torch.from_numpy(pos).to(dev), scan=scan.split("-")[0], tiles_per_chunk=tpc,
+                                 share_bound=not scan.endswith("noshare"))
     ri, rd, rr = _oracle(g, qs, pos, min(10, N))
     np.testing.assert_array_equal(idx.cpu().numpy(), ri)
     np.testing.assert_allclose(dist.cpu().numpy(), rd, rtol=1e-12)
@@ -126,7 +127,8 @@ def test_knn_scan_v2_candidates_equal_v1(dev):
         cd = torch.empty(Q, ncand, device=dev)
         ci = torch.empty(Q, ncand, dtype=torch.int32, device=dev)
         if v2:
-            call("artsbir_knn_scan_aug", ptr(qc), ptr(ga), ptr(qsq), float(gsq.max()), Q, N, D, tpc, ptr(lo), ptr(hi),
+            call("artsbir_knn_scan_aug", ptr(qc), ptr(ga), ptr(qsq), float(gsq.max()), Q, N, D, tpc, None, None, 0, 0.0,
+                 ptr(lo), ptr(hi),
                  ptr(cnt), ptr(unc), 4096, ptr(cd), ptr(ci), _hip.stream())
         else:
             call("artsbir_knn_scan", _hip.DT_BF16, ptr(qc), ptr(gc), ptr(qsq), ptr(gsq), Q, N, D, tpc, ptr(lo),
@@ -144,3 +146,19 @@ def test_knn_scan_v2_candidates_equal_v1(dev):
     assert len(set(p1) ^ set(p2)) <= max(2, n1 // 50)
     m = ci1 == ci2
     np.testing.assert_allclose(cd1[m].numpy(), cd2[m].numpy(), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("noise", [0.5, 3.0])
+def test_knn_threshold_prepass(noise, dev):
+    """the v2 scan seeded by the pre-pass threshold (prepass_rows=1024 so that a 20k gallery
+    takes that path) gives the oracle's exact top-k and ranks; also with far positives."""
+    import knn
+    N, D, Q = 20000, 128, 300
+    g, qs, pos = oret.synthetic_gallery(N, D, Q, noise=noise)
+    for tpc in (64, 2):
+        idx, dist, rank, _ = knn.knn(torch.from_numpy(qs).to(dev), torch.from_numpy(g).to(dev), 10,
+                                     torch.from_numpy(pos).to(dev), prepass_rows=1024, tiles_per_chunk=tpc)
+        ri, rd, rr = _oracle(g, qs, pos, 10)
+        np.testing.assert_array_equal(idx.cpu().numpy(), ri)
+        np.testing.assert_allclose(dist.cpu().numpy(), rd, rtol=1e-12)
+        np.testing.assert_array_equal(rank.cpu().numpy(), rr)

@@ -18,7 +18,9 @@ if __name__ == "__main__":
     dev = torch.device("cuda:0")
     orig = knn.knn
     for scan in (sys.argv[1:] or ["auto", "v1"]):
-        knn.knn = lambda *a, _s=scan, **kw: orig(*a, scan=_s, **kw)
+        sc = scan.split("+")[0].split("-")[0]  # e.g. auto, v1, auto-noshare, auto+prepass
+        knn.knn = (lambda *a, _s=sc, _p=(8192 if "+prepass" in scan else 0), _b=("-noshare" not in scan), **kw:
+                   orig(*a, scan=_s, prepass_rows=_p, share_bound=_b, **kw))
         r = bench.retrieval_leg(dev, 0, 1)
         r["scan"] = scan
         print(json.dumps(r), flush=True)
