@@ -541,6 +541,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
   const float eps_own = q_own < a.Nq ? a.rel * sqrtf(a.qsq[q_own] * gmax) * 1.001f + 1e-3f : 0.f;
   float thr_g = s_thr[R_own];  // best shared bound seen (with thr0)
 
+  bool atom = false;  // this wave issued a global atomic since its last DMA wait
   for (int t = 0; t < ntiles; ++t) {
     if (t + 2 < ntiles) issue_tile(t + 2);
     const char* st = smem + (t % C::NST) * C::STAGE;
@@ -563,15 +564,30 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
     const int bn = g0 + t * V2_ROWS;
     const bool cvalid = bn + r32 < a.Ng;
     const float gsq = cvalid ? *reinterpret_cast<const float*>(st + r32 * C::RB + 32 * KB) : INFINITY;
+    // stage t+1 landed (this wave's DMAs; the barrier publishes everyone's).  The
+    // barrier sits BEFORE this tile's epilogue: a wave busy inserting list hits
+    // then overlaps the next tile's MFMAs of the other waves instead of holding
+    // them at the barrier.  So after it, stage t may already be refilled (DMA of
+    // tile t+3): the epilogue reads no stage, only gsq (saved above) and its own
+    // wave's LDS.  An atomic of the previous epilogue forces the full wait.
+    if (t + 1 < ntiles) {
+      if (t + 2 < ntiles && !__builtin_amdgcn_ballot_w64(atom))
+        rvm_wait_n(my_ni);
+      else
+        rvm_wait<0>();
+    }
+    atom = false;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage t (gsq) are done
+    __syncthreads();
     bool any = false;
 #pragma unroll
     for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[e], gsq) <= critp[e];
-    bool atom = false;
     if (__builtin_amdgcn_ballot_w64(any)) {
       // stage the raw dot products of every row with a prefilter hit; the owner
       // of each row re-evaluates its hits exactly (d2 with the same formula as
       // knn_scan_kernel): list insertion, certainly-closer count, uncertain queue
       unsigned mymask = 0;
+      if (lane < 32) stg[r32 * C::SP + 32] = gsq;  // column r32's |g|^2 (INF past Ng), in the row padding
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const unsigned long long m = __builtin_amdgcn_ballot_w64(fmaf(-2.f, acc[e], gsq) <= critp[e]);
@@ -583,15 +599,17 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       bool changed = false;
+      // every lane reads its (owner) row's state: lanes >= 32 mirror row lane - 32
+      const float qs = s_qsq[R_own], hi = s_hi[R_own];
+      float thr = s_thr[R_own];
       if (lane < 32 && mymask) {
-        const float qs = s_qsq[R_own], lo = s_lo[R_own], hi = s_hi[R_own];
+        const float lo = s_lo[R_own];
         const float* srow = stg + orow * C::SP;
-        float thr = s_thr[R_own];
         while (mymask) {
           const int c = __builtin_ctz(mymask);
           mymask &= mymask - 1;
           const bool valid = bn + c < a.Ng;
-          const float g2 = valid ? *reinterpret_cast<const float*>(st + c * C::RB + 32 * KB) : INFINITY;
+          const float g2 = stg[c * C::SP + 32];
           const float d2 = fmaf(-2.f, srow[c], qs + g2);
           if (d2 < thr) {
             float x = d2;
@@ -639,9 +657,16 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
         }
       }
       if (__builtin_amdgcn_ballot_w64(changed)) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        load_crit();
+        // refresh the prefilter bounds from the owner lanes' registers (readlane:
+        // no fence, no LDS round trip); the same value load_crit() would read
+        const float mine = (fmaxf(thr, hi) - qs) + 0x1p-18f * (qs + gmax);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r0 = (e & 3) + 8 * (e >> 2);
+          const float n0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), r0));
+          const float n1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), r0 + 4));
+          critp[e] = h ? n1 : n0;
+        }
       }
     }
     if (a.kb && (t & 7) == 7 && t + 1 < ntiles) {
@@ -667,14 +692,6 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
         load_crit();
       }
     }
-    if (t + 1 < ntiles) {
-      // stage t+1 landed (this wave's DMAs; the barrier publishes everyone's)
-      if (t + 2 < ntiles && !__builtin_amdgcn_ballot_w64(atom))
-        rvm_wait_n(my_ni);
-      else
-        rvm_wait<0>();
-    }
-    __syncthreads();
   }
   if (lane < 32) {
     const int q = qb + R_own;
