@@ -176,6 +176,24 @@ def _exact_counts(q, g, pos, dpos, g_base):
     return cnt
 
 
+def shard_positive_distances(queries, gallery_shard, g_base: int, positives):
+    """f64 [Q]: the exact ||q - g_pos + 1e-6|| for queries whose positive lies in this
+    shard's rows [g_base, g_base + n), -1 for the others (and for no positive).  One
+    knn_band launch: the same exact_l2 as every other exact decision of the scan."""
+    q = queries.detach().contiguous().float()
+    g = gallery_shard.detach().contiguous().float()
+    Q, D = q.shape
+    dev = q.device
+    pos = positives.to(dev, torch.int64).contiguous()
+    dpos = torch.full((Q,), -1.0, dtype=torch.float64, device=dev)
+    qsq = torch.zeros(Q, dtype=torch.float32, device=dev)  # only feeds lo/hi, unused here
+    lo = torch.empty(Q, dtype=torch.float32, device=dev)
+    hi = torch.empty(Q, dtype=torch.float32, device=dev)
+    call("artsbir_knn_band", ptr(q), ptr(g), ptr(pos), g_base, g.shape[0], ptr(qsq), 0.0, Q, D, 0.0, ptr(dpos),
+         ptr(lo), ptr(hi), _s())
+    return dpos
+
+
 def knn_sharded(queries, gallery_shard, g_base: int, k: int = 10, positives=None, compute="bf16"):
     """Gallery sharded over the ranks of the default process group (RCCL):
     every rank passes ITS shard [g_base, g_base + n) and the same queries."""
@@ -185,18 +203,7 @@ def knn_sharded(queries, gallery_shard, g_base: int, k: int = 10, positives=None
     dpos = None
     if positives is not None:
         # exact positive distance from the owning shard, then shared (max of -1s)
-        pos = positives.to(queries.device, torch.int64)
-        n = gallery_shard.shape[0]
-        own = (pos >= g_base) & (pos < g_base + n)
-        dpos = torch.full((Q,), -1.0, dtype=torch.float64, device=queries.device)
-        if bool(own.any()):
-            qi = torch.nonzero(own).flatten()
-            sub = queries[qi].contiguous().float()
-            d = torch.empty(len(qi), dtype=torch.float64, device=queries.device)
-            gsub = gallery_shard.float()[pos[qi] - g_base].contiguous()
-            for j in range(len(qi)):
-                call("artsbir_knn_exact_all", ptr(sub[j]), ptr(gsub[j]), sub.shape[1], 1, ptr(d[j:j + 1]), _s())
-            dpos[qi] = d
+        dpos = shard_positive_distances(queries, gallery_shard, g_base, positives)
         dist.all_reduce(dpos, op=dist.ReduceOp.MAX)
     idx, dd, rank, _ = knn(queries, gallery_shard, k, positives, compute, g_base=g_base, dpos=dpos)
     all_i = [torch.empty_like(idx) for _ in range(world)]

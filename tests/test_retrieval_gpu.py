@@ -162,3 +162,28 @@ def test_knn_threshold_prepass(noise, dev):
         np.testing.assert_array_equal(idx.cpu().numpy(), ri)
         np.testing.assert_allclose(dist.cpu().numpy(), rd, rtol=1e-12)
         np.testing.assert_array_equal(rank.cpu().numpy(), rr)
+
+
+def test_knn_shards_on_one_gpu_match_oracle(dev):
+    """the sharded protocol of knn.knn_sharded run shard by shard on one GPU (uneven
+    row shards, positives in every shard and some missing): owner dpos, max-combine,
+    per-shard exact top-k and counts, merge_topk, summed ranks == the oracle."""
+    import knn
+    N, D, Q, k = 7000, 512, 300, 10
+    g, qs, pos = oret.synthetic_gallery(N, D, Q, noise=1.5)
+    pos = pos.copy()
+    pos[::9] = -1
+    q = torch.from_numpy(qs).to(dev)
+    gg = torch.from_numpy(g).to(dev)
+    p = torch.from_numpy(pos).to(dev)
+    bounds = [0, 1234, 4000, N]
+    shards = [(b0, gg[b0:b1].contiguous()) for b0, b1 in zip(bounds[:-1], bounds[1:])]
+    dpos = torch.stack([knn.shard_positive_distances(q, sh, b0, p) for b0, sh in shards]).max(dim=0).values
+    outs = [knn.knn(q, sh, k, p, g_base=b0, dpos=dpos) for b0, sh in shards]
+    mi, md = knn.merge_topk([o[0] for o in outs], [o[1] for o in outs], k)
+    rank = sum(o[2] for o in outs)
+    ri, rd, rr = _oracle(g, qs, pos, k)
+    np.testing.assert_array_equal(mi.cpu().numpy(), ri)
+    np.testing.assert_allclose(md.cpu().numpy(), rd, rtol=1e-12)
+    r = rank.cpu().numpy()
+    np.testing.assert_array_equal(r[pos >= 0], rr[pos >= 0])
