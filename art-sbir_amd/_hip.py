@@ -33,7 +33,7 @@ class ConvDesc(ctypes.Structure):
 
 class BnBwdDesc(ctypes.Structure):
     _fields_ = [("dtype", _c_int), ("kind", _c_int), ("pool", _c_int), ("d", _vp), ("mask", _vp),
-                ("mask_scale", _vp), ("mask_shift", _vp), ("ntarget", _c_int), ("y", _vp * 2),
+                ("mask_bn", _vp), ("ntarget", _c_int), ("y", _vp * 2),
                 ("mean", _vp * 2), ("istd", _vp * 2), ("slots", _vp * 2), ("coef", _vp * 2), ("dy", _vp * 2),
                 ("gout", _vp), ("B", _c_int), ("H", _c_int), ("W", _c_int), ("C", _c_int)]
 
@@ -50,6 +50,8 @@ SIGNATURES = {
     "artsbir_version": [],
     "artsbir_last_error": [],
     "artsbir_last_kernel": [],
+    "artsbir_tune_save": [ctypes.c_char_p],
+    "artsbir_tune_load": [ctypes.c_char_p],
     "artsbir_conv2d_fwd": [_P, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_conv2d_wgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_gemm_nt": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
@@ -63,9 +65,10 @@ SIGNATURES = {
     "artsbir_cast": [_c_int, _vp, _c_int, _vp, _c_ll, _vp],
     "artsbir_bn_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float, _c_float, _c_int,
                             _vp, _vp, _vp, _vp, _vp],
-    "artsbir_act_pool": [_c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
-    "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp],
-    "artsbir_block_out_mask": [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
+    "artsbir_bn_stats_det": [_c_int, _vp, _c_int, _c_ll, _c_int, _vp, _c_ll, _vp],
+    "artsbir_act_pool": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp],
+    "artsbir_block_out_mask": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
     "artsbir_layernorm_fwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp],
     "artsbir_quickgelu": [_c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
@@ -74,6 +77,7 @@ SIGNATURES = {
     "artsbir_bn_bwd_finalize_seg": [_vp, _c_int, _c_ll, _c_int, ctypes.c_double, _vp, _vp, _c_ll, _vp, _vp, _vp,
                                     _vp],
     "artsbir_bn_bwd_reduce": [_PB, _vp],
+    "artsbir_set_deterministic": [_c_int],
     "artsbir_bn_bwd_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp],
     "artsbir_bn_bwd_apply": [_PB, _vp],
     "artsbir_colsum": [_c_int, _vp, _c_ll, _c_ll, _c_ll, _vp, _vp],
@@ -101,6 +105,14 @@ SIGNATURES = {
                           _vp, _vp, _vp],
     "artsbir_knn_uncertain": [_vp, _vp, _c_int, _vp, _c_int, _vp, _vp, _c_ll, _vp, _vp],
     "artsbir_knn_exact_all": [_vp, _vp, _c_int, _c_int, _vp, _vp],
+    "artsbir_pairwise_l2_topk_workspace": [_c_int, _c_int, _c_ll, _c_int, _c_int, _c_int],
+    "artsbir_pairwise_l2_topk": [_c_int, _c_int, _vp, _c_int, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _c_ll, _c_int,
+                                 _vp, _vp, _vp, _vp, _vp, _c_ll, _vp],
+    "artsbir_scan_profile": [_c_int],
+    "artsbir_knn_set_unc_cap": [_c_int],
+    "artsbir_scan_profile_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)],
+    "artsbir_topk_merge": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_positive_key": [_c_int, _vp, _c_int, _vp, _c_ll, _c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_pairwise_l2_bwd": [_vp, _c_ll, _vp, _c_ll, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp],
     "artsbir_linear_fwd": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_linear_bwd": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
@@ -112,7 +124,7 @@ SIGNATURES = {
     "artsbir_hinge_bwd": [_vp, _vp, _c_int, _c_float, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_last_kernel": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll,
-             "artsbir_knn_candidates_per_query": _c_int}
+             "artsbir_knn_candidates_per_query": _c_int, "artsbir_pairwise_l2_topk_workspace": _c_ll}
 
 _lib = None
 

@@ -58,11 +58,11 @@ __global__ void pack_input_kernel(const float* __restrict__ x, T* __restrict__ o
 }
 
 // ------------------------------------------------------- bn finalize (forward)
-// stats [NSLOT][2][C] (sum, sum of squares) -> mean, istd, scale, shift;
+// stats [NSLOT][2][C] (sum, sum of squares) -> mean, istd, scale = gamma*istd, beta;
 // train: update running stats (momentum, unbiased var) and num_batches_tracked.
 __global__ void bn_finalize_kernel(const float* __restrict__ stats, int C, double count, const float* gamma,
                                    const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
-                                   float eps, int train, float* mean_out, float* istd_out, float* scale, float* shift) {
+                                   float eps, int train, float* mean_out, float* istd_out, float* scale, float* beta_out) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && train && nbt) nbt[0] += 1;
   if (c >= C) return;
@@ -87,12 +87,13 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int C, doubl
   mean_out[c] = (float)mean;
   istd_out[c] = is;
   scale[c] = sc;
-  shift[c] = beta[c] - (float)mean * sc;
+  beta_out[c] = beta[c];
 }
 
 // all nseg BN segments of one layer in one launch: per channel the segments in
 // order (running statistics updated once per segment, as the reference's
-// consecutive forward calls do); out[s] = {mean, istd, scale, shift}[C]
+// consecutive forward calls do); out[s] = {mean, istd, scale, beta}[C] — the BN
+// parameter block every consumer applies as (y - mean) * scale + beta
 __global__ void bn_finalize_seg_kernel(const float* __restrict__ stats, int nseg, long long seg_stride, int C,
                                        double count, const float* gamma, const float* beta, float* rmean, float* rvar,
                                        long long* nbt, float momentum, float eps, int train, float* __restrict__ out) {
@@ -123,15 +124,67 @@ __global__ void bn_finalize_seg_kernel(const float* __restrict__ stats, int nseg
     o[c] = (float)mean;
     o[C + c] = is;
     o[2 * C + c] = sc;
-    o[3 * C + c] = beta[c] - (float)mean * sc;
+    o[3 * C + c] = beta[c];
+  }
+}
+
+// --------------------------------------- deterministic BN statistics (parity)
+// The conv epilogues add their per-channel sums into replica slots with f32
+// atomics, whose order changes from run to run; on tiny parity batches that
+// noise can move a pre-activation across zero (a ReLU flip).  In the
+// deterministic mode (artsbir_set_deterministic) the engine launches the conv
+// without statistics and this kernel sums the stored output y of each segment
+// in a fixed order in f64: thread (rl, c) takes rows rl, rl+16, ... of channel
+// c, the 16 partials are added in index order.  The f64 sums are written as
+// f32 hi/lo pairs into slots 0 and 1 (other slots zero), so bn_finalize's f64
+// sum over the slots sees ~48 significant bits.  grid (ceil(C/64), nseg).
+template <typename T>
+__global__ void __launch_bounds__(1024) bn_stats_det_kernel(const T* __restrict__ y, long long rows, int C,
+                                                            float* __restrict__ stats, long long seg_stride) {
+  __shared__ double red[2][16][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const T* ys = y + (long long)blockIdx.y * rows * C;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < C) {
+    for (long long r = rl; r < rows; r += 16) {
+      const double v = (double)to_f(ys[r * C + c]);
+      s1 += v;
+      s2 += v * v;
+    }
+  }
+  red[0][rl][cl] = s1;
+  red[1][rl][cl] = s2;
+  __syncthreads();
+  if (rl != 0 || c >= C) return;
+  double t1 = 0.0, t2 = 0.0;
+  for (int k = 0; k < 16; ++k) { t1 += red[0][k][cl]; t2 += red[1][k][cl]; }
+  float* st = stats + (long long)blockIdx.y * seg_stride;
+  const float h1 = (float)t1, h2 = (float)t2;
+  st[c] = h1;
+  st[C + c] = h2;
+  st[2 * C + c] = (float)(t1 - (double)h1);
+  st[3 * C + c] = (float)(t2 - (double)h2);
+  for (int k = 2; k < ARTSBIR_NSLOT; ++k) {
+    st[(long long)k * 2 * C + c] = 0.f;
+    st[(long long)k * 2 * C + C + c] = 0.f;
   }
 }
 
 // ------------------------------------------------ affine(+relu)(+avgpool 2x2)
-// out = pool?( act(x) ), act = x*sc+sh then ReLU (sc==NULL: identity, no relu)
+// out = pool?( act(x) ), act = (x - mean) * scale + beta then ReLU, from the BN
+// parameter block bn [4][C] = mean, istd, scale, beta (bn == NULL: identity, no
+// relu).  Subtracting the mean first keeps the f32 result accurate when
+// |mean| >> std (x*scale + (beta - mean*scale) loses |mean|/std ulps).
+__device__ __forceinline__ void load_bn8(const float* bn, int C, int c0, float (&m)[8], float (&s)[8], float (&b)[8]) {
+  loadf8(bn + c0, m);
+  loadf8(bn + 2 * C + c0, s);
+  loadf8(bn + 3 * C + c0, b);
+}
+
 template <typename T>
-__global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict__ sc, const float* __restrict__ sh,
-                                int relu, int pool, int B, int H, int W, int C, T* __restrict__ out) {
+__global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict__ bn, int relu, int pool, int B,
+                                int H, int W, int C, T* __restrict__ out) {
   const int CG = C / 8;
   const int Ho = pool ? H / pool : H, Wo = pool ? W / pool : W;
   const long long n = (long long)B * Ho * Wo * CG;
@@ -142,8 +195,8 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
     long long t = pix / Wo;
     int oh = (int)(t % Ho);
     long long b = t / Ho;
-    float s[8], h[8];
-    if (sc) { loadf8(sc + cg * 8, s); loadf8(sh + cg * 8, h); }
+    float mn[8], s[8], h[8];
+    if (bn) load_bn8(bn, C, cg * 8, mn, s, h);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int P = pool ? pool : 1;
     for (int dy = 0; dy < P; ++dy)
@@ -152,7 +205,7 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
         load8<T>(x + (((b * H + oh * P + dy) * W + ow * P + dx) * C + cg * 8), v);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float a = sc ? v[e] * s[e] + h[e] : v[e];
+          float a = bn ? (v[e] - mn[e]) * s[e] + h[e] : v[e];
           if (relu) a = fmaxf(a, 0.f);
           acc[e] += a;
         }
@@ -165,33 +218,30 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
 }
 
 // --------------------------------------------------------- bottleneck output
-// out = relu(y3*sc3+sh3 + (yd ? yd*scd+shd : idn))
+// out = relu(bn3(y3) + (yd ? bnd(yd) : idn)), bn(y) = (y - mean) * scale + beta
 template <typename T>
-__global__ void block_out_kernel(const T* __restrict__ y3, const float* __restrict__ sc3, const float* __restrict__ sh3,
-                                 const T* __restrict__ yd, const float* __restrict__ scd, const float* __restrict__ shd,
-                                 const T* __restrict__ idn, long long rows, int C, T* __restrict__ out,
-                                 unsigned char* __restrict__ bits) {
+__global__ void block_out_kernel(const T* __restrict__ y3, const float* __restrict__ bn3, const T* __restrict__ yd,
+                                 const float* __restrict__ bnd, const T* __restrict__ idn, long long rows, int C,
+                                 T* __restrict__ out, unsigned char* __restrict__ bits) {
   const int CG = C / 8;
   const long long n = rows * CG;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     int cg = (int)(i % CG);
     long long off = (i / CG) * C + cg * 8;
-    float a[8], s[8], h[8], r[8];
+    float a[8], m[8], s[8], h[8], r[8];
     load8<T>(y3 + off, a);
-    loadf8(sc3 + cg * 8, s);
-    loadf8(sh3 + cg * 8, h);
+    load_bn8(bn3, C, cg * 8, m, s, h);
     if (yd) {
-      float s2[8], h2[8];
+      float m2[8], s2[8], h2[8];
       load8<T>(yd + off, r);
-      loadf8(scd + cg * 8, s2);
-      loadf8(shd + cg * 8, h2);
+      load_bn8(bnd, C, cg * 8, m2, s2, h2);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) r[e] = r[e] * s2[e] + h2[e];
+      for (int e = 0; e < 8; ++e) r[e] = (r[e] - m2[e]) * s2[e] + h2[e];
     } else {
       load8<T>(idn + off, r);
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) a[e] = fmaxf(a[e] * s[e] + h[e] + r[e], 0.f);
+    for (int e = 0; e < 8; ++e) a[e] = fmaxf((a[e] - m[e]) * s[e] + h[e] + r[e], 0.f);
     store8<T>(out + off, a);
     if (bits) {  // ReLU mask of the stored values, one bit per channel
       unsigned m = 0;
@@ -205,7 +255,7 @@ __global__ void block_out_kernel(const T* __restrict__ y3, const float* __restri
 // ------------------------------------------------------------ BN backward
 // Two flavours of the upstream gradient g at an element of the BN output:
 //   RES: g = dout * (out > 0)                      (block output ReLU)
-//   ACT: g = up(d) * (y*sc + sh > 0)               (ReLU after BN; up = identity
+//   ACT: g = up(d) * (bn(y) > 0)                   (ReLU after BN; up = identity
 //        or 2x2 average-unpool when the forward pooled after the ReLU)
 // For up to two BN targets t (y3 and the downsample yd share g), with
 //   xhat_t = (y_t - mean_t) * istd_t:
@@ -216,8 +266,7 @@ struct BnBwdArgs {
   int pool;   // ACT: forward pooled by `pool` after the ReLU (0/1 = none)
   const void* d;     // RES: dout ; ACT: d (pooled resolution if pool>1)
   const void* mask;  // RES: out
-  const float* msc;  // ACT: scale/shift of the BN feeding the ReLU (target 0)
-  const float* msh;
+  const float* mbn;  // ACT: parameter block [4][C] of the BN feeding the ReLU (target 0)
   int ntarget;
   const void* y[2];
   const float* mean[2];
@@ -235,7 +284,8 @@ struct BnBwdArgs {
 // per-channel parameters are loaded once; no per-element index division.
 template <typename T, int KIND, int POOL>
 __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, long long (&offs)[POOL * POOL],
-                                          float (&g)[POOL * POOL][8], const float (&ms)[8], const float (&mh)[8]) {
+                                          float (&g)[POOL * POOL][8], const float (&mm)[8], const float (&ms)[8],
+                                          const float (&mh)[8]) {
   if constexpr (POOL == 1) {
     offs[0] = (long long)u * a.C + cg * 8;
   } else {
@@ -272,7 +322,7 @@ __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, lo
       float y[8];
       load8<T>(reinterpret_cast<const T*>(a.y[0]) + offs[q], y);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) g[q][e] = (y[e] * ms[e] + mh[e]) > 0.f ? dv[e] * inv : 0.f;
+      for (int e = 0; e < 8; ++e) g[q][e] = ((y[e] - mm[e]) * ms[e] + mh[e]) > 0.f ? dv[e] * inv : 0.f;
     }
   }
 }
@@ -295,13 +345,13 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[t][q][e] = 0.f;
   if (rl < RL) {
-    float mn[2][8], is[2][8], ms[8], mh[8];
+    float mn[2][8], is[2][8], mm[8], ms[8], mh[8];
     for (int t = 0; t < a.ntarget; ++t) { loadf8(a.mean[t] + cg * 8, mn[t]); loadf8(a.istd[t] + cg * 8, is[t]); }
-    if constexpr (KIND == 1) { loadf8(a.msc + cg * 8, ms); loadf8(a.msh + cg * 8, mh); }
+    if constexpr (KIND == 1) load_bn8(a.mbn, a.C, cg * 8, mm, ms, mh);
     for (int u = u0 + rl; u < u1; u += RL) {
       long long offs[NQ];
       float g[NQ][8];
-      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, ms, mh);
+      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, mm, ms, mh);
       if constexpr (POOL == 1) {  // g written back (in place over d allowed)
         if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + offs[0], g[0]);
       }
@@ -347,6 +397,72 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
     }
 }
 
+// Deterministic mode (artsbir_set_deterministic): the same reduction by ONE
+// workgroup in a fixed order with f64 accumulators — lane (rl, cg) walks units
+// rl, rl+RL, ..., the RL partials are added in lane order — written as f32 hi/lo
+// pairs to slots 0/1 (other slots zeroed).  The f32 atomics above lose ~1e-7 of
+// sum |g xhat| per add, which the BN backward's cancellation (g - mean g - xhat
+// mean(g xhat)) turns into percent-level errors of small channels in parity runs.
+template <typename T, int KIND, int POOL>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_det_kernel(BnBwdArgs a) {
+  constexpr int NQ = POOL * POOL;
+  const int CG = a.C / 8;
+  const int RL = 256 / CG;
+  const int tid = threadIdx.x;
+  const int cg = tid % CG, rl = tid / CG;
+  const int units = a.B * (a.H / POOL) * (a.W / POOL);
+  double acc[2][2][8];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[t][q][e] = 0.0;
+  if (rl < RL) {
+    float mn[2][8], is[2][8], mm[8], ms[8], mh[8];
+    for (int t = 0; t < a.ntarget; ++t) { loadf8(a.mean[t] + cg * 8, mn[t]); loadf8(a.istd[t] + cg * 8, is[t]); }
+    if constexpr (KIND == 1) load_bn8(a.mbn, a.C, cg * 8, mm, ms, mh);
+    for (int u = rl; u < units; u += RL) {
+      long long offs[NQ];
+      float g[NQ][8];
+      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, mm, ms, mh);
+      if constexpr (POOL == 1) {
+        if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + offs[0], g[0]);
+      }
+      for (int t = 0; t < a.ntarget; ++t) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          float y[8];
+          load8<T>(reinterpret_cast<const T*>(a.y[t]) + offs[q], y);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            acc[t][0][e] += (double)g[q][e];
+            acc[t][1][e] += (double)g[q][e] * ((double)(y[e] - mn[t][e]) * (double)is[t][e]);
+          }
+        }
+      }
+    }
+  }
+  __shared__ double red[256 * 8];
+  for (int t = 0; t < a.ntarget; ++t)
+    for (int q = 0; q < 2; ++q) {
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[tid * 8 + e] = (rl < RL) ? acc[t][q][e] : 0.0;
+      __syncthreads();
+      for (int c = tid; c < a.C; c += 256) {
+        const int cgi = c / 8, e = c % 8;
+        double sum = 0.0;
+        for (int l = 0; l < RL; ++l) sum += red[(l * CG + cgi) * 8 + e];
+        const float hi = (float)sum;
+        float* sl = a.slots[t] + q * a.C + c;
+        sl[0] = hi;
+        sl[2LL * a.C] = (float)(sum - (double)hi);
+        for (int k = 2; k < ARTSBIR_NSLOT; ++k) sl[(long long)k * 2 * a.C] = 0.f;
+      }
+    }
+}
+
 template <typename T, int KIND, int POOL>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int units_per_block) {
   constexpr int NQ = POOL * POOL;
@@ -358,7 +474,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
   const int units = a.B * (a.H / POOL) * (a.W / POOL);
   const int u0 = blockIdx.x * units_per_block;
   const int u1 = min(u0 + units_per_block, units);
-  float mn[2][8], is[2][8], c1[2][8], c2[2][8], c3[2][8], ms[8], mh[8];
+  float mn[2][8], is[2][8], c1[2][8], c2[2][8], c3[2][8], mm[8], ms[8], mh[8];
   for (int t = 0; t < a.ntarget; ++t) {
     loadf8(a.mean[t] + cg * 8, mn[t]);
     loadf8(a.istd[t] + cg * 8, is[t]);
@@ -366,11 +482,11 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
     loadf8(a.coef[t] + a.C + cg * 8, c2[t]);
     loadf8(a.coef[t] + 2 * a.C + cg * 8, c3[t]);
   }
-  if constexpr (KIND == 1) { loadf8(a.msc + cg * 8, ms); loadf8(a.msh + cg * 8, mh); }
+  if constexpr (KIND == 1) load_bn8(a.mbn, a.C, cg * 8, mm, ms, mh);
   for (int u = u0 + rl; u < u1; u += RL) {
     long long offs[NQ];
     float g[NQ][8];
-    bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, ms, mh);
+    bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, mm, ms, mh);
     if (a.gout) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) store8<T>(reinterpret_cast<T*>(a.gout) + offs[q], g[q]);
@@ -578,12 +694,12 @@ extern "C" int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int
 extern "C" int artsbir_bn_finalize(const float* stats, int C, double count, const float* gamma, const float* beta,
                                    float* running_mean, float* running_var, long long* num_batches_tracked,
                                    float momentum, float eps, int train, float* mean, float* istd, float* scale,
-                                   float* shift, void* stream) {
+                                   float* beta_out, void* stream) {
   if (train && !stats) { set_error("bn_finalize: train mode needs stats"); return -1; }
   if (!train && (!running_mean || !running_var)) { set_error("bn_finalize: eval mode needs running stats"); return -1; }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, stats, C, count,
                      gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps, train, mean, istd,
-                     scale, shift);
+                     scale, beta_out);
   ARTSBIR_CHECK_LAUNCH("bn_finalize");
   return 0;
 }
@@ -602,35 +718,45 @@ extern "C" int artsbir_bn_finalize_seg(const float* stats, int nseg, long long s
   return 0;
 }
 
-extern "C" int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* shift, int relu, int pool,
-                                int B, int H, int W, int C, void* out, void* stream) {
+extern "C" int artsbir_bn_stats_det(int dtype, const void* y, int nseg, long long rows, int C, float* stats,
+                                    long long seg_stride, void* stream) {
+  if (nseg < 1 || rows < 1 || C < 1 || !y || !stats) { set_error("bn_stats_det: bad arguments"); return -1; }
+  if (seg_stride < (long long)ARTSBIR_NSLOT * 2 * C) { set_error("bn_stats_det: seg_stride < NSLOT*2*C"); return -1; }
+  DISPATCH_T(dtype, hipLaunchKernelGGL(bn_stats_det_kernel<T>, dim3((C + 63) / 64, nseg), dim3(1024), 0,
+                                       (hipStream_t)stream, (const T*)y, rows, C, stats, seg_stride));
+  ARTSBIR_CHECK_LAUNCH("bn_stats_det");
+  return 0;
+}
+
+extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W,
+                                int C, void* out, void* stream) {
   if (C % 8) { set_error("act_pool: C %% 8 != 0"); return -1; }
   if (pool > 1 && (H % pool || W % pool)) { set_error("act_pool: H,W not divisible by pool"); return -1; }
   const int Ho = pool > 1 ? H / pool : H, Wo = pool > 1 ? W / pool : W;
   long long n = (long long)B * Ho * Wo * (C / 8);
   DISPATCH_T(dtype, hipLaunchKernelGGL(act_pool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)x, scale, shift, relu, pool > 1 ? pool : 0, B, H, W, C, (T*)out));
+                                       (const T*)x, bn, relu, pool > 1 ? pool : 0, B, H, W, C, (T*)out));
   ARTSBIR_CHECK_LAUNCH("act_pool");
   return 0;
 }
 
-extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
-                                      const float* scd, const float* shd, const void* identity, long long rows, int C,
-                                      void* out, unsigned char* mask_bits, void* stream) {
+extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                                      const void* identity, long long rows, int C, void* out,
+                                      unsigned char* mask_bits, void* stream) {
   if (C % 8) { set_error("block_out: C %% 8 != 0"); return -1; }
   if (!yd && !identity) { set_error("block_out: need downsample or identity input"); return -1; }
+  if (!bn3 || (yd && !bnd)) { set_error("block_out: missing BN parameter block"); return -1; }
   long long n = rows * (C / 8);
   DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)y3, sc3, sh3, (const T*)yd, scd, shd, (const T*)identity, rows, C,
+                                       (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, rows, C,
                                        (T*)out, mask_bits));
   ARTSBIR_CHECK_LAUNCH("block_out");
   return 0;
 }
 
-extern "C" int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
-                                 const float* scd, const float* shd, const void* identity, long long rows, int C,
-                                 void* out, void* stream) {
-  return artsbir_block_out_mask(dtype, y3, sc3, sh3, yd, scd, shd, identity, rows, C, out, nullptr, stream);
+extern "C" int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                                 const void* identity, long long rows, int C, void* out, void* stream) {
+  return artsbir_block_out_mask(dtype, y3, bn3, yd, bnd, identity, rows, C, out, nullptr, stream);
 }
 
 static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
@@ -644,7 +770,7 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
   if (d->kind < 0 || d->kind > 3) { set_error("bn_bwd: kind must be 0 .. 3"); return -1; }
   if (d->kind != 1 && d->pool > 1) { set_error("bn_bwd: pool only with kind 1"); return -1; }
   if ((long long)d->B * d->H * d->W >= (1LL << 31)) { set_error("bn_bwd: too many pixels"); return -1; }
-  a.kind = d->kind; a.pool = d->pool; a.d = d->d; a.mask = d->mask; a.msc = d->mask_scale; a.msh = d->mask_shift;
+  a.kind = d->kind; a.pool = d->pool; a.d = d->d; a.mask = d->mask; a.mbn = d->mask_bn;
   a.ntarget = d->ntarget;
   for (int t = 0; t < 2; ++t) {
     a.y[t] = d->y[t]; a.mean[t] = d->mean[t]; a.istd[t] = d->istd[t];
@@ -655,9 +781,21 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
   return 0;
 }
 
+static int g_deterministic = 0;  // artsbir_set_deterministic
+
 template <typename T>
 static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
   const int P = (a.kind == 1 && a.pool > 1) ? a.pool : 1;
+  if (reduce && g_deterministic) {
+#define BNB_DET(K, PP) hipLaunchKernelGGL((bn_bwd_reduce_det_kernel<T, K, PP>), dim3(1), dim3(256), 0, st, a)
+    if (a.kind == 0) BNB_DET(0, 1);
+    else if (a.kind == 2) BNB_DET(2, 1);
+    else if (a.kind == 3) BNB_DET(3, 1);
+    else if (P == 2) BNB_DET(1, 2);
+    else BNB_DET(1, 1);
+#undef BNB_DET
+    return;
+  }
   const int units = a.B * (a.H / P) * (a.W / P);
   const int RL = 256 / (a.C / 8);
   // ~2048 workgroups, each walking a contiguous range of units
@@ -675,6 +813,12 @@ static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
   else if (P == 2) BNB_LAUNCH(1, 2);
   else BNB_LAUNCH(1, 1);
 #undef BNB_LAUNCH
+}
+
+extern "C" int artsbir_set_deterministic(int on) {
+  const int old = g_deterministic;
+  g_deterministic = on ? 1 : 0;
+  return old;
 }
 
 extern "C" int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream) {

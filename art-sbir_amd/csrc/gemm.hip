@@ -28,6 +28,7 @@
 // (pixel offset + one validity bit per filter tap); per K-step only the tap
 // (r, s, ci) changes, and when C is a multiple of the K-step it is uniform
 // across the workgroup (scalar arithmetic).
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -744,7 +745,7 @@ static int bnb_reduce_pass(const ConvArgs& a, const artsbir_bn_bwd_desc* bd, hip
     d.gout = reinterpret_cast<char*>(a.y) + eo;
     if (bd->mask)  // kind 3: one mask byte per 8 channels
       d.mask = reinterpret_cast<const char*>(bd->mask) + (bd->kind == 3 ? s * seg_m * (a.Cout / 8) : eo);
-    if (bd->mask_scale) { d.mask_scale = bd->mask_scale + po; d.mask_shift = bd->mask_shift + po; }
+    if (bd->mask_bn) d.mask_bn = bd->mask_bn + po;
     for (int t = 0; t < bd->ntarget; ++t) {
       d.y[t] = reinterpret_cast<const char*>(bd->y[t]) + eo;
       d.mean[t] = bd->mean[t] + po;
@@ -846,7 +847,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
         p.bnb_istd[t] = bd->istd[t];
         p.bnb_slots[t] = bd->slots[t];
       }
-      p.bnb_msc = bd->mask_scale; p.bnb_msh = bd->mask_shift; p.bnb_mask = bd->mask;
+      p.bnb_mbn = bd->mask_bn; p.bnb_mask = bd->mask;
       p.bnb_pstride = a.bnb_pstride;
     }
     int choice;
@@ -960,7 +961,7 @@ extern "C" int artsbir_conv2d_dgrad_bnb(const artsbir_conv_desc* d, const void* 
     set_error("conv2d_dgrad_bnb: bad target count %d", bnb->ntarget);
     return -1;
   }
-  if (bnb->kind != 1 ? !bnb->mask : (!bnb->mask_scale || !bnb->mask_shift)) {
+  if (bnb->kind != 1 ? !bnb->mask : !bnb->mask_bn) {
     set_error("conv2d_dgrad_bnb: missing ReLU mask");
     return -1;
   }
@@ -1193,6 +1194,58 @@ extern "C" int artsbir_conv2d_wgrad(const artsbir_conv_desc* d, const void* dy, 
   a.dw = dw;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_wgrad<bf16>(a, st) : launch_wgrad<float>(a, st);
+}
+
+// Autotuner cache as a text file: one line per tuned shape ("c" conv keys, "w"
+// wgrad keys, then the choice).  bench.py saves it after a run and the profiled
+// re-runs load it first, so rocprofv3 / PMC passes see only the launches of the
+// steady-state step, no trial launches.
+extern "C" int artsbir_tune_save(const char* path) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  FILE* f = fopen(path, "w");
+  if (!f) { set_error("tune_save: cannot open %s", path); return -1; }
+  for (const auto& kv : g_conv_choice) {
+    const ConvKey& k = kv.first;
+    fprintf(f, "c %lld %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d\n", k.M, k.H, k.W, k.C, k.Cout, k.R, k.S,
+            k.stride, k.pad, k.Ho, k.Wo, k.res_mode, k.stats, k.nseg, k.bnb, kv.second);
+  }
+  for (const auto& kv : g_wg_choice) {
+    const WgKey& k = kv.first;
+    fprintf(f, "w %lld %d %d %d %d %d %d %d %d %d %d %lld %lld %d\n", k.M, k.H, k.W, k.C, k.Cout, k.R, k.S, k.stride,
+            k.pad, k.dense, k.K, k.ldd, k.ldx, kv.second);
+  }
+  fclose(f);
+  return 0;
+}
+
+// returns the number of entries loaded (existing entries are overwritten)
+extern "C" int artsbir_tune_load(const char* path) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  FILE* f = fopen(path, "r");
+  if (!f) { set_error("tune_load: cannot open %s", path); return -1; }
+  int n = 0;
+  char tag[4];
+  while (fscanf(f, "%3s", tag) == 1) {
+    int choice;
+    if (tag[0] == 'c') {
+      ConvKey k;
+      if (fscanf(f, "%lld %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d", &k.M, &k.H, &k.W, &k.C, &k.Cout, &k.R, &k.S,
+                 &k.stride, &k.pad, &k.Ho, &k.Wo, &k.res_mode, &k.stats, &k.nseg, &k.bnb, &choice) != 16)
+        break;
+      g_conv_choice[k] = choice;
+    } else if (tag[0] == 'w') {
+      WgKey k;
+      if (fscanf(f, "%lld %d %d %d %d %d %d %d %d %d %d %lld %lld %d", &k.M, &k.H, &k.W, &k.C, &k.Cout, &k.R, &k.S,
+                 &k.stride, &k.pad, &k.dense, &k.K, &k.ldd, &k.ldx, &choice) != 14)
+        break;
+      g_wg_choice[k] = choice;
+    } else {
+      break;
+    }
+    ++n;
+  }
+  fclose(f);
+  return n;
 }
 
 extern "C" int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void* dy, long long ldd,

@@ -26,14 +26,13 @@ struct PgArgs {
   // fused BatchNorm-backward reduction (data gradient only, no stats): the
   // output d is the gradient at a BN(+ReLU) output; g = d * mask is stored and
   // sum g, sum g * xhat_t are added to bnb_slots[t] ([nseg][NSLOT][2][Cout])
-  int bnb;                // 0 off; 1: mask y_0 * msc + msh > 0; 2: mask bnb_mask > 0;
+  int bnb;                // 0 off; 1: mask (y_0 - mean) * scale + beta > 0; 2: mask bnb_mask > 0;
                           // 3: bnb_mask holds one bit per channel ([M][Cout/8] bytes)
   int bnb_nt;             // BN inputs sharing g (1 or 2)
   const void* bnb_y[2];   // bf16 [M][ldy] BN inputs (pre-BN convolution outputs)
   const float* bnb_mean[2];
   const float* bnb_istd[2];
-  const float* bnb_msc;   // bnb 1: scale / shift of the BN before the ReLU
-  const float* bnb_msh;
+  const float* bnb_mbn;   // bnb 1: parameter block [4][Cout] (mean, istd, scale, beta) of the BN before the ReLU
   const void* bnb_mask;   // bnb 2: the ReLU output (block output)
   float* bnb_slots[2];
   long long bnb_pstride;  // floats between the per-channel parameters of consecutive segments

@@ -214,7 +214,7 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
     // a batch go out together and are waited for once, not one round trip each
     const int chc = chok ? ch0 : 0;
     // BN-backward per-channel constants: xhat_t = y * xa_t + xb_t; mask affine
-    float xa0[8], xb0[8], xa1[8], xb1[8], ms[8], mh[8];
+    float xa0[8], xb0[8], xa1[8], xb1[8], mm[8], ms[8], mh[8];
     if constexpr (BNB) {
       const long long po = wseg * a.bnb_pstride + chc;
       float m0[8], m1[8];
@@ -227,12 +227,13 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
 #pragma unroll
         for (int e = 0; e < 8; ++e) { xa1[e] = 0.f; m1[e] = 0.f; }
       }
-      if (a.bnb == 1) {
-        loadf8v(a.bnb_msc + po, ms);
-        loadf8v(a.bnb_msh + po, mh);
+      if (a.bnb == 1) {  // parameter block of the BN feeding the ReLU: mean, -, scale, beta
+        loadf8v(a.bnb_mbn + po, mm);
+        loadf8v(a.bnb_mbn + po + 2 * a.Cout, ms);
+        loadf8v(a.bnb_mbn + po + 3 * a.Cout, mh);
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { ms[e] = 0.f; mh[e] = 0.f; }
+        for (int e = 0; e < 8; ++e) { mm[e] = 0.f; ms[e] = 0.f; mh[e] = 0.f; }
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) { xb0[e] = -m0[e] * xa0[e]; xb1[e] = -m1[e] * xa1[e]; }
@@ -288,7 +289,7 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float yv = to_f(y0v[u].v[e]);
-              const bool keep = a.bnb == 1   ? yv * ms[e] + mh[e] > 0.f
+              const bool keep = a.bnb == 1   ? (yv - mm[e]) * ms[e] + mh[e] > 0.f
                                 : a.bnb == 3 ? ((mbits[u] >> e) & 1u) != 0u
                                              : to_f(mkv[u].v[e]) > 0.f;
               v[e] = keep ? v[e] : 0.f;
@@ -927,7 +928,7 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
   static_assert(NTP * NWC == TR * TCB, "pixel tiles per wave");
   static_assert(Gm::LDS <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
-  float* prm = reinterpret_cast<float*>(smem + WB + 2 * HB);  // [seg][istd, mean, msc, msh][COUT]
+  float* prm = reinterpret_cast<float*>(smem + WB + 2 * HB);  // [seg][istd, mean, mask scale, mask beta][COUT]
   float* red = reinterpret_cast<float*>(smem + WB + 2 * HB + Gm::PRM);
   int* red_cnt = reinterpret_cast<int*>(smem + WB + 2 * HB + Gm::PRM + 6 * COUT * 4);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -967,7 +968,8 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
       const int nsg = a.seg_m > 0 ? (int)(a.M / a.seg_m) : 1;
       for (int i = tid; i < nsg * 4 * COUT; i += 64 * NWC) {
         const int sg = i / (4 * COUT), r = (i / COUT) & 3, ch = i % COUT;
-        const float* src = r == 0 ? a.bnb_istd[0] : r == 1 ? a.bnb_mean[0] : r == 2 ? a.bnb_msc : a.bnb_msh;
+        const float* src = r == 0 ? a.bnb_istd[0] : r == 1 ? a.bnb_mean[0]
+                         : r == 2 ? a.bnb_mbn + 2 * a.Cout : a.bnb_mbn + 3 * a.Cout;
         prm[i] = src[sg * a.bnb_pstride + ch];
       }
     }
@@ -1085,7 +1087,7 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float yv = to_f(yp[p][j].v[e]);
-              v[e] = yv * ms[e] + mh[e] > 0.f ? v[e] : 0.f;
+              v[e] = (yv - xm[e]) * ms[e] + mh[e] > 0.f ? v[e] : 0.f;  // kind 1: target 0 is the ReLU's BN
               s1[e] += v[e];
               s2[e] += v[e] * ((yv - xm[e]) * xa[e]);
             }

@@ -30,6 +30,9 @@
 // adds < 2^-13 |q||g| for D <= 4096.  Hence |err(d^2)| <= rel |q| |g|max + 1e-3
 // with rel = 2^-6 + 2^-12 (bf16) or 2^-14 (exact-f32 MFMA); every decision
 // that could depend on the approximation is re-made in f64.
+#include <utility>
+#include <vector>
+
 #include "common.h"
 #include "../../include/artsbir.h"
 
@@ -66,17 +69,29 @@ template <> struct RM<float> {
 };
 
 // ---------------------------------------------------------------- helpers
-// squared norm of each f32 row, and the compute-dtype copy of the row
+// squared norm of each f32 row, and the compute-dtype copy of the row.
+// normalize (cosine metric): the row is first scaled by 1/max(|x|, 1e-8) (|x| in
+// f64), so the L2 scan of the unit rows orders by 1 - cos (|a-b|^2 = 2 - 2 cos)
+__device__ __forceinline__ float row_scale(const float* r, int D, int lane, int normalize) {
+  if (!normalize) return 1.f;
+  double s = 0.0;
+  for (int d = lane; d < D; d += 64) s += (double)r[d] * (double)r[d];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  return (float)(1.0 / fmax(sqrt(s), 1e-8));
+}
+
 template <typename T>
 __global__ void rows_prep_kernel(const float* __restrict__ x, int n, int D, float* __restrict__ sq, T* __restrict__ xc,
-                                 int ldc) {
+                                 int ldc, int normalize) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (row >= n) return;
   const float* r = x + (long long)row * D;
+  const float sc = row_scale(r, D, lane, normalize);
   float s = 0.f;
   for (int d = lane; d < ldc; d += 64) {  // the compute copy is zero-padded to ldc columns
-    const float v = d < D ? r[d] : 0.f;
+    const float v = d < D ? r[d] * sc : 0.f;
     s += v * v;
     if (xc) xc[(long long)row * ldc + d] = from_f<T>(v);
   }
@@ -96,29 +111,66 @@ __device__ __forceinline__ double exact_l2(const float* q, const float* g, int D
   return sqrt(s);
 }
 
+// Exact ordering key of (q, g) in f64 (one wave; all lanes return it):
+//   metric 0  ||q - g + 1e-6||                                 nn.PairwiseDistance(p=2, eps=1e-6), utils.py:42
+//   metric 1  1 - q.g / (max(|q|, 1e-8) max(|g|, 1e-8))        cosine_distance, utils.py:31-40
+//             (nn.CosineSimilarity(dim=1, eps=1e-8): each norm clamped separately)
+__device__ __forceinline__ double exact_key(const float* q, const float* g, int D, int lane, int metric) {
+  if (metric == 0) return exact_l2(q, g, D, lane);
+  double dot = 0.0, qq = 0.0, gg = 0.0;
+  for (int d = lane; d < D; d += 64) {
+    const double a = q[d], b = g[d];
+    dot += a * b;
+    qq += a * a;
+    gg += b * b;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dot += __shfl_xor(dot, o, 64);
+    qq += __shfl_xor(qq, o, 64);
+    gg += __shfl_xor(gg, o, 64);
+  }
+  return 1.0 - dot / (fmax(sqrt(qq), 1e-8) * fmax(sqrt(gg), 1e-8));
+}
+
+// the scan-domain squared distance of an exact key: d^2 itself for L2; for the
+// cosine metric the scan runs on unit rows where d^2 = 2 key (the deviation of
+// the f32 unit rows' norms from 1 is folded into the per-query eps, knn_qeps)
+__device__ __forceinline__ double key_d2(double key, int metric) { return metric ? 2.0 * key : key * key; }
+
+// per-query bound of |approx d^2 - scan-domain exact d^2|: rel |q| max|g| + 1e-3,
+// plus for the cosine metric 2 (|1 - |q|^2| + max(gmax - 1, 1 - gmin)), the room
+// between 2 key and |q^|^2 + |g^|^2 - 2 q^.g^ of the normalised f32 rows
+__device__ __forceinline__ double query_eps(float qsq, float gmax, float gmin, float rel, int metric) {
+  double e = rel * sqrt((double)qsq * gmax) + 1e-3;
+  if (metric) e += 2.0 * (fabs(1.0 - (double)qsq) + fmax((double)gmax - 1.0, 1.0 - (double)gmin));
+  return e;
+}
+
 // d_pos^2 (exact, f64) and the uncertainty band of every query
 __global__ void knn_band_kernel(const float* __restrict__ q, const float* __restrict__ g, const long long* __restrict__ pos,
                                 long long g_base, long long n_g, const float* __restrict__ qsq, float gsq_max, int nq, int D,
-                                float rel, double* __restrict__ dpos, float* __restrict__ lo, float* __restrict__ hi) {
+                                float rel, double* __restrict__ dpos, float* __restrict__ lo, float* __restrict__ hi,
+                                int metric, const float* __restrict__ qeps) {
   const int lane = threadIdx.x & 63;
   const int qi = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (qi >= nq) return;
   const long long p = pos[qi];
-  const double eps = rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
+  const double eps = qeps ? (double)qeps[qi] : rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
   if (p < g_base || p >= g_base + n_g) {
     // positive not in this shard: the caller provides dpos from its owner
     if (lane == 0) {
       const double d = dpos[qi];
-      lo[qi] = d >= 0 ? (float)(d * d - eps) : -1.f;
-      hi[qi] = d >= 0 ? (float)(d * d + eps) : -1.f;
+      lo[qi] = d >= 0 ? (float)(key_d2(d, metric) - eps) : -1.f;
+      hi[qi] = d >= 0 ? (float)(key_d2(d, metric) + eps) : -1.f;
     }
     return;
   }
-  const double d = exact_l2(q + (long long)qi * D, g + (p - g_base) * D, D, lane);
+  const double d = exact_key(q + (long long)qi * D, g + (p - g_base) * D, D, lane, metric);
   if (lane == 0) {
     dpos[qi] = d;
-    lo[qi] = (float)(d * d - eps);
-    hi[qi] = (float)(d * d + eps);
+    lo[qi] = (float)(key_d2(d, metric) - eps);
+    hi[qi] = (float)(key_d2(d, metric) + eps);
   }
 }
 
@@ -139,6 +191,7 @@ struct KnnScanArgs {
   const float* qsq;
   const float* gsq;
   float gsq_max;  // knn_scan_v2: max |g|^2 (prefilter slack)
+  const float* gsq_max_p;  // knn_scan_v2: if set, max |g|^2 read from device memory (one-call path, no host sync)
   const float* thr0;  // knn_scan_v2: optional per-query initial list threshold (see knn.py)
   unsigned* kb;       // knn_scan_v2: optional [Nq] shared k-th bound (kb_enc of an approx d2), atomicMin
   int kq;             //   k of the final top-k (1..KT)
@@ -492,7 +545,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
     const int q = qb + tid;
     const bool ok = q < a.Nq;
     float t0 = (ok && a.thr0) ? a.thr0[q] : INFINITY;
-    if (ok && a.kb) t0 = fminf(t0, kb_bound(a.kb[q], a.rel * sqrtf(a.qsq[q] * a.gsq_max) * 1.001f + 1e-3f));
+    if (ok && a.kb) t0 = fminf(t0, kb_bound(a.kb[q], a.rel * sqrtf(a.qsq[q] * (a.gsq_max_p ? *a.gsq_max_p : a.gsq_max)) * 1.001f + 1e-3f));
     s_thr[tid] = ok ? t0 : -INFINITY;
     s_lo[tid] = (band_lo && ok) ? band_lo[q] : -1.f;
     s_hi[tid] = (band_lo && ok) ? band_hi[q] : -1.f;
@@ -525,7 +578,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
   // prefilter: t = |g|^2 - 2 q.g <= crit - |q|^2 + slack, a superset of
   // d2 = (|q|^2 + |g|^2) - 2 q.g <= crit whatever the rounding of either form
   // (every magnitude is <= 2 (|q|^2 + gsq_max), each rounding <= 2^-24 of it)
-  const float gmax = a.gsq_max;
+  const float gmax = a.gsq_max_p ? *a.gsq_max_p : a.gsq_max;
   float critp[16];
   auto load_crit = [&]() {
 #pragma unroll
@@ -659,7 +712,8 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
       if (__builtin_amdgcn_ballot_w64(changed)) {
         // refresh the prefilter bounds from the owner lanes' registers (readlane:
         // no fence, no LDS round trip); the same value load_crit() would read
-        const float mine = (fmaxf(thr, hi) - qs) + 0x1p-18f * (qs + gmax);
+        // (padding rows q >= Nq keep -INF, as load_crit() reads them)
+        const float mine = q_own < a.Nq ? (fmaxf(thr, hi) - qs) + 0x1p-18f * (qs + gmax) : -INFINITY;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int r0 = (e & 3) + 8 * (e >> 2);
@@ -708,16 +762,18 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
 }
 
 // augmented bf16 rows for knn_scan_v2: [n][Dp + 8], columns Dp..Dp+1 = f32 |x|^2
+// (normalize: unit rows for the cosine metric, as rows_prep_kernel)
 __global__ void rows_prep_aug_kernel(const float* __restrict__ x, int n, int D, int Dp, float* __restrict__ sq,
-                                     bf16* __restrict__ xa) {
+                                     bf16* __restrict__ xa, int normalize) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
   if (row >= n) return;
   const float* r = x + (long long)row * D;
+  const float sc = row_scale(r, D, lane, normalize);
   bf16* o = xa + (long long)row * (Dp + 8);
   float s = 0.f;
   for (int d = lane; d < Dp; d += 64) {
-    const float v = d < D ? r[d] : 0.f;
+    const float v = d < D ? r[d] * sc : 0.f;
     s += v * v;
     o[d] = (bf16)v;
   }
@@ -740,7 +796,8 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
                                                         const int* __restrict__ cand_i, const float* __restrict__ qsq,
                                                         float gsq_max, float rel, long long g_base, int k,
                                                         long long* __restrict__ out_i, double* __restrict__ out_d,
-                                                        int* __restrict__ flag) {
+                                                        int* __restrict__ flag, int metric,
+                                                        const float* __restrict__ qeps, long long n_g) {
   extern __shared__ char sm[];
   const int nc = nchunks * KT;
   double* ed = reinterpret_cast<double*>(sm);           // [nc]
@@ -750,7 +807,7 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
   const float* qr = q + (long long)qi * D;
   const float* cd = cand_d + (long long)qi * nc;
   const int* ci = cand_i + (long long)qi * nc;
-  const double eps = rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
+  const double eps = qeps ? (double)qeps[qi] : rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
   __shared__ double rd[4];
   __shared__ int ri[4], rslot[4];
   // (1) a_k = k-th smallest approximate value: the k items with approx <= a_k have
@@ -789,7 +846,7 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
     const int gi = ci[c];
     double d = INFINITY;
     const bool live = gi >= 0 && (double)cd[c] <= cut;
-    if (live) d = exact_l2(qr, g + (long long)gi * D, D, lane);
+    if (live) d = exact_key(qr, g + (long long)gi * D, D, lane, metric);
     if (lane == 0) { ed[c] = d; ei[c] = live ? gi : -1; }
   }
   __syncthreads();
@@ -827,12 +884,16 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
   }
   // verification: a full chunk list whose last approximate value is within the
   // error band of the k-th exact distance may have dropped a true top-k item
+  // (also when the chunk lists hold fewer than min(k, n_g) items at all)
   if (threadIdx.x == 0) {
     int bad = 0;
+    long long valid = 0;
     for (int c = 0; c < nchunks; ++c) {
       const float last = cd[c * KT + KT - 1];
-      if (ci[c * KT + KT - 1] >= 0 && (double)last - eps <= kth * kth) bad = 1;
+      if (ci[c * KT + KT - 1] >= 0 && (double)last - eps <= key_d2(kth, metric)) bad = 1;
+      for (int i = 0; i < KT; ++i) valid += ci[c * KT + i] >= 0;
     }
+    if (n_g > 0 && valid < (n_g < k ? n_g : (long long)k)) bad = 1;
     flag[qi] = bad;
   }
 }
@@ -840,12 +901,13 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
 // exact checks of the uncertain items of the rank count
 __global__ void knn_uncertain_kernel(const float* __restrict__ q, const float* __restrict__ g, int D,
                                      const int* __restrict__ unc, int unc_cap, const double* __restrict__ dpos,
-                                     const long long* __restrict__ pos, long long g_base, int* __restrict__ cnt) {
+                                     const long long* __restrict__ pos, long long g_base, int* __restrict__ cnt,
+                                     int metric) {
   const int lane = threadIdx.x & 63;
   const int n = min(unc[2 * unc_cap], unc_cap);
   for (int e = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); e < n; e += gridDim.x * (blockDim.x / 64)) {
     const int qi = unc[2 * e], gi = unc[2 * e + 1];
-    const double d = exact_l2(q + (long long)qi * D, g + (long long)gi * D, D, lane);
+    const double d = exact_key(q + (long long)qi * D, g + (long long)gi * D, D, lane, metric);
     const double dp = dpos[qi];
     const long long ggi = g_base + gi;
     if (lane == 0 && (d < dp || (d == dp && ggi < pos[qi]))) atomicAdd(cnt + qi, 1);
@@ -855,10 +917,10 @@ __global__ void knn_uncertain_kernel(const float* __restrict__ q, const float* _
 // exhaustive exact scan of one query (fallback for flagged queries, and the
 // small-gallery path): writes all exact distances
 __global__ void knn_exact_all_kernel(const float* __restrict__ q, const float* __restrict__ g, int D, int n,
-                                     double* __restrict__ out) {
+                                     double* __restrict__ out, int metric) {
   const int lane = threadIdx.x & 63;
   for (int i = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += gridDim.x * (blockDim.x / 64)) {
-    const double d = exact_l2(q, g + (long long)i * D, D, lane);
+    const double d = exact_key(q, g + (long long)i * D, D, lane, metric);
     if (lane == 0) out[i] = d;
   }
 }
@@ -883,6 +945,198 @@ __global__ void pairwise_l2_kernel(const float* __restrict__ x1, long long n1, c
   }
 }
 
+// ------------------------------------------- one-call top-k (no host syncs)
+// The kernels below complete artsbir_pairwise_l2_topk: every decision the
+// multi-call protocol made on the host (max |g|^2, the uncertain-queue overflow,
+// flagged queries) is made on the device.
+
+// min and max of |g|^2 over the gallery into ext[0] (max), ext[1] (min) as f32
+// bit patterns (non-negative floats order like their bits); ext preset to (0, +INF)
+__global__ void sq_minmax_kernel(const float* __restrict__ sq, long long n, unsigned* __restrict__ ext) {
+  float mx = 0.f, mn = INFINITY;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    mx = fmaxf(mx, sq[i]);
+    mn = fminf(mn, sq[i]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    mn = fminf(mn, __shfl_xor(mn, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(ext, __float_as_uint(mx));
+    atomicMin(ext + 1, __float_as_uint(mn));
+  }
+}
+
+// per-query eps (query_eps) and the initial dpos (caller's value for shard
+// calls, else -1); cnt and the uncertain-queue length start at 0
+__global__ void knn_init_kernel(const float* __restrict__ qsq, const unsigned* __restrict__ ext, int nq, float rel,
+                                int metric, const double* __restrict__ dpos_in, float* __restrict__ qeps,
+                                double* __restrict__ dpos, int* __restrict__ cnt, int* __restrict__ unc_n) {
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi == 0) *unc_n = 0;
+  if (qi >= nq) return;
+  const float gmax = __uint_as_float(ext[0]), gmin = __uint_as_float(ext[1]);
+  qeps[qi] = (float)(query_eps(qsq[qi], gmax, gmin, rel, metric) * (1.0 + 1e-6));
+  dpos[qi] = dpos_in ? dpos_in[qi] : -1.0;
+  cnt[qi] = 0;
+}
+
+// uncertain-queue overflow (more uncertain items than unc_cap): recount every
+// query's rank exhaustively in f64.  Both kernels return at once otherwise.
+__global__ void knn_count_reset_kernel(const int* __restrict__ unc_n, int unc_cap, int nq, int* __restrict__ cnt) {
+  if (*unc_n <= unc_cap) return;
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi < nq) cnt[qi] = 0;
+}
+
+__global__ void __launch_bounds__(256) knn_count_exhaustive_kernel(const float* __restrict__ q,
+                                                                   const float* __restrict__ g, int D, long long n,
+                                                                   const int* __restrict__ unc_n, int unc_cap,
+                                                                   const double* __restrict__ dpos,
+                                                                   const long long* __restrict__ pos,
+                                                                   long long g_base, int* __restrict__ cnt,
+                                                                   int metric) {
+  if (*unc_n <= unc_cap) return;
+  const int qi = blockIdx.y;
+  const double dp = dpos[qi];
+  if (dp < 0) return;
+  const int lane = threadIdx.x & 63;
+  const long long W = (long long)gridDim.x * (blockDim.x / 64);
+  const long long w = blockIdx.x * (long long)(blockDim.x / 64) + (threadIdx.x >> 6);
+  const long long p = pos[qi];
+  int c = 0;
+  for (long long r = w; r < n; r += W) {
+    const double d = exact_key(q + (long long)qi * D, g + r * D, D, lane, metric);
+    c += (d < dp || (d == dp && g_base + r < p)) ? 1 : 0;
+  }
+  if (lane == 0 && c) atomicAdd(cnt + qi, c);
+}
+
+// exhaustive exact top-k of the flagged queries (a chunk list could have hidden
+// a true top-k item, or the gallery is too small for the lists): every wave
+// keeps a sorted (key, index) list of the k best rows it sees, lane i holding
+// entry i (k <= 64), inserted by ballot + shuffle; lists to part[q][W][k]
+constexpr int KNN_XB = 8;  // workgroups (x 4 waves) per flagged query
+
+__global__ void __launch_bounds__(256) knn_exact_topk_part_kernel(const float* __restrict__ q,
+                                                                  const float* __restrict__ g, int D, long long n,
+                                                                  int k, int metric, const int* __restrict__ flag,
+                                                                  double* __restrict__ pkey,
+                                                                  long long* __restrict__ pidx) {
+  const int qi = blockIdx.y;
+  if (!flag[qi]) return;
+  const int lane = threadIdx.x & 63;
+  const int W = gridDim.x * 4;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  double lk = INFINITY;
+  long long li = 0x7fffffffffffffffLL;
+  for (long long r = w; r < n; r += W) {
+    const double key = exact_key(q + (long long)qi * D, g + r * D, D, lane, metric);
+    const double kk = __shfl(lk, k - 1, 64);
+    const long long ki = __shfl(li, k - 1, 64);
+    if (key < kk || (key == kk && r < ki)) {  // wave-uniform
+      const bool before = lane < k && (lk < key || (lk == key && li < r));
+      const int at = __popcll(__builtin_amdgcn_ballot_w64(before));
+      const double uk = __shfl_up(lk, 1, 64);
+      const long long ui = __shfl_up(li, 1, 64);
+      if (lane == at) {
+        lk = key;
+        li = r;
+      } else if (lane > at && lane < k) {
+        lk = uk;
+        li = ui;
+      }
+    }
+  }
+  if (lane < k) {
+    const long long o = ((long long)qi * W + w) * k + lane;
+    pkey[o] = lk;
+    pidx[o] = li == 0x7fffffffffffffffLL ? -1 : li;
+  }
+}
+
+// k smallest (key, index) of nl lists of k entries (index -1 = empty) -> out;
+// one workgroup per row of lists; rows with flag == 0 are left alone (flag ==
+// nullptr: every row).  Shared by the flagged-query fallback and
+// artsbir_topk_merge (per-shard top-k lists of a sharded gallery).
+// Entry j of list l of row qi is at qi * s_row + l * s_list + j.
+__global__ void __launch_bounds__(256) topk_lists_merge_kernel(const double* __restrict__ key,
+                                                               const long long* __restrict__ idx, int nl, int k,
+                                                               long long s_row, long long s_list,
+                                                               const int* __restrict__ flag, long long idx_base,
+                                                               long long* __restrict__ out_i,
+                                                               double* __restrict__ out_d) {
+  const int qi = blockIdx.x;
+  if (flag && !flag[qi]) return;
+  extern __shared__ char sm[];
+  unsigned char* used = reinterpret_cast<unsigned char*>(sm);
+  const int nc = nl * k;
+  const double* kr = key + (long long)qi * s_row;
+  const long long* ir = idx + (long long)qi * s_row;
+  auto at = [&](int c) { return (long long)(c / k) * s_list + (c % k); };
+  for (int c = threadIdx.x; c < nc; c += blockDim.x) used[c] = ir[at(c)] < 0 ? 1 : 0;
+  __syncthreads();
+  __shared__ double rd[4];
+  __shared__ long long ri[4];
+  __shared__ int rs[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int r = 0; r < k; ++r) {
+    double bd = INFINITY;
+    long long bi = 0x7fffffffffffffffLL;
+    int bs = -1;
+    for (int c = threadIdx.x; c < nc; c += blockDim.x) {
+      if (used[c]) continue;
+      const double d = kr[at(c)];
+      const long long i = ir[at(c)];
+      if (bs < 0 || d < bd || (d == bd && i < bi)) { bd = d; bi = i; bs = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, 64);
+      const long long oi = __shfl_xor(bi, o, 64);
+      const int os = __shfl_xor(bs, o, 64);
+      if (os >= 0 && (bs < 0 || od < bd || (od == bd && oi < bi))) { bd = od; bi = oi; bs = os; }
+    }
+    if (lane == 0) { rd[wid] = bd; ri[wid] = bi; rs[wid] = bs; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double b = rd[0];
+      long long bi2 = ri[0];
+      int bs2 = rs[0];
+      for (int w = 1; w < (int)blockDim.x / 64; ++w)
+        if (rs[w] >= 0 && (bs2 < 0 || rd[w] < b || (rd[w] == b && ri[w] < bi2))) { b = rd[w]; bi2 = ri[w]; bs2 = rs[w]; }
+      out_i[(long long)qi * k + r] = bs2 >= 0 ? idx_base + bi2 : -1;
+      out_d[(long long)qi * k + r] = bs2 >= 0 ? b : INFINITY;
+      if (bs2 >= 0) used[bs2] = 1;
+    }
+    __syncthreads();
+  }
+}
+
+// exact key of every query's positive when it lies in this shard's rows
+// [g_base, g_base + n), else -1 (one wave per query)
+__global__ void positive_key_kernel(const float* __restrict__ q, const float* __restrict__ g, int D, int nq,
+                                    const long long* __restrict__ pos, long long g_base, long long n, int metric,
+                                    double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int qi = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (qi >= nq) return;
+  const long long p = pos[qi];
+  if (p < g_base || p >= g_base + n) {
+    if (lane == 0) out[qi] = -1.0;
+    return;
+  }
+  const double d = exact_key(q + (long long)qi * D, g + (p - g_base) * D, D, lane, metric);
+  if (lane == 0) out[qi] = d;
+}
+
+__global__ void rank_out_kernel(const int* __restrict__ cnt, int nq, long long* __restrict__ out) {
+  const int qi = blockIdx.x * blockDim.x + threadIdx.x;
+  if (qi < nq) out[qi] = cnt[qi];
+}
+
 }  // namespace artsbir
 
 using namespace artsbir;
@@ -904,9 +1158,9 @@ extern "C" int artsbir_rows_prep(int dtype, const float* x, int n, int D, float*
   if (n <= 0) return 0;
   if (ldc < D) ldc = D;
   if (dtype == ARTSBIR_DT_BF16)
-    hipLaunchKernelGGL(rows_prep_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, D, sq, (bf16*)xc, ldc);
+    hipLaunchKernelGGL(rows_prep_kernel<bf16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, D, sq, (bf16*)xc, ldc, 0);
   else
-    hipLaunchKernelGGL(rows_prep_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, D, sq, (float*)xc, ldc);
+    hipLaunchKernelGGL(rows_prep_kernel<float>, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, n, D, sq, (float*)xc, ldc, 0);
   ARTSBIR_CHECK_LAUNCH("rows_prep");
   return 0;
 }
@@ -916,7 +1170,7 @@ extern "C" int artsbir_knn_band(const float* q, const float* g, const long long*
                                 float* hi, void* stream) {
   if (nq <= 0) return 0;
   hipLaunchKernelGGL(knn_band_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, (hipStream_t)stream, q, g, pos, g_base,
-                     n_g, qsq, gsq_max, nq, D, rel, dpos, lo, hi);
+                     n_g, qsq, gsq_max, nq, D, rel, dpos, lo, hi, 0, nullptr);
   ARTSBIR_CHECK_LAUNCH("knn_band");
   return 0;
 }
@@ -943,7 +1197,7 @@ extern "C" int artsbir_knn_scan(int dtype, const void* qc, const void* gc, const
   if (D % (8 * EPC)) { set_error("knn_scan: D=%d must be a multiple of %d", D, 8 * EPC); return -1; }
   if (nq <= 0 || ng <= 0) return 0;
   KnnScanArgs a;
-  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.thr0 = nullptr; a.kb = nullptr; a.kq = 0; a.rel = 0.f; a.Nq = nq; a.Ng = ng; a.D = D;
+  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.gsq_max_p = nullptr; a.thr0 = nullptr; a.kb = nullptr; a.kq = 0; a.rel = 0.f; a.Nq = nq; a.Ng = ng; a.D = D;
   a.tiles_per_chunk = tiles_per_chunk;
   const int tiles = (ng + 127) / 128;
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
@@ -965,7 +1219,7 @@ extern "C" int artsbir_knn_merge(const float* q, const float* g, int D, int nq, 
   const size_t sh = (size_t)nchunks * KT * (sizeof(double) + sizeof(int));
   if (sh > 60000) { set_error("knn_merge: too many candidates (%d chunks)", nchunks); return -1; }
   hipLaunchKernelGGL(knn_merge_kernel, dim3(nq), dim3(256), sh, (hipStream_t)stream, q, g, D, nchunks, cand_d, cand_i,
-                     qsq, gsq_max, rel, g_base, k, out_i, out_d, flag);
+                     qsq, gsq_max, rel, g_base, k, out_i, out_d, flag, 0, nullptr, 0LL);
   ARTSBIR_CHECK_LAUNCH("knn_merge");
   return 0;
 }
@@ -973,7 +1227,7 @@ extern "C" int artsbir_knn_merge(const float* q, const float* g, int D, int nq, 
 extern "C" int artsbir_knn_uncertain(const float* q, const float* g, int D, const int* unc, int unc_cap,
                                      const double* dpos, const long long* pos, long long g_base, int* cnt, void* stream) {
   hipLaunchKernelGGL(knn_uncertain_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, q, g, D, unc, unc_cap, dpos,
-                     pos, g_base, cnt);
+                     pos, g_base, cnt, 0);
   ARTSBIR_CHECK_LAUNCH("knn_uncertain");
   return 0;
 }
@@ -982,7 +1236,7 @@ extern "C" int artsbir_knn_exact_all(const float* q, const float* g, int D, int 
   if (n <= 0) return 0;
   unsigned grid = (unsigned)((n + 3) / 4);
   if (grid > 65536) grid = 65536;
-  hipLaunchKernelGGL(knn_exact_all_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, q, g, D, n, out);
+  hipLaunchKernelGGL(knn_exact_all_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, q, g, D, n, out, 0);
   ARTSBIR_CHECK_LAUNCH("knn_exact_all");
   return 0;
 }
@@ -991,7 +1245,7 @@ extern "C" int artsbir_rows_prep_aug(const float* x, int n, int D, int Dp, float
   if (Dp < D || Dp % 16) { set_error("rows_prep_aug: Dp=%d must be >= D=%d and a multiple of 16", Dp, D); return -1; }
   if (n <= 0) return 0;
   hipLaunchKernelGGL(rows_prep_aug_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, n, D, Dp,
-                     sq, (bf16*)xa);
+                     sq, (bf16*)xa, 0);
   ARTSBIR_CHECK_LAUNCH("rows_prep_aug");
   return 0;
 }
@@ -1010,7 +1264,7 @@ extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float*
   if (kbound && (k < 1 || k > KT)) { set_error("knn_scan_aug: k=%d must be in 1..%d with a shared bound", k, KT); return -1; }
   if (nq <= 0 || ng <= 0) return 0;
   KnnScanArgs a;
-  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.thr0 = thr0; a.kb = kbound; a.kq = k; a.rel = rel; a.Nq = nq; a.Ng = ng; a.D = Dp;
+  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.gsq_max_p = nullptr; a.thr0 = thr0; a.kb = kbound; a.kq = k; a.rel = rel; a.Nq = nq; a.Ng = ng; a.D = Dp;
   a.tiles_per_chunk = tiles_per_chunk;
   const int tiles = (ng + 127) / 128;
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
@@ -1025,4 +1279,260 @@ extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float*
   }
   ARTSBIR_CHECK_LAUNCH("knn_scan_aug");
   return 0;
+}
+
+// ---------------------------------------------------------------------------
+// One-call exact top-k + rank of the positive (the drop-in for the per-query
+// loop of inference.py:30-69: utils.euclidean_distance / cosine_distance of
+// [1,D] vs [N,D], topk(N) -> position of the positive, topk(k)).  Launch
+// sequence (all on `stream`, no host synchronisation):
+//   rows_prep(q), rows_prep_aug(g) [unit rows for cosine] -> min/max |g|^2 ->
+//   per-query eps + dpos init -> band (exact key of the positive) -> MFMA scan
+//   -> exact merge -> uncertain checks -> overflow recount -> exhaustive top-k
+//   of flagged queries -> ranks.
+namespace {
+// optional HIP-event timing of the scan kernel inside artsbir_pairwise_l2_topk
+// (bench.py prices the scan against the MFMA roof with it)
+int g_scan_prof = 0;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_scan_ev;
+
+struct TopkPlan {
+  int dtype, v2, Dp, tpc, nchunks, ncand, unc_cap;
+  size_t off[20];
+  size_t total;
+};
+constexpr int TOPK_KMAX = 64;
+int g_topk_unc_cap = 1 << 20;  // artsbir_knn_set_unc_cap (tests force the overflow path)
+
+enum { W_QSQ, W_GSQ, W_EXT, W_QEPS, W_QC, W_GC, W_LO, W_HI, W_DPOS, W_CNT, W_UNC, W_CD, W_CI, W_FLAG, W_PK, W_PI, W_END };
+
+int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan& p) {
+  if (Q < 0 || N < 1 || D < 1 || k < 1 || k > TOPK_KMAX || N > 0x7fffffffLL) {
+    set_error("pairwise_l2_topk: need Q >= 0, 1 <= N < 2^31, D >= 1, 1 <= k <= %d (Q=%d N=%lld D=%d k=%d)", TOPK_KMAX,
+              Q, N, D, k);
+    return -1;
+  }
+  if (dtype != ARTSBIR_DT_BF16 && dtype != ARTSBIR_DT_F32) { set_error("pairwise_l2_topk: dtype %d", dtype); return -1; }
+  p.dtype = dtype;
+  const int step = dtype == ARTSBIR_DT_BF16 ? 64 : 32;
+  p.Dp = (D + step - 1) / step * step;
+  p.v2 = dtype == ARTSBIR_DT_BF16 && artsbir_knn_scan_aug_supported(p.Dp);
+  const long long tiles = (N + 127) / 128;
+  long long tpc = tpc_req > 0 ? tpc_req : (p.v2 ? 256 : 64);
+  const long long need = (k + KT - 1) / KT;           // chunks whose lists can hold k items
+  if (tiles / need < tpc) tpc = tiles / need > 0 ? tiles / need : 1;
+  const long long maxch = 60000 / (KT * 12);          // knn_merge's shared memory
+  if ((tiles + tpc - 1) / tpc > maxch) tpc = (tiles + maxch - 1) / maxch;
+  p.tpc = (int)tpc;
+  p.nchunks = (int)((tiles + tpc - 1) / tpc);
+  p.ncand = p.nchunks * KT;
+  p.unc_cap = g_topk_unc_cap;
+  const size_t es = dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+  const size_t W = KNN_XB * 4;
+  size_t sz[W_END];
+  sz[W_QSQ] = 4 * (size_t)Q;
+  sz[W_GSQ] = 4 * (size_t)N;
+  sz[W_EXT] = 8;
+  sz[W_QEPS] = 4 * (size_t)Q;
+  sz[W_QC] = (size_t)Q * p.Dp * es;
+  sz[W_GC] = p.v2 ? (size_t)N * (p.Dp + 8) * 2 : (size_t)N * p.Dp * es;
+  sz[W_LO] = sz[W_HI] = 4 * (size_t)Q;
+  sz[W_DPOS] = 8 * (size_t)Q;
+  sz[W_CNT] = 4 * (size_t)Q;
+  sz[W_UNC] = 4 * (2 * (size_t)p.unc_cap + 1);
+  sz[W_CD] = sz[W_CI] = 4 * (size_t)Q * p.ncand;
+  sz[W_FLAG] = 4 * (size_t)Q;
+  sz[W_PK] = sz[W_PI] = 8 * (size_t)Q * W * k;
+  size_t o = 0;
+  for (int i = 0; i < W_END; ++i) {
+    p.off[i] = o;
+    o += (sz[i] + 255) / 256 * 256;
+  }
+  p.total = o;
+  return 0;
+}
+}  // namespace
+
+extern "C" long long artsbir_pairwise_l2_topk_workspace(int dtype, int Q, long long N, int D, int k,
+                                                        int tiles_per_chunk) {
+  TopkPlan p;
+  if (topk_plan(dtype, Q, N, D, k, tiles_per_chunk, p)) return -1;
+  return (long long)p.total;
+}
+
+extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, int Q, const float* g, long long N, int D,
+                                        int k, const long long* positives, const double* dpos_in, long long g_base,
+                                        int tiles_per_chunk, long long* out_idx, double* out_dist, long long* out_rank,
+                                        double* out_dpos, void* workspace, long long workspace_bytes, void* stream) {
+  if (metric != 0 && metric != 1) { set_error("pairwise_l2_topk: metric %d (0 = euclidean, 1 = cosine)", metric); return -1; }
+  TopkPlan p;
+  if (topk_plan(dtype, Q, N, D, k, tiles_per_chunk, p)) return -1;
+  if (!workspace || workspace_bytes < (long long)p.total) {
+    set_error("pairwise_l2_topk: workspace of %lld bytes < %zu needed", workspace_bytes, p.total);
+    return -1;
+  }
+  if (!q || !g || !out_idx || !out_dist) { set_error("pairwise_l2_topk: null input/output"); return -1; }
+  if (out_rank && !positives) { set_error("pairwise_l2_topk: ranks need positives"); return -1; }
+  if (Q == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  char* w = static_cast<char*>(workspace);
+  float* qsq = reinterpret_cast<float*>(w + p.off[W_QSQ]);
+  float* gsq = reinterpret_cast<float*>(w + p.off[W_GSQ]);
+  unsigned* ext = reinterpret_cast<unsigned*>(w + p.off[W_EXT]);
+  float* qeps = reinterpret_cast<float*>(w + p.off[W_QEPS]);
+  void* qc = w + p.off[W_QC];
+  void* gc = w + p.off[W_GC];
+  float* lo = reinterpret_cast<float*>(w + p.off[W_LO]);
+  float* hi = reinterpret_cast<float*>(w + p.off[W_HI]);
+  double* dpos = reinterpret_cast<double*>(w + p.off[W_DPOS]);
+  int* cnt = reinterpret_cast<int*>(w + p.off[W_CNT]);
+  int* unc = reinterpret_cast<int*>(w + p.off[W_UNC]);
+  float* cand_d = reinterpret_cast<float*>(w + p.off[W_CD]);
+  int* cand_i = reinterpret_cast<int*>(w + p.off[W_CI]);
+  int* flag = reinterpret_cast<int*>(w + p.off[W_FLAG]);
+  double* pkey = reinterpret_cast<double*>(w + p.off[W_PK]);
+  long long* pidx = reinterpret_cast<long long*>(w + p.off[W_PI]);
+  const int ng = (int)N;
+  const float rel = dtype == ARTSBIR_DT_BF16 ? (float)(0x1p-6 + 0x1p-12) : (float)0x1p-14;
+
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext), 0, 1, st) != hipSuccess ||
+      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext + 1), 0x7f800000, 1, st) != hipSuccess) {
+    set_error("pairwise_l2_topk: memset failed");
+    return -2;
+  }
+  const unsigned gq = (unsigned)((Q + 3) / 4), gg = (unsigned)((N + 3) / 4);
+  if (dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL(rows_prep_kernel<bf16>, dim3(gq), dim3(256), 0, st, q, Q, D, qsq, (bf16*)qc, p.Dp, metric);
+  else
+    hipLaunchKernelGGL(rows_prep_kernel<float>, dim3(gq), dim3(256), 0, st, q, Q, D, qsq, (float*)qc, p.Dp, metric);
+  if (p.v2)
+    hipLaunchKernelGGL(rows_prep_aug_kernel, dim3(gg), dim3(256), 0, st, g, ng, D, p.Dp, gsq, (bf16*)gc, metric);
+  else if (dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL(rows_prep_kernel<bf16>, dim3(gg), dim3(256), 0, st, g, ng, D, gsq, (bf16*)gc, p.Dp, metric);
+  else
+    hipLaunchKernelGGL(rows_prep_kernel<float>, dim3(gg), dim3(256), 0, st, g, ng, D, gsq, (float*)gc, p.Dp, metric);
+  {
+    long long b = (N + 255) / 256;
+    if (b > 1024) b = 1024;
+    hipLaunchKernelGGL(sq_minmax_kernel, dim3((unsigned)b), dim3(256), 0, st, gsq, N, ext);
+  }
+  hipLaunchKernelGGL(knn_init_kernel, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, st, qsq, ext, Q, rel, metric,
+                     dpos_in, qeps, dpos, cnt, unc + 2 * p.unc_cap);
+  if (positives)
+    hipLaunchKernelGGL(knn_band_kernel, dim3(gq), dim3(256), 0, st, q, g, positives, g_base, N, qsq, 0.f, Q, D, rel, dpos,
+                       lo, hi, metric, qeps);
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  if (g_scan_prof && hipEventCreate(&ev0) == hipSuccess && hipEventCreate(&ev1) == hipSuccess) {
+    (void)hipEventRecord(ev0, st);
+    g_scan_ev.emplace_back(ev0, ev1);
+  }
+  KnnScanArgs a;
+  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.gsq_max_p = reinterpret_cast<const float*>(ext);
+  a.thr0 = nullptr; a.kb = nullptr; a.kq = k; a.rel = rel; a.Nq = Q; a.Ng = ng; a.D = p.Dp;
+  a.tiles_per_chunk = p.tpc;
+  a.nchunks = p.nchunks;
+  a.lo = positives ? lo : nullptr; a.hi = positives ? hi : nullptr;
+  a.cnt = cnt; a.unc = unc; a.unc_cap = p.unc_cap; a.cand_d = cand_d; a.cand_i = cand_i;
+  if (p.v2) {
+    const unsigned grid = (unsigned)(p.nchunks * ((Q + 255) / 256));
+    switch (p.Dp) {
+      case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, st, a); break;
+      case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, st, a); break;
+      case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, st, a); break;
+      default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, st, a); break;
+    }
+    set_last_kernel("knn_scan_v2_kernel");
+  } else {
+    // knn_scan_kernel's chunks are tiles_per_chunk x 128 rows as well
+    const unsigned grid = (unsigned)(p.nchunks * ((Q + 127) / 128));
+    if (dtype == ARTSBIR_DT_BF16)
+      hipLaunchKernelGGL(knn_scan_kernel<bf16>, dim3(grid), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL(knn_scan_kernel<float>, dim3(grid), dim3(256), 0, st, a);
+    set_last_kernel("knn_scan_kernel");
+  }
+  ARTSBIR_CHECK_LAUNCH("pairwise_l2_topk scan");
+  if (ev1) (void)hipEventRecord(ev1, st);
+  const size_t sh = (size_t)p.ncand * (sizeof(double) + sizeof(int));
+  hipLaunchKernelGGL(knn_merge_kernel, dim3(Q), dim3(256), sh, st, q, g, D, p.nchunks, cand_d, cand_i, qsq, 0.f, rel,
+                     g_base, k, out_idx, out_dist, flag, metric, qeps, N);
+  if (positives) {
+    hipLaunchKernelGGL(knn_uncertain_kernel, dim3(1024), dim3(256), 0, st, q, g, D, unc, p.unc_cap, dpos, positives,
+                       g_base, cnt, metric);
+    hipLaunchKernelGGL(knn_count_reset_kernel, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, st,
+                       unc + 2 * p.unc_cap, p.unc_cap, Q, cnt);
+    hipLaunchKernelGGL(knn_count_exhaustive_kernel, dim3(64, Q), dim3(256), 0, st, q, g, D, N, unc + 2 * p.unc_cap,
+                       p.unc_cap, dpos, positives, g_base, cnt, metric);
+  }
+  hipLaunchKernelGGL(knn_exact_topk_part_kernel, dim3(KNN_XB, Q), dim3(256), 0, st, q, g, D, N, k, metric, flag, pkey,
+                     pidx);
+  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(Q), dim3(256), (size_t)KNN_XB * 4 * k, st, pkey, pidx,
+                     KNN_XB * 4, k, (long long)KNN_XB * 4 * k, (long long)k, flag, g_base, out_idx, out_dist);
+  if (out_rank) hipLaunchKernelGGL(rank_out_kernel, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, st, cnt, Q, out_rank);
+  if (out_dpos && hipMemcpyAsync(out_dpos, dpos, 8 * (size_t)Q, hipMemcpyDeviceToDevice, st) != hipSuccess) {
+    set_error("pairwise_l2_topk: dpos copy failed");
+    return -2;
+  }
+  ARTSBIR_CHECK_LAUNCH("pairwise_l2_topk");
+  return 0;
+}
+
+// per-shard top-k lists [nshard][Q][k] (as gathered from the ranks, index -1 =
+// empty) -> the global top-k by (distance, index); replaces the host-side sort
+// of the gathered lists (inference.py:49,65 topk on the whole gallery)
+extern "C" int artsbir_topk_merge(int nshard, int Q, int k, const double* dist, const long long* idx,
+                                  long long* out_idx, double* out_dist, void* stream) {
+  if (nshard < 1 || k < 1 || Q < 0 || (long long)nshard * k > 65536) {
+    set_error("topk_merge: nshard=%d k=%d Q=%d", nshard, k, Q);
+    return -1;
+  }
+  if (Q == 0) return 0;
+  hipLaunchKernelGGL(topk_lists_merge_kernel, dim3(Q), dim3(256), (size_t)nshard * k, (hipStream_t)stream, dist, idx,
+                     nshard, k, (long long)k, (long long)Q * k, (const int*)nullptr, 0LL, out_idx, out_dist);
+  ARTSBIR_CHECK_LAUNCH("topk_merge");
+  return 0;
+}
+
+extern "C" int artsbir_positive_key(int metric, const float* q, int Q, const float* g, long long n, int D,
+                                    const long long* pos, long long g_base, double* out, void* stream) {
+  if (metric != 0 && metric != 1) { set_error("positive_key: metric %d", metric); return -1; }
+  if (Q <= 0) return 0;
+  hipLaunchKernelGGL(positive_key_kernel, dim3((unsigned)((Q + 3) / 4)), dim3(256), 0, (hipStream_t)stream, q, g, D, Q,
+                     pos, g_base, n, metric, out);
+  ARTSBIR_CHECK_LAUNCH("positive_key");
+  return 0;
+}
+
+// scan-kernel timing of artsbir_pairwise_l2_topk: on = 1 starts collecting (and
+// drops what was collected), 0 stops; read waits for the recorded events and
+// returns the summed scan time (ms) and the number of scans.
+extern "C" int artsbir_scan_profile(int on) {
+  for (auto& e : g_scan_ev) {
+    (void)hipEventDestroy(e.first);
+    (void)hipEventDestroy(e.second);
+  }
+  g_scan_ev.clear();
+  g_scan_prof = on;
+  return 0;
+}
+
+extern "C" int artsbir_scan_profile_read(double* total_ms, int* count) {
+  double t = 0.0;
+  int n = 0;
+  for (auto& e : g_scan_ev) {
+    if (hipEventSynchronize(e.second) != hipSuccess) { set_error("scan_profile_read: event sync failed"); return -2; }
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) { t += ms; ++n; }
+  }
+  *total_ms = t;
+  *count = n;
+  return 0;
+}
+
+// capacity of the uncertain-item queue of artsbir_pairwise_l2_topk (default
+// 2^20); a small value forces the exhaustive recount path (tests).  Returns the old one.
+extern "C" int artsbir_knn_set_unc_cap(int cap) {
+  const int old = g_topk_unc_cap;
+  if (cap > 0) g_topk_unc_cap = cap;
+  return old;
 }

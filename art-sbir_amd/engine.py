@@ -50,6 +50,26 @@ OVERLAP_WGRAD = os.environ.get("ARTSBIR_OVERLAP_WGRAD", "1") != "0"
 # ARTSBIR_MASK_BITS=0 makes the fused backward re-read the block output for its
 # ReLU mask instead of the bit mask written by the forward
 MASK_BITS = os.environ.get("ARTSBIR_MASK_BITS", "1") != "0"
+# ARTSBIR_DETERMINISTIC=1 (parity runs): forward BatchNorm statistics
+# by a fixed-order f64 reduction of the stored conv output (artsbir_bn_stats_det)
+# instead of the epilogue's f32 atomics, so a forward is bit-identical from run
+# to run and ReLU masks cannot flip between runs
+DETERMINISTIC = os.environ.get("ARTSBIR_DETERMINISTIC", "0") == "1"
+
+
+def set_deterministic(on: bool = True) -> bool:
+    """switch the deterministic mode (fixed-order f64 BatchNorm reductions, forward
+    and backward; unfused data gradients); returns the old value"""
+    global DETERMINISTIC
+    old, DETERMINISTIC = DETERMINISTIC, bool(on)
+    _hip.lib().artsbir_set_deterministic(1 if DETERMINISTIC else 0)
+    return old
+
+
+def _fuse_bnb():
+    """BN-backward reductions fused into the data-gradient epilogues (f32 atomics)
+    except in the deterministic mode, which reduces them in a fixed order"""
+    return FUSE_BNB and not DETERMINISTIC
 
 # bumped by optim.Adam (which updates parameters through raw pointers, invisible
 # to torch's version counters) so packed weights are rebuilt after every step
@@ -71,8 +91,9 @@ def _at(t, i):
 
 @dataclass
 class BNState:
-    """per-call batch-norm parameters of G segments: buf [G][4][C] f32 holds the
-    mean, istd, scale, shift of each segment; count = elements per segment."""
+    """per-call batch-norm parameters of G segments: buf [G][4][C] f32 holds each
+    segment's parameter block mean, istd, scale = gamma*istd, beta — applied by
+    the kernels as (y - mean) * scale + beta; count = elements per segment."""
     buf: torch.Tensor
     count: float
 
@@ -101,8 +122,9 @@ class BNState:
         return self.buf[0, 2]
 
     @property
-    def shift(self):
-        return self.buf[0, 3]
+    def block(self):
+        """the first segment's [4][C] parameter block (segments follow at 4*C floats)"""
+        return self.buf[0]
 
 
 @dataclass
@@ -221,13 +243,17 @@ class Engine:
         nbytes = float(es * (B * H * W * C + cout * R * S * C + B * Ho * Wo * cout))  # algorithmic: x, w, y once
         if stats_buf is not None and bn is None:
             # BN statistics per segment (one launch for all G forward calls)
-            call("artsbir_conv2d_fwd_seg", d, ptr(a.t), ptr(fw), ptr(y), self._G, ptr(stats_buf), _s(),
-                 kernel="auto", flops=flops, nbytes=nbytes, tag=f"fwd {B}x{H}x{W}x{C}->{cout} {R}x{S}/{stride}")
+            det = DETERMINISTIC
+            call("artsbir_conv2d_fwd_seg", d, ptr(a.t), ptr(fw), ptr(y), self._G, None if det else ptr(stats_buf),
+                 _s(), kernel="auto", flops=flops, nbytes=nbytes,
+                 tag=f"fwd {B}x{H}x{W}x{C}->{cout} {R}x{S}/{stride}")
+            if det:  # fixed-order f64 sums of the stored output instead of epilogue atomics
+                call("artsbir_bn_stats_det", self.dt, ptr(y), self._G, B // self._G * Ho * Wo, cout,
+                     ptr(stats_buf), 2 * NSLOT * cout, _s())
             return y
-        if bn is not None and bn.G != 1:
-            raise NotImplementedError("affine-on-load convolutions take one segment")
-        call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None,
-             ptr(bn.scale) if bn else None, ptr(bn.shift) if bn else None, a.relu,
+        if bn is not None:
+            raise NotImplementedError("BatchNorm is applied once by act_pool, not on the conv's load")
+        call("artsbir_conv2d_fwd", d, ptr(a.t), ptr(fw), ptr(y), cout, 0, 0, None, None, None, 0,
              ptr(stats_buf), _s(), kernel="auto", flops=flops, nbytes=nbytes)
         return y
 
@@ -258,8 +284,8 @@ class Engine:
         Bs = B // G
         for s in range(G):
             sb = bn.seg(s) if bn is not None else None
-            call("artsbir_act_pool", self.dt, _at(x, s * Bs), ptr(sb.scale) if sb else None,
-                 ptr(sb.shift) if sb else None, relu, pool, Bs, H, W, C, _at(out, s * Bs), _s())
+            call("artsbir_act_pool", self.dt, _at(x, s * Bs), ptr(sb.block) if sb else None, relu, pool, Bs, H, W,
+                 C, _at(out, s * Bs), _s())
         return out
 
     # ---------------------------------------------------------------- forward
@@ -274,6 +300,7 @@ class Engine:
                 raise ValueError("forward_branches: every branch needs the same input shape")
         G = len(xs)
         self._G = G
+        _hip.lib().artsbir_set_deterministic(1 if DETERMINISTIC else 0)
         m = self.model
         pk = self.packed()
         Bs, cin, R, R2 = xs[0].shape
@@ -338,13 +365,13 @@ class Engine:
         # bf16 training: the ReLU mask of the block output as bits for the fused
         # backward (kind 3), 1/16 of re-reading `out` there
         bits = None
-        if train and FUSE_BNB and MASK_BITS and self.dt == _hip.DT_BF16:
+        if train and _fuse_bnb() and MASK_BITS and self.dt == _hip.DT_BF16:
             bits = torch.empty(out.numel() // 8, dtype=torch.uint8, device=out.device)
         for g in range(G):
             s3 = b3.seg(g)
             sd = bd.seg(g) if bd is not None else None
-            call("artsbir_block_out_mask", self.dt, _at(y3, g * Bs), ptr(s3.scale), ptr(s3.shift),
-                 _at(yd, g * Bs), ptr(sd.scale) if sd else None, ptr(sd.shift) if sd else None,
+            call("artsbir_block_out_mask", self.dt, _at(y3, g * Bs), ptr(s3.block),
+                 _at(yd, g * Bs), ptr(sd.block) if sd else None,
                  None if yd is not None else _at(h, g * Bs), rows, C, _at(out, g * Bs),
                  (bits.data_ptr() + g * rows * (C // 8)) if bits is not None else None, _s())
         ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, bits=bits, b1=b1, b2=b2, b3=b3,
@@ -390,6 +417,7 @@ class Engine:
         m = self.model
         pk = self.packed()
         self._G = G = ctx["G"]
+        _hip.lib().artsbir_set_deterministic(1 if DETERMINISTIC else 0)
         dev = dout.device
         grads = self.grad_buffer(dev)
         ws = _Arena(torch.zeros(max(2 * NSLOT * m.total_bn_channels() * 2 * G, 1), dtype=torch.float32, device=dev),
@@ -460,8 +488,7 @@ class Engine:
             desc.d = _at(d, s * Bs)
             desc.mask = _at(mask, s * Bs)
             mb = mask_bn.seg(s) if mask_bn is not None else None
-            desc.mask_scale = ptr(mb.scale) if mb else None
-            desc.mask_shift = ptr(mb.shift) if mb else None
+            desc.mask_bn = ptr(mb.block) if mb else None
             desc.ntarget = len(targets)
             for i, (y, st) in enumerate(targets):
                 ss = st.seg(s)
@@ -505,8 +532,7 @@ class Engine:
         desc.kind = kind
         desc.pool = 0
         desc.mask = ptr(mask)
-        desc.mask_scale = ptr(mask_bn.scale) if mask_bn is not None else None
-        desc.mask_shift = ptr(mask_bn.shift) if mask_bn is not None else None
+        desc.mask_bn = ptr(mask_bn.block) if mask_bn is not None else None
         desc.ntarget = len(targets)
         slots = []
         for i, (y, st) in enumerate(targets):
@@ -580,8 +606,9 @@ class Engine:
         else:
             target = torch.zeros(co, R, S, C, dtype=torch.float32, device=dy.device)
         Ho, Wo = dy.shape[1], dy.shape[2]
-        call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), ptr(bn.scale) if bn else None,
-             ptr(bn.shift) if bn else None, a.relu, ptr(target), _s(), kernel="auto",
+        if bn is not None:
+            raise NotImplementedError("BatchNorm is applied once by act_pool, not on the wgrad's load")
+        call("artsbir_conv2d_wgrad", d, ptr(dy), ptr(a.t), None, None, 0, ptr(target), _s(), kernel="auto",
              flops=2.0 * B * Ho * Wo * co * R * S * C, tag=f"wgrad {B}x{H}x{W}x{C}->{co} {R}x{S}/{stride}",
              nbytes=float(dy.element_size() * (B * Ho * Wo * co + B * H * W * C) + 4 * co * R * S * C))
         if target is not g:
@@ -631,7 +658,7 @@ class Engine:
         c3in = Act(p2)
         self._wgrad(dy3, c3in, blk.conv3, 1, 0, grads)
         c3out = c3in.shape[:3] + (blk.conv3.weight.shape[1],)
-        if s == 1 and FUSE_BNB:
+        if s == 1 and _fuse_bnb():
             f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
             g2 = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out, fused=f2)
             dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
@@ -639,7 +666,7 @@ class Engine:
             dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out)
             dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
         self._wgrad(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
-        if FUSE_BNB:
+        if _fuse_bnb():
             f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
             g1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape, fused=f1)
             dy1, = self._bn_finish(g1, f1, [blk.bn1], grads)
@@ -657,7 +684,7 @@ class Engine:
         else:
             res, res_mode = gid, 1
         fprev = None
-        if prev is not None and FUSE_BNB:
+        if prev is not None and _fuse_bnb():
             pblk, pc = prev
             ptargets = [(pc["y3"], pc["b3"])] + ([(pc["yd"], pc["bd"])] if pblk.downsample is not None else [])
             if pc.get("bits") is not None:
@@ -672,7 +699,7 @@ class Engine:
         (_, _), (_, dw2), (_, dw3) = pk["stem"]
         dy3, = self._bn_bwd(1, dh, [(y3, b3)], [m.bn3], ws, grads, mask_bn=b3, pool=2)
         self._wgrad(dy3, Act(c["a2"]), m.conv3, 1, 1, grads)
-        if FUSE_BNB:
+        if _fuse_bnb():
             f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
             g2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape, fused=f2)
             dy2, = self._bn_finish(g2, f2, [m.bn2], grads)
@@ -680,7 +707,7 @@ class Engine:
             da2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape)
             dy2, = self._bn_bwd(1, da2, [(y2, b2)], [m.bn2], ws, grads, mask_bn=b2)
         self._wgrad(dy2, Act(c["a1"]), m.conv2, 1, 1, grads)
-        if FUSE_BNB:
+        if _fuse_bnb():
             f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
             g1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape, fused=f1)
             dy1, = self._bn_finish(g1, f1, [m.bn1], grads)

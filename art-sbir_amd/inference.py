@@ -46,22 +46,14 @@ def sketch_target_name(sketch_path, image_paths):
     return None
 
 
-def _normalise(x):
-    n = torch.linalg.vector_norm(x.float(), dim=1, keepdim=True).clamp_min(1e-8)
-    return x.float() / n
-
-
 def _search(sketch_features, image_features, k, positives, loss_type):
+    """exact top-k (keys: ||q - g + 1e-6|| for 'euclidean', 1 - cos for 'cosine',
+    utils.py:31-42) and 0-based ranks of the positives, one library call"""
     q, g = sketch_features.float(), image_features.float()
-    if loss_type == 'euclidean':
-        pass
-    elif loss_type == 'cosine':
-        # 1 - cos is monotone in the L2 distance of unit vectors
-        q, g = _normalise(q), _normalise(g)
-    else:
-        raise Exception(f"loss type not correct {loss_type}")
+    if loss_type not in ('euclidean', 'cosine'):
+        raise Exception(f"loss type not correct {loss_type}")  # inference.py:48
     k = min(k, g.shape[0])
-    return knn.knn(q.contiguous(), g.contiguous(), k, positives)
+    return knn.knn(q.contiguous(), g.contiguous(), k, positives, metric=loss_type)
 
 
 def get_ranking_position(sketch_path, image_paths: List[Path], sketch_feature: torch.Tensor,

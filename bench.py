@@ -77,13 +77,31 @@ def train_flops_per_triplet():
     return 3 * (3 * encoder_flops_per_image() - stem1)
 
 
-def cpu_baseline(batch=32, steps=3):
-    """The oracle (torch CPU fp32 restatement of the reference path) on the host
-    cores: same model/config, a bounded sample of `batch` triplets per step."""
+def cpu_model():
+    """the host CPU's model string (stated with every CPU baseline)"""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def cpu_cores():
+    cores = len(os.sched_getaffinity(0))
+    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+
+
+def cpu_baseline(batch=32, steps=3, layers=LAYERS, out_dim=OUT_DIM):
+    """The oracle (torch CPU fp32 restatement of the reference path: three
+    separate forwards, nn.TripletMarginLoss, torch.optim.Adam — train.py:27-37,
+    59-70) on the host cores: a bounded sample of `batch` triplets per step."""
     from oracle import encoder as oenc, steps as osteps
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    cores = cpu_cores()
     torch.set_num_threads(cores)
-    m = osteps.build(LAYERS, OUT_DIM, HEADS, RES, WIDTH)
+    m = osteps.build(layers, out_dim, HEADS, RES, WIDTH)
     opt = osteps.make_optimizer(m)
     loss = osteps.make_loss(0.2)
     el = list(oenc.synthetic_triplet(batch, RES))
@@ -93,8 +111,9 @@ def cpu_baseline(batch=32, steps=3):
         osteps.train_step(m, opt, loss, el)
     dt = time.perf_counter() - t0
     return {"value": round(3 * batch * steps / dt, 3), "unit": "triplet-images/s", "cores": cores, "kind": "port",
-            "sample": f"oracle/steps.py train_step, ModifiedResNet((3,4,6,3),512) fp32 224^2, {steps} timed steps x "
-                      f"{batch} triplets after 1 warm-up, torch CPU {torch.__version__} on {platform.processor() or 'x86_64'}"}
+            "cpu": cpu_model(),
+            "sample": f"oracle/steps.py train_step, ModifiedResNet({layers},{out_dim}) fp32 224^2, {steps} timed "
+                      f"steps x {batch} triplets after 1 warm-up, torch CPU {torch.__version__}"}
 
 
 def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
@@ -122,23 +141,25 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    prof = []
+    import ctypes
     import _hip
-    _hip.PROFILE = prof
+    lib = _hip.lib()
+    lib.artsbir_scan_profile(1)  # HIP events around the scan kernel inside the one call
     t0 = time.perf_counter()
     for _ in range(reps):
         idx, dd, r = run()
     torch.cuda.synchronize()
     el = (time.perf_counter() - t0) / reps
-    _hip.PROFILE = None
+    tot, cnt = ctypes.c_double(0.0), ctypes.c_int(0)
+    lib.artsbir_scan_profile_read(ctypes.byref(tot), ctypes.byref(cnt))
+    lib.artsbir_scan_profile(0)
     if world > 1:
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    scan_kernel = "knn_scan_v2_kernel" if any(kn == "knn_scan_v2_kernel" for kn, *_ in prof) else "knn_scan_kernel"
-    scan = [(fl, e0.elapsed_time(e1) / 1e3) for kn, fl, _, e0, e1, *_ in prof if kn == scan_kernel]
-    scan_s = sum(s for _, s in scan) / len(scan)
-    scan_fl = sum(f for f, _ in scan) / len(scan)
+    scan_kernel = lib.artsbir_last_kernel().decode()
+    scan_s = tot.value / 1e3 / max(cnt.value, 1)
+    scan_fl = 2.0 * Q * (hi - lo) * D
     rk = r.double() + 1
     map10 = float(torch.where(rk <= k, 1.0 / rk, torch.zeros_like(rk)).mean())
     return {"metric": "gallery kNN QPS @1M x 512 (exact top-10 + rank of positive)", "value": round(Q / el, 1),
@@ -152,22 +173,99 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
                          "traffic": pmc_traffic(scan_kernel)}}
 
 
-def cpu_retrieval_baseline(N=1_000_000, D=512, nq=8):
-    """reference-style per-query loop (inference.py:30-57: PairwiseDistance over the
-    whole gallery + full sort + position of the positive) via the oracle's float64
-    restatement on the host cores, on nq queries of the C4 workload, as queries/s."""
-    import numpy as np
-    from oracle import retrieval as oret
-    g, qs, pos = oret.synthetic_gallery(N, D, nq)
+def cpu_retrieval_baseline(N=1_000_000, D=512, nq=100, budget_s=25.0):
+    """SURVEY §8d retrieval CPU baseline on the host cores, torch fp32:
+      per_query — the reference's op sequence per query (inference.py:43-56:
+                  nn.PairwiseDistance(p=2) of [1,D] vs the [N,D] gallery, full
+                  topk(N, largest=False), position of the positive), over up to nq
+                  queries of the C4 workload or until budget_s is spent;
+      batched   — a fair CPU variant: one GEMM-form distance matrix for the same
+                  queries and topk(10) per row, plus the rank of the positive."""
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    g = torch.randn(N, D, generator=torch.Generator().manual_seed(7))
+    pos = (torch.arange(nq) * 7919) % N
+    qs = g[pos] + 0.5 * torch.randn(nq, D, generator=torch.Generator().manual_seed(8))
+    pdist = torch.nn.PairwiseDistance(p=2)
+    pdist(qs[:1], g).topk(N, largest=False)  # warm-up
+    done = 0
     t0 = time.perf_counter()
-    for i in range(nq):
-        d = oret.l2_distances(qs[i], g)
-        o = oret.order(d)
-        int(np.nonzero(o == pos[i])[0][0])
+    while done < nq and time.perf_counter() - t0 < budget_s:
+        d = pdist(qs[done:done + 1], g)
+        _, idx = d.topk(N, largest=False)
+        int((idx == pos[done]).nonzero()[0, 0])
+        done += 1
     dt = time.perf_counter() - t0
-    return {"value": round(nq / dt, 3), "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": f"{nq} queries x full {N}x{D} gallery, oracle/retrieval.py float64 distances + stable argsort "
-                      "(numpy, single-threaded), per-query like the reference"}
+    t1 = time.perf_counter()
+    gsq = (g * g).sum(1)
+    d2 = (qs * qs).sum(1)[:, None] + gsq[None, :] - 2.0 * (qs @ g.T)
+    d2.topk(10, dim=1, largest=False)
+    (d2 < d2.gather(1, pos[:, None])).sum(1)
+    dtb = time.perf_counter() - t1
+    return {"value": round(done / dt, 3), "unit": "queries/s", "cores": cores, "kind": "port", "cpu": cpu_model(),
+            "sample": f"{done} queries (of {nq}, {budget_s:.0f} s budget) x full {N}x{D} gallery: torch fp32 "
+                      f"nn.PairwiseDistance + topk(N) per query like inference.py:43-56, {cores} threads",
+            "batched": {"value": round(nq / dtb, 3), "unit": "queries/s",
+                        "sample": f"{nq} queries as one fp32 GEMM-form distance matrix + topk(10) + rank, "
+                                  f"{cores} threads"}}
+
+
+def embed_leg(model, batch, dtype_name, world, reps):
+    """Embed-only throughput of C2 (the BASELINE metric's "triplet-images/sec
+    embedded"): eval-mode BatchNorm (running statistics), no autograd, the 3 x B
+    images of one triplet batch per pass — inference.py:72-92's
+    compute_image_features arithmetic on the triplet workload."""
+    import _hip
+    model.eval()
+    with torch.no_grad():
+        model.forward_branches(batch)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        prof = []
+        _hip.PROFILE = prof
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            out = model.forward_branches(batch)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        _hip.PROFILE = None
+    model.train()
+    if world > 1:
+        t = torch.tensor([el], device=batch[0].device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    images = sum(x.shape[0] for x in batch) * reps * world
+    gpu_s = sum(e0.elapsed_time(e1) for _, _, _, e0, e1, *_ in prof) / 1e3
+    fl = encoder_flops_per_image() * images / world
+    return {"metric": "triplet-images/s embedded (eval BatchNorm, no backward)", "value": round(images / el, 2),
+            "unit": "triplet-images/s", "ms_per_pass": round(el / reps * 1e3, 3), "n_gpus": world,
+            "images_per_pass": sum(x.shape[0] for x in batch), "dtype": dtype_name,
+            "finite": bool(torch.isfinite(torch.cat(out)).all()),
+            "roofline": {"bound": "mfma", "achieved": round(fl / el / 1e12, 2),
+                         "peak": MFMA_PEAK_TFLOPS[dtype_name], "unit": "TFLOP/s",
+                         "frac": round(fl / el / 1e12 / MFMA_PEAK_TFLOPS[dtype_name], 4),
+                         "kernel_time_share": round(gpu_s / el, 3) if el else None,
+                         "note": "whole forward pass: algorithmic encoder FLOPs (bench.encoder_flops_per_image) "
+                                 "over wall time"}}
+
+
+def cpu_embed_baseline(batch=48, reps=2):
+    """oracle eval-mode embedding (inference.py:72-92 in batches of 50) of a
+    bounded sample on the host cores"""
+    from oracle import encoder as oenc, steps as osteps
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    m = osteps.build(LAYERS, OUT_DIM, HEADS, RES, WIDTH)
+    imgs = torch.cat(oenc.synthetic_triplet(batch // 3, RES))
+    osteps.embed(m, imgs[:8])
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        osteps.embed(m, imgs)
+    dt = time.perf_counter() - t0
+    return {"value": round(len(imgs) * reps / dt, 3), "unit": "triplet-images/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model(), "sample": f"oracle/steps.py embed (eval BN, batches of 50), {len(imgs)} images x "
+                                          f"{reps}, ModifiedResNet((3,4,6,3),512) fp32 224^2"}
 
 
 def main():
@@ -182,6 +280,11 @@ def main():
     ap.add_argument("--no-retrieval", action="store_true", help="skip the 1M x 512 kNN leg")
     ap.add_argument("--unbatched", dest="batched", action="store_false",
                     help="three separate encoder calls per step instead of forward_branches")
+    ap.add_argument("--no-embed", action="store_true", help="skip the embed-only (eval-BN) leg")
+    ap.add_argument("--no-loss-check", action="store_true", help="skip the f32 step-0 loss check")
+    ap.add_argument("--tune-cache", default=None,
+                    help="autotuner choices file: loaded first if it exists, written after the warm-up "
+                         "(profiled re-runs then launch no tuning trials)")
     args = ap.parse_args()
 
     import _hip
@@ -217,6 +320,24 @@ def main():
     std = torch.tensor(models.CLIP_STD, device=dev)[None, :, None, None]
     batch = [((t - mean) / std).contiguous() for t in (sketch, pos, neg)]
 
+    if args.tune_cache and os.path.exists(args.tune_cache):
+        n = _hip.lib().artsbir_tune_load(args.tune_cache.encode())
+        if n < 0:
+            raise RuntimeError(f"tune cache {args.tune_cache}: {_hip.lib().artsbir_last_error().decode()}")
+
+    # step-0 loss check: the f32 parity mode of the same library (within 1e-3 of
+    # the oracle, tests/test_c2_gpu.py) on the same batch and initial weights;
+    # the bf16 step's loss must agree (running stats restored afterwards)
+    loss_f32 = None
+    if not args.no_loss_check:
+        saved = {k: v.clone() for k, v in model.state_dict().items() if "running" in k or "num_batches" in k}
+        model.compute_dtype = torch.float32
+        with torch.no_grad():
+            loss_f32 = float(loss_fn(*model.forward_branches(batch)).item())
+        model.compute_dtype = dtype
+        model.load_state_dict(saved, strict=False)
+        torch.cuda.empty_cache()
+
     def step():
         # the three branch forwards of train.py:28-30 (per-branch BN statistics),
         # each GEMM launched once over the 3 x B images
@@ -234,9 +355,14 @@ def main():
     prio = int(os.environ.get("ARTSBIR_STEP_PRIO", "-1"))
     if prio:
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=prio))
-    for _ in range(args.warmup):
-        step()
+    loss0 = None
+    for i in range(max(args.warmup, 1)):
+        li = step()
+        if i == 0:
+            loss0 = float(li.item())
     torch.cuda.synchronize()
+    if args.tune_cache and rank == 0:
+        _hip.lib().artsbir_tune_save(args.tune_cache.encode())
     if world > 1:
         ddp.broadcast_buffers(model)
         dist.barrier()
@@ -306,14 +432,25 @@ def main():
             "triplets_per_s": round(value / 3, 2),
             "step_tflops": round(step_flops * world / (elapsed / args.steps) / 1e12, 2),
             "loss": last_loss,
+            "loss_step0": loss0,
+            "loss_step0_f32": loss_f32,
+            "loss_step0_rel_diff": (round(abs(loss0 - loss_f32) / max(abs(loss_f32), 1e-12), 6)
+                                    if loss_f32 is not None else None),
             "roofline": roof,
         }
+    emb = None if args.no_embed else embed_leg(model, batch, args.dtype, world, args.steps)
     ret = None if args.no_retrieval else retrieval_leg(dev, rank, world)
     if rank == 0:
+        if emb is not None:
+            line["embed"] = emb
         if ret is not None:
             line["retrieval"] = ret
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
+            # C1 (BASELINE configs[0]): the "ResNet18 128-d" config = ModifiedResNet((2,2,2,2),128), batch 32
+            line["cpu_baseline"]["c1"] = cpu_baseline(batch=32, steps=2, layers=(2, 2, 2, 2), out_dim=128)
+            if emb is not None:
+                emb["cpu_baseline"] = cpu_embed_baseline()
             if ret is not None:
                 ret["cpu_baseline"] = cpu_retrieval_baseline()
         print(json.dumps(line), flush=True)

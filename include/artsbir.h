@@ -37,6 +37,11 @@ int artsbir_version(void);
 /* Name of the GEMM kernel variant the last conv2d_fwd / conv2d_dgrad / gemm_nt /
  * conv2d_wgrad / gemm_tn call on this thread launched (for per-kernel profiling). */
 const char* artsbir_last_kernel(void);
+/* Autotuner choices (kernel variant per conv / wgrad shape) to and from a text
+ * file, so a profiled re-run launches only the steady-state kernels (no trial
+ * launches).  load returns the number of entries read, or -1. */
+int artsbir_tune_save(const char* path);
+int artsbir_tune_load(const char* path);
 
 /* ---- convolution / linear (models.py:198-221,310-319 nn.Conv2d; models.py:243-246 nn.Linear) */
 
@@ -83,7 +88,7 @@ int artsbir_conv2d_fwd_seg(const artsbir_conv_desc* d, const void* x, const void
 
 /* conv2d_dgrad whose output is the gradient at the output of a BatchNorm2d(+ReLU)
  * (models.py:199-210, 234-235): the BN-backward reduction is fused into it.  dx
- * receives g = dx_raw * relu-mask (bnb->kind 1: y[0]*mask_scale+mask_shift > 0;
+ * receives g = dx_raw * relu-mask (bnb->kind 1: mask_bn(y[0]) > 0;
  * kind 0: mask > 0, the block output; kind 3: the block output's mask bits, bf16
  * only) and bnb->slots[t] += (sum g, sum g*xhat_t)
  * exactly as artsbir_bn_bwd_reduce; finish with artsbir_bn_bwd_finalize and
@@ -109,43 +114,53 @@ int artsbir_cast(int src_dtype, const void* x, int dst_dtype, void* y, long long
 /* ---- batch norm / activations (models.py BatchNorm2d, ReLU, AvgPool2d) -- */
 /* train: mean/var from stats slots, running stats updated (momentum, unbiased
  * var), num_batches_tracked += 1; eval: from running stats.  Outputs per-channel
- * mean, istd, scale = gamma*istd, shift = beta - mean*scale. */
+ * mean, istd, scale = gamma*istd and beta: the BN PARAMETER BLOCK that every
+ * consumer below applies as bn(y) = (y - mean) * scale + beta (the mean is
+ * subtracted first so f32 stays accurate when |mean| >> std). */
 int artsbir_bn_finalize(const float* stats, int C, double count, const float* gamma, const float* beta,
                         float* running_mean, float* running_var, long long* num_batches_tracked,
                         float momentum, float eps, int train, float* mean, float* istd, float* scale,
-                        float* shift, void* stream);
+                        float* beta_out, void* stream);
 /* artsbir_bn_finalize for the nseg BN segments of one layer in one launch
  * (segment s: stats + s*seg_stride; running statistics updated once per segment,
- * in order; num_batches_tracked += nseg); out[s][4][C] = mean, istd, scale, shift. */
+ * in order; num_batches_tracked += nseg); out[s][4][C] = mean, istd, scale, beta
+ * (segment s's parameter block). */
 int artsbir_bn_finalize_seg(const float* stats, int nseg, long long seg_stride, int C, double count,
                             const float* gamma, const float* beta, float* running_mean, float* running_var,
                             long long* num_batches_tracked, float momentum, float eps, int train, float* out,
                             void* stream);
-/* out = avgpool_pool( relu?(x*scale+shift) ) (scale == NULL: no affine). */
-int artsbir_act_pool(int dtype, const void* x, const float* scale, const float* shift, int relu, int pool,
-                     int B, int H, int W, int C, void* out, void* stream);
+/* Deterministic-mode BatchNorm statistics (SURVEY §5 "deterministic-kernel mode
+ * for parity runs"; replaces the batch moments nn.BatchNorm2d takes in train
+ * mode, models.py:199,203,209,220,311,314,317): per segment s of y
+ * [nseg*rows][C], the f64 sum and sum of squares in a fixed order, written as
+ * f32 hi/lo pairs to slots 0/1 of stats + s*seg_stride ([NSLOT][2][C], other
+ * slots zeroed), the layout artsbir_bn_finalize_seg reads.  Bit-identical from
+ * run to run (the conv epilogues' atomics are not). */
+int artsbir_bn_stats_det(int dtype, const void* y, int nseg, long long rows, int C, float* stats,
+                         long long seg_stride, void* stream);
+/* out = avgpool_pool( relu?(bn(x)) ), bn = a [4][C] parameter block (NULL: no affine). */
+int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W, int C,
+                     void* out, void* stream);
 /* Bottleneck tail (models.py:234-235): out = relu(bn3(y3) + (bn_d(yd) | identity)). */
-int artsbir_block_out(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
-                      const float* scd, const float* shd, const void* identity, long long rows, int C,
-                      void* out, void* stream);
+int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                      const void* identity, long long rows, int C, void* out, void* stream);
 /* The same, also writing the block output's ReLU mask as bits: mask_bits[row][C/8],
  * bit e of byte c = out[row][8c+e] > 0 (the backward's kind-3 mask: 1/16 of the
  * bytes of re-reading out). */
-int artsbir_block_out_mask(int dtype, const void* y3, const float* sc3, const float* sh3, const void* yd,
-                           const float* scd, const float* shd, const void* identity, long long rows, int C,
-                           void* out, unsigned char* mask_bits, void* stream);
+int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                           const void* identity, long long rows, int C, void* out, unsigned char* mask_bits,
+                           void* stream);
 
 /* BatchNorm2d(train) backward, see elementwise.hip for the math. */
 struct artsbir_bn_bwd_desc {
   int dtype;
-  int kind;               /* 0: g = d*(mask>0) (block output); 1: g = up(d)*(y*mask_scale+mask_shift>0);
+  int kind;               /* 0: g = d*(mask>0) (block output); 1: g = up(d)*(mask_bn(y[0])>0);
                              2: g = d (already masked, artsbir_conv2d_dgrad_bnb);
                              3: as 0 with mask = mask bits of artsbir_block_out_mask (reduce, dgrad_bnb) */
   int pool;               /* kind 1: d is at 1/pool resolution (AvgPool backward) */
   const void* d;
   const void* mask;
-  const float* mask_scale;
-  const float* mask_shift;
+  const float* mask_bn;   /* kind 1: parameter block [4][C] of the BN feeding the ReLU */
   int ntarget;            /* 1 or 2 BN inputs sharing g */
   const void* y[2];
   const float* mean[2];
@@ -157,6 +172,11 @@ struct artsbir_bn_bwd_desc {
   int B, H, W, C;
 };
 int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
+/* Deterministic mode for parity runs: artsbir_bn_bwd_reduce then sums
+ * in a fixed order in f64 (one workgroup, f32 hi/lo pairs in slots 0/1) instead
+ * of f32 atomics.  Pair with artsbir_bn_stats_det for the forward statistics and
+ * the unfused data gradients.  Returns the previous setting. */
+int artsbir_set_deterministic(int on);
 /* dgamma += sum g*xhat, dbeta += sum g; coef = [gamma*istd, sum g/cnt, sum g*xhat/cnt]. */
 int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,
                             float* dgamma, float* dbeta, float* coef, void* stream);
@@ -256,6 +276,45 @@ int artsbir_knn_uncertain(const float* q, const float* g, int D, const int* unc,
                           const double* dpos, const long long* pos, long long g_base, int* cnt, void* stream);
 /* out[i] = exact f64 ||q - g_i + 1e-6|| for all i (fallback / tiny galleries). */
 int artsbir_knn_exact_all(const float* q, const float* g, int D, int n, double* out, void* stream);
+
+/* ONE-CALL exact retrieval (replaces the per-query loop of inference.py:30-69:
+ * utils.euclidean_distance / utils.cosine_distance of [1,D] vs the [N,D]
+ * gallery, distances.topk(N, largest=False) -> position of the positive, and
+ * topk(k) for get_topk_images).  metric 0: key = ||q - g + 1e-6|| (f64 from the
+ * f32 rows, nn.PairwiseDistance(p=2, eps=1e-6), utils.py:42); metric 1: key =
+ * 1 - q.g / (max(|q|,1e-8) max(|g|,1e-8)) (utils.py:31-40).  Order = (key,
+ * gallery index), the tie rule the reference leaves unspecified.
+ *   out_idx [Q][k] global indices g_base + i (-1 past the gallery), out_dist [Q][k]
+ *   keys (f64, +inf past the gallery); with positives [Q] (global index, -1 =
+ *   none): out_rank [Q] = #{i : (key_i, g_base+i) < (key_pos, pos)} over THIS
+ *   gallery (0-based rank, inference.py:49-56), out_dpos [Q] = key of the
+ *   positive (-1 if none).  dpos_in (nullable): for a shard call, the positive's
+ *   key when it lives in another shard (artsbir_positive_key + a MAX all-reduce).
+ * dtype: ARTSBIR_DT_BF16 (bf16 MFMA scan) or ARTSBIR_DT_F32 (f32 MFMA scan); the
+ * result is exact either way.  1 <= k <= 64, N < 2^31.  tiles_per_chunk 0 = auto.
+ * workspace: device memory of artsbir_pairwise_l2_topk_workspace() bytes.  No
+ * host synchronisation; the rare fallbacks (uncertain-queue overflow, a chunk
+ * list that may have hidden a top-k item) run as device kernels. */
+long long artsbir_pairwise_l2_topk_workspace(int dtype, int Q, long long N, int D, int k, int tiles_per_chunk);
+int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, int Q, const float* g, long long N, int D, int k,
+                             const long long* positives, const double* dpos_in, long long g_base, int tiles_per_chunk,
+                             long long* out_idx, double* out_dist, long long* out_rank, double* out_dpos,
+                             void* workspace, long long workspace_bytes, void* stream);
+/* capacity of its uncertain-item queue (default 2^20; a small value forces the
+ * exhaustive recount fallback, for tests); returns the previous capacity. */
+int artsbir_knn_set_unc_cap(int cap);
+/* HIP-event timing of the scan kernel inside artsbir_pairwise_l2_topk (profiling):
+ * on = 1 starts collecting, 0 stops; read returns the summed scan time and count. */
+int artsbir_scan_profile(int on);
+int artsbir_scan_profile_read(double* total_ms, int* count);
+/* per-shard top-k lists gathered from nshard ranks, dist/idx [nshard][Q][k]
+ * (index -1 = empty) -> global top-k by (distance, index) (sharded C4). */
+int artsbir_topk_merge(int nshard, int Q, int k, const double* dist, const long long* idx, long long* out_idx,
+                       double* out_dist, void* stream);
+/* out[q] = exact key (metric as above) of q's positive pos[q] if it lies in rows
+ * [g_base, g_base+n) of this shard g, else -1 (feeds dpos_in after a MAX all-reduce). */
+int artsbir_positive_key(int metric, const float* q, int Q, const float* g, long long n, int D, const long long* pos,
+                         long long g_base, double* out, void* stream);
 
 /* backward of artsbir_pairwise_l2 (one-row operands accumulate with atomics). */
 int artsbir_pairwise_l2_bwd(const float* x1, long long n1, const float* x2, long long n2, int D, float eps,

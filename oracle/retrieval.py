@@ -33,10 +33,21 @@ def l2_distances(q: np.ndarray, g: np.ndarray) -> np.ndarray:
 
 
 def cosine_distances(q: np.ndarray, g: np.ndarray, eps: float = 1e-8) -> np.ndarray:
+    """1 - cos(q, g_i) in float64 with nn.CosineSimilarity's eps: each norm is
+    clamped separately, x1.x2 / (max(|x1|, eps) max(|x2|, eps)) (torch 2.10)."""
     q64, g64 = q.astype(np.float64), g.astype(np.float64)
-    num = g64 @ q64
-    den = np.maximum(np.linalg.norm(g64, axis=1) * np.linalg.norm(q64), eps)
+    num = np.einsum("nd,d->n", g64, q64)
+    den = np.maximum(np.sqrt(np.einsum("nd,nd->n", g64, g64)), eps) * max(np.sqrt(q64 @ q64), eps)
     return 1.0 - num / den
+
+
+def distances(q: np.ndarray, g: np.ndarray, metric: str = "euclidean") -> np.ndarray:
+    """the reference's distance of inference.py:43-48 for loss_type `metric`"""
+    if metric == "euclidean":
+        return l2_distances(q, g)
+    if metric == "cosine":
+        return cosine_distances(q, g)
+    raise Exception(f"loss type not correct {metric}")
 
 
 def order(dist: np.ndarray) -> np.ndarray:
@@ -53,6 +64,50 @@ def rank_of(dist: np.ndarray, pos: int) -> int:
     """0-based position of gallery item `pos` in the stable ascending order."""
     d = dist[pos]
     return int(np.count_nonzero(dist < d) + np.count_nonzero(dist[:pos] == d))
+
+
+def topk_rank_large(qs: np.ndarray, g: np.ndarray, pos, k: int, metric: str = "euclidean", chunk: int = 16):
+    """topk(distances(q, g), k) and rank_of(..., pos) for every query, for
+    galleries too large for the per-query float64 loop (1M x 512).  Candidate
+    sets come from the float64 GEMM form; every decision is re-made with the
+    direct form above, so the answers are those of distances() + stable sort:
+      euclidean: |GEMM d^2 - direct d^2| <= 2e-6 sqrt(D) |q - g| + D e-12 + f64
+                 rounding, covered by the margin m below;
+      cosine:    the GEMM and direct forms differ by f64 rounding only."""
+    import torch
+    G = torch.from_numpy(np.ascontiguousarray(g)).double()
+    gsq = (G * G).sum(1)
+    N, D = G.shape
+    gn = gsq.sqrt().clamp_min(1e-8)
+    out_i = np.zeros((len(qs), k), np.int64)
+    out_d = np.zeros((len(qs), k))
+    ranks = np.full(len(qs), -1, np.int64)
+    for c0 in range(0, len(qs), chunk):
+        Qc = torch.from_numpy(np.ascontiguousarray(qs[c0:c0 + chunk])).double()
+        dot = Qc @ G.T
+        qsq = (Qc * Qc).sum(1, keepdim=True)
+        if metric == "euclidean":
+            a = qsq + gsq[None, :] - 2.0 * dot                       # ~ key^2
+            m = 4e-6 * torch.sqrt(D * (qsq + gsq.max())) + 1e-9 * (qsq + gsq.max()) + 1e-9
+        else:
+            a = 1.0 - dot / (qsq.sqrt().clamp_min(1e-8) * gn[None, :])  # ~ key
+            m = torch.full_like(qsq, 1e-9)
+        kth = torch.kthvalue(a, k, dim=1).values[:, None]
+        for j in range(Qc.shape[0]):
+            qi = c0 + j
+            cand = torch.nonzero(a[j] <= kth[j] + 2 * m[j]).flatten().numpy()
+            d = distances(qs[qi], g[cand], metric)
+            o = np.lexsort((cand, d))[:k]
+            out_i[qi], out_d[qi] = cand[o], d[o]
+            p = int(pos[qi])
+            if p >= 0:
+                dp = distances(qs[qi], g[p:p + 1], metric)[0]
+                ap = (dp * dp) if metric == "euclidean" else dp
+                sure = int((a[j] < ap - m[j]).sum())
+                band = torch.nonzero((a[j] >= ap - m[j]) & (a[j] <= ap + m[j])).flatten().numpy()
+                db = distances(qs[qi], g[band], metric)
+                ranks[qi] = sure + int(((db < dp) | ((db == dp) & (band < p))).sum())
+    return out_i, out_d, ranks
 
 
 def find_image_index(image_paths, name: str) -> int:

@@ -1,8 +1,9 @@
 """The N>1 paths on CPU with the gloo backend, world_size 2:
 gradient averaging over the flat gradient buffer (ddp.py), rank-0 parameter
 and BN-buffer broadcast, and the gallery-sharded retrieval protocol of
-knn.knn_sharded (per-shard exact top-k + rank counts -> all_gather/all_reduce
--> merge_topk) against the unsharded oracle."""
+knn.knn_sharded itself (owner's positive key -> all_reduce MAX, per-shard
+exact top-k + rank counts -> all_gather_into_tensor / all_reduce SUM -> merge),
+with CPU stand-ins for the GPU kernels, against the unsharded oracle."""
 import os
 import socket
 import types
@@ -75,45 +76,70 @@ def test_broadcast_parameters_and_buffers():
     _run(_broadcast)
 
 
-def _sharded(rank, k):
+def _cpu_local_search(queries, shard, k, positives, compute, g_base=0, dpos=None, metric="euclidean"):
+    """CPU stand-in of knn.knn for one shard (the oracle's exact keys): the same
+    return contract — global indices padded with -1 / +inf, per-shard rank counts"""
+    from oracle import retrieval as oret
+    qs, g = queries.numpy(), shard.numpy()
+    n = len(g)
+    Q = len(qs)
+    idx = np.full((Q, k), -1, np.int64)
+    dd = np.full((Q, k), np.inf)
+    cnt = np.zeros(Q, np.int64)
+    for i, q in enumerate(qs):
+        d = oret.distances(q, g, metric)
+        ti, td = oret.topk(d, min(k, n))
+        idx[i, :len(ti)] = ti + g_base
+        dd[i, :len(td)] = td
+        if positives is not None and dpos[i] >= 0:
+            gi = np.arange(g_base, g_base + n)
+            p = int(positives[i])
+            cnt[i] = int(((d < dpos[i].item()) | ((d == dpos[i].item()) & (gi < p))).sum())
+    rank = torch.from_numpy(cnt) if positives is not None else None
+    return torch.from_numpy(idx), torch.from_numpy(dd), rank, dpos
+
+
+def _cpu_positive_keys(queries, shard, g_base, positives, metric="euclidean"):
+    from oracle import retrieval as oret
+    out = torch.full((len(queries),), -1.0, dtype=torch.float64)
+    for i, p in enumerate(positives.tolist()):
+        if g_base <= p < g_base + len(shard):
+            out[i] = float(oret.distances(queries[i].numpy(), shard[p - g_base:p - g_base + 1].numpy(), metric)[0])
+    return out
+
+
+def _sharded(rank, k, metric):
+    """knn.knn_sharded's own collective code (all_reduce MAX of the positives' keys,
+    all_gather_into_tensor of the lists, merge, all_reduce SUM of the ranks) over
+    gloo, with CPU stand-ins for the GPU search and merge"""
     import knn
     from oracle import retrieval as oret
     g, qs, pos = oret.synthetic_gallery(1000, 16, 32, seed_g=5, seed_q=6)
     g[900:910] = g[0:10]  # duplicates straddling the shard boundary -> cross-shard ties
     qs[:4] = g[:4]
+    pos = pos.copy()
+    pos[5] = -1  # a query without a positive
     bounds = [0, 537, 1000]  # ragged shards
     lo, hi = bounds[rank], bounds[rank + 1]
-    idx = np.zeros((len(qs), k), np.int64)
-    dd = np.full((len(qs), k), np.inf)
-    cnt = np.zeros(len(qs), np.int64)
+    mi, md, rk = knn.knn_sharded(torch.from_numpy(qs), torch.from_numpy(g[lo:hi]), lo, k, torch.from_numpy(pos),
+                                 metric=metric, local_search=_cpu_local_search, positive_keys=_cpu_positive_keys,
+                                 merge=lambda d, i, kk: knn.merge_topk(list(i), list(d), kk))
     for i, q in enumerate(qs):
-        d_full = oret.l2_distances(q, g)
-        dpos = d_full[pos[i]]  # exact positive distance, shared by the owner shard (all_reduce MAX)
-        d = d_full[lo:hi]
-        ti, td = oret.topk(d, min(k, hi - lo))
-        idx[i, :len(ti)] = ti + lo
-        dd[i, :len(td)] = td
-        if len(ti) < k:
-            idx[i, len(ti):] = -1
-        gi = np.arange(lo, hi)
-        cnt[i] = int(((d < dpos) | ((d == dpos) & (gi < pos[i]))).sum())
-    ti, td, c = torch.from_numpy(idx), torch.from_numpy(dd), torch.from_numpy(cnt)
-    all_i = [torch.empty_like(ti) for _ in range(WORLD)]
-    all_d = [torch.empty_like(td) for _ in range(WORLD)]
-    dist.all_gather(all_i, ti)
-    dist.all_gather(all_d, td)
-    dist.all_reduce(c, op=dist.ReduceOp.SUM)
-    mi, md = knn.merge_topk(all_i, all_d, k)
-    for i, q in enumerate(qs):
-        d_full = oret.l2_distances(q, g)
+        d_full = oret.distances(q, g, metric)
         ri, rd = oret.topk(d_full, k)
         np.testing.assert_array_equal(mi[i].numpy(), ri)
         np.testing.assert_array_equal(md[i].numpy(), rd)
-        assert c[i].item() == oret.rank_of(d_full, pos[i])
+        if pos[i] >= 0:
+            assert rk[i].item() == oret.rank_of(d_full, pos[i])
 
 
 def test_sharded_retrieval_protocol_matches_unsharded_oracle():
-    _run(_sharded, 10)
+    _run(_sharded, 10, "euclidean")
+
+
+def test_sharded_retrieval_protocol_cosine_short_shard():
+    """cosine keys and k = 20 (the lists of both shards are merged by (key, index))"""
+    _run(_sharded, 20, "cosine")
 
 
 def test_merge_topk_short_shards():

@@ -89,9 +89,10 @@ BNB_CASES = [
 
 
 def _bnb_reference(d, kind, ys, means, istds, msc, msh, mask):
-    """g = d*mask, sum g, sum g*xhat_t (f64) for one segment; tensors [n, C]"""
+    """g = d*mask, sum g, sum g*xhat_t (f64) for one segment; tensors [n, C];
+    kind 1 masks with the ReLU's BN applied as (y - mean) * scale + beta"""
     if kind == 1:
-        keep = (ys[0] * msc + msh) > 0
+        keep = ((ys[0] - means[0]) * msc + msh) > 0
     else:
         keep = mask > 0
     g = torch.where(keep, d, torch.zeros_like(d))
@@ -129,7 +130,7 @@ def test_dgrad_fused_bn_reduce(case, cfg, bits, dev, cfg_env):
         draw = draw + 0.25 * F.interpolate(res, scale_factor=2, mode="nearest")
     ys = [torch.randn(N, Ci, H, W, generator=g).bfloat16().float() for _ in range(nt)]
     mask = torch.randn(N, Ci, H, W, generator=g).bfloat16().float()
-    params = torch.randn(G, 4, Ci, generator=g)  # mean, istd, scale, shift per segment
+    params = torch.randn(G, 4, Ci, generator=g)  # BN parameter block per segment: mean, istd, scale, beta
     params[:, 1] = params[:, 1].abs() + 0.5
     params2 = torch.randn(G, 4, Ci, generator=g)
     params2[:, 1] = params2[:, 1].abs() + 0.5
@@ -148,8 +149,7 @@ def test_dgrad_fused_bn_reduce(case, cfg, bits, dev, cfg_env):
     desc.pool = 0
     maskb = _pack_bits(maskd) if bits else None
     desc.mask = (maskb.data_ptr() if bits else maskd.data_ptr()) if kind == 0 else None
-    desc.mask_scale = pd_[0][0, 2].data_ptr() if kind == 1 else None
-    desc.mask_shift = pd_[0][0, 3].data_ptr() if kind == 1 else None
+    desc.mask_bn = pd_[0][0].data_ptr() if kind == 1 else None
     desc.ntarget = nt
     for t in range(nt):
         desc.y[t] = yds[t].data_ptr()
@@ -218,7 +218,12 @@ def test_forward_branches_matches_separate_calls(dtype, dev):
         if "running" in k or "num_batches" in k:
             assert torch.allclose(sa[k].double(), sb[k].double(), atol=tol, rtol=tol), k
     if dtype != torch.float32:
-        return  # bf16 run-to-run gradient noise (atomic order + ReLU flips) is ~15 % on this tiny net
+        # bf16 gradients of the default mode differ run to run by ~15 % on this tiny
+        # net (atomic order -> ReLU flips); the deterministic mode makes the batched
+        # and the separate calls take the same ReLU decisions, so their gradients
+        # must agree up to the weight gradients' split-K summation order
+        _bf16_det_gradients_agree(dev, xs, loss_fn)
+        return
     # per parameter, relative to max(|g|, 1e-4 * the largest gradient anywhere):
     # mathematically-zero gradients (k_proj.bias, c_proj.bias of a triplet loss)
     # are rounding noise of ~1e-8 and must not dominate a global norm
@@ -235,6 +240,29 @@ def test_forward_branches_matches_separate_calls(dtype, dev):
         assert err < 2e-2, (k, err)
 
 
+def _bf16_det_gradients_agree(dev, xs, loss_fn):
+    import engine
+    batched, separate = _models(dev, torch.bfloat16)
+    old = engine.set_deterministic(True)
+    try:
+        batched.train()
+        lb = loss_fn(*batched.forward_branches(xs))
+        lb.backward()
+        separate.train()
+        ls = loss_fn(*[separate(x) for x in xs])
+        ls.backward()
+        torch.cuda.synchronize()
+    finally:
+        engine.set_deterministic(old)
+    assert abs(lb.item() - ls.item()) <= 1e-6 * max(1.0, abs(ls.item())), (lb.item(), ls.item())
+    gb = {k: p.grad for k, p in batched.named_parameters()}
+    gs = {k: p.grad for k, p in separate.named_parameters()}
+    floor = 1e-4 * max(g.norm().item() for g in gs.values())
+    for k, g in gs.items():
+        err = (gb[k] - g).norm().item() / max(g.norm().item(), floor)
+        assert err < 1e-2, (k, err)
+
+
 @pytest.mark.parametrize("C", [64, 256])
 def test_block_out_mask_bits(C, dev):
     """artsbir_block_out_mask: the same output as artsbir_block_out plus its
@@ -243,17 +271,16 @@ def test_block_out_mask_bits(C, dev):
     rows = 3 * 7 * 5
     y3 = torch.randn(rows, C, device=dev, generator=g).bfloat16()
     idn = torch.randn(rows, C, device=dev, generator=g).bfloat16()
-    sc = torch.randn(C, device=dev, generator=g)
-    sh = torch.randn(C, device=dev, generator=g)
+    bn = torch.randn(4, C, device=dev, generator=g)  # mean, istd (unused), scale, beta
     out0 = torch.empty_like(y3)
     out1 = torch.empty_like(y3)
     bits = torch.full((rows, C // 8), 77, dtype=torch.uint8, device=dev)
-    _hip.call("artsbir_block_out", _hip.DT_BF16, y3.data_ptr(), sc.data_ptr(), sh.data_ptr(), None, None, None,
+    _hip.call("artsbir_block_out", _hip.DT_BF16, y3.data_ptr(), bn.data_ptr(), None, None,
               idn.data_ptr(), rows, C, out0.data_ptr(), _hip.stream())
-    _hip.call("artsbir_block_out_mask", _hip.DT_BF16, y3.data_ptr(), sc.data_ptr(), sh.data_ptr(), None, None, None,
+    _hip.call("artsbir_block_out_mask", _hip.DT_BF16, y3.data_ptr(), bn.data_ptr(), None, None,
               idn.data_ptr(), rows, C, out1.data_ptr(), bits.data_ptr(), _hip.stream())
     torch.cuda.synchronize()
     assert torch.equal(out0, out1)
-    ref = torch.relu(y3.float() * sc + sh + idn.float()).bfloat16()
+    ref = torch.relu((y3.float() - bn[0]) * bn[2] + bn[3] + idn.float()).bfloat16()
     assert torch.allclose(out1.float(), ref.float(), atol=3e-2, rtol=1e-2)
     assert torch.equal(bits, _pack_bits(out1))

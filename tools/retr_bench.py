@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Retrieval leg of bench.py alone (1M x 512 gallery, 10k queries, top-10 + rank),
-once per scan kernel: `python tools/retr_bench.py [v1|auto ...]`."""
+once per gallery chunk size: `python tools/retr_bench.py [tiles_per_chunk ...]`
+(0 = the library's default)."""
 import json
 import os
 import sys
@@ -17,10 +18,8 @@ import knn  # noqa: E402
 if __name__ == "__main__":
     dev = torch.device("cuda:0")
     orig = knn.knn
-    for scan in (sys.argv[1:] or ["auto", "v1"]):
-        sc = scan.split("+")[0].split("-")[0]  # e.g. auto, v1, auto-noshare, auto+prepass
-        knn.knn = (lambda *a, _s=sc, _p=(8192 if "+prepass" in scan else 0), _b=("-noshare" not in scan), **kw:
-                   orig(*a, scan=_s, prepass_rows=_p, share_bound=_b, **kw))
+    for tpc in (sys.argv[1:] or ["0"]):
+        knn.knn = (lambda *a, _t=int(tpc), **kw: orig(*a, tiles_per_chunk=_t, **kw))
         r = bench.retrieval_leg(dev, 0, 1)
-        r["scan"] = scan
+        r["tiles_per_chunk"] = int(tpc)
         print(json.dumps(r), flush=True)
