@@ -35,7 +35,8 @@ class BnBwdDesc(ctypes.Structure):
     _fields_ = [("dtype", _c_int), ("kind", _c_int), ("pool", _c_int), ("d", _vp), ("mask", _vp),
                 ("mask_bn", _vp), ("ntarget", _c_int), ("y", _vp * 2),
                 ("mean", _vp * 2), ("istd", _vp * 2), ("slots", _vp * 2), ("coef", _vp * 2), ("dy", _vp * 2),
-                ("gout", _vp), ("B", _c_int), ("H", _c_int), ("W", _c_int), ("C", _c_int)]
+                ("gout", _vp), ("B", _c_int), ("H", _c_int), ("W", _c_int), ("C", _c_int), ("nseg", _c_int),
+                ("pstride", _c_ll), ("cstride", _c_ll), ("sstride", _c_ll)]
 
 
 class AdamTensor(ctypes.Structure):
@@ -52,6 +53,8 @@ SIGNATURES = {
     "artsbir_last_kernel": [],
     "artsbir_tune_save": [ctypes.c_char_p],
     "artsbir_tune_load": [ctypes.c_char_p],
+    "artsbir_stream_create_cu_mask": [ctypes.POINTER(ctypes.c_uint), _c_int, ctypes.POINTER(_vp)],
+    "artsbir_stream_destroy": [_vp],
     "artsbir_conv2d_fwd": [_P, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_conv2d_wgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_gemm_nt": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
@@ -66,9 +69,9 @@ SIGNATURES = {
     "artsbir_bn_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float, _c_float, _c_int,
                             _vp, _vp, _vp, _vp, _vp],
     "artsbir_bn_stats_det": [_c_int, _vp, _c_int, _c_ll, _c_int, _vp, _c_ll, _vp],
-    "artsbir_act_pool": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
-    "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp],
-    "artsbir_block_out_mask": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
+    "artsbir_act_pool": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp],
+    "artsbir_block_out_mask": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_layernorm_fwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp],
     "artsbir_quickgelu": [_c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],

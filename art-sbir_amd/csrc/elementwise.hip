@@ -182,9 +182,11 @@ __device__ __forceinline__ void load_bn8(const float* bn, int C, int c0, float (
   loadf8(bn + 3 * C + c0, b);
 }
 
+// nseg segments (the triplet branches): images b of segment b / (B / nseg) use
+// the parameter block bn + segment * 4 C
 template <typename T>
 __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict__ bn, int relu, int pool, int B,
-                                int H, int W, int C, T* __restrict__ out) {
+                                int H, int W, int C, int nseg, T* __restrict__ out) {
   const int CG = C / 8;
   const int Ho = pool ? H / pool : H, Wo = pool ? W / pool : W;
   const long long n = (long long)B * Ho * Wo * CG;
@@ -196,7 +198,7 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
     int oh = (int)(t % Ho);
     long long b = t / Ho;
     float mn[8], s[8], h[8];
-    if (bn) load_bn8(bn, C, cg * 8, mn, s, h);
+    if (bn) load_bn8(bn + (b / (B / nseg)) * 4 * C, C, cg * 8, mn, s, h);
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int P = pool ? pool : 1;
     for (int dy = 0; dy < P; ++dy)
@@ -222,19 +224,22 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
 template <typename T>
 __global__ void block_out_kernel(const T* __restrict__ y3, const float* __restrict__ bn3, const T* __restrict__ yd,
                                  const float* __restrict__ bnd, const T* __restrict__ idn, long long rows, int C,
-                                 T* __restrict__ out, unsigned char* __restrict__ bits) {
+                                 int nseg, T* __restrict__ out, unsigned char* __restrict__ bits) {
   const int CG = C / 8;
   const long long n = rows * CG;
+  const long long seg_rows = rows / nseg;  // rows of segment s use the blocks + s * 4 C
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     int cg = (int)(i % CG);
-    long long off = (i / CG) * C + cg * 8;
+    const long long row = i / CG;
+    long long off = row * C + cg * 8;
+    const long long po = (row / seg_rows) * 4 * C;
     float a[8], m[8], s[8], h[8], r[8];
     load8<T>(y3 + off, a);
-    load_bn8(bn3, C, cg * 8, m, s, h);
+    load_bn8(bn3 + po, C, cg * 8, m, s, h);
     if (yd) {
       float m2[8], s2[8], h2[8];
       load8<T>(yd + off, r);
-      load_bn8(bnd, C, cg * 8, m2, s2, h2);
+      load_bn8(bnd + po, C, cg * 8, m2, s2, h2);
 #pragma unroll
       for (int e = 0; e < 8; ++e) r[e] = (r[e] - m2[e]) * s2[e] + h2[e];
     } else {
@@ -275,8 +280,32 @@ struct BnBwdArgs {
   const float* coef[2];      // APPLY: [3][C] = c1, c2, c3
   void* dy[2];               // APPLY outputs
   void* gout;                // APPLY optional
-  int B, H, W, C;            // geometry of y (full resolution)
+  int B, H, W, C;            // geometry of y (full resolution), per segment
+  long long pstride, cstride, sstride;  // per-segment strides of mean/istd/mbn, coef, slots (floats)
 };
+
+// segment blockIdx.y of a multi-segment launch: every tensor pointer advanced
+// by whole segments (B images each), the per-channel arrays by their strides
+template <typename T, int POOL>
+__device__ __forceinline__ void bnb_seg(BnBwdArgs& a) {
+  const int s = blockIdx.y;
+  if (s == 0) return;
+  const long long full = (long long)a.B * a.H * a.W * a.C;
+  a.d = reinterpret_cast<const T*>(a.d) + s * (full / (POOL * POOL));
+  if (a.mask)
+    a.mask = a.kind == 3 ? static_cast<const void*>(reinterpret_cast<const unsigned char*>(a.mask) + s * (full / 8))
+                         : static_cast<const void*>(reinterpret_cast<const T*>(a.mask) + s * full);
+  if (a.mbn) a.mbn += s * a.pstride;
+  for (int t = 0; t < 2; ++t) {
+    if (a.y[t]) a.y[t] = reinterpret_cast<const T*>(a.y[t]) + s * full;
+    if (a.dy[t]) a.dy[t] = reinterpret_cast<T*>(a.dy[t]) + s * full;
+    if (a.mean[t]) a.mean[t] += s * a.pstride;
+    if (a.istd[t]) a.istd[t] += s * a.pstride;
+    if (a.coef[t]) a.coef[t] += s * a.cstride;
+    if (a.slots[t]) a.slots[t] += s * a.sstride;
+  }
+  if (a.gout) a.gout = reinterpret_cast<T*>(a.gout) + s * full;
+}
 
 // A "unit" is one pixel, or one 2x2 (pool x pool) quad when the forward pooled
 // after the ReLU: the quad's pooled gradient d is read once and spread over its
@@ -329,6 +358,7 @@ __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, lo
 
 template <typename T, int KIND, int POOL>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int units_per_block) {
+  bnb_seg<T, POOL>(a);
   constexpr int NQ = POOL * POOL;
   const int CG = a.C / 8;
   const int RL = 256 / CG;  // unit lanes
@@ -405,6 +435,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
 // mean(g xhat)) turns into percent-level errors of small channels in parity runs.
 template <typename T, int KIND, int POOL>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_det_kernel(BnBwdArgs a) {
+  bnb_seg<T, POOL>(a);
   constexpr int NQ = POOL * POOL;
   const int CG = a.C / 8;
   const int RL = 256 / CG;
@@ -465,6 +496,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_det_kernel(BnBwdArgs a) {
 
 template <typename T, int KIND, int POOL>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int units_per_block) {
+  bnb_seg<T, POOL>(a);
   constexpr int NQ = POOL * POOL;
   const int CG = a.C / 8;
   const int RL = 256 / CG;
@@ -729,34 +761,36 @@ extern "C" int artsbir_bn_stats_det(int dtype, const void* y, int nseg, long lon
 }
 
 extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W,
-                                int C, void* out, void* stream) {
+                                int C, int nseg, void* out, void* stream) {
   if (C % 8) { set_error("act_pool: C %% 8 != 0"); return -1; }
+  if (nseg < 1 || B % nseg) { set_error("act_pool: %d segments do not split %d images", nseg, B); return -1; }
   if (pool > 1 && (H % pool || W % pool)) { set_error("act_pool: H,W not divisible by pool"); return -1; }
   const int Ho = pool > 1 ? H / pool : H, Wo = pool > 1 ? W / pool : W;
   long long n = (long long)B * Ho * Wo * (C / 8);
   DISPATCH_T(dtype, hipLaunchKernelGGL(act_pool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)x, bn, relu, pool > 1 ? pool : 0, B, H, W, C, (T*)out));
+                                       (const T*)x, bn, relu, pool > 1 ? pool : 0, B, H, W, C, nseg, (T*)out));
   ARTSBIR_CHECK_LAUNCH("act_pool");
   return 0;
 }
 
 extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
-                                      const void* identity, long long rows, int C, void* out,
+                                      const void* identity, long long rows, int C, int nseg, void* out,
                                       unsigned char* mask_bits, void* stream) {
   if (C % 8) { set_error("block_out: C %% 8 != 0"); return -1; }
+  if (nseg < 1 || rows % nseg) { set_error("block_out: %d segments do not split %lld rows", nseg, rows); return -1; }
   if (!yd && !identity) { set_error("block_out: need downsample or identity input"); return -1; }
   if (!bn3 || (yd && !bnd)) { set_error("block_out: missing BN parameter block"); return -1; }
   long long n = rows * (C / 8);
   DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, rows, C,
+                                       (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, rows, C, nseg,
                                        (T*)out, mask_bits));
   ARTSBIR_CHECK_LAUNCH("block_out");
   return 0;
 }
 
 extern "C" int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
-                                 const void* identity, long long rows, int C, void* out, void* stream) {
-  return artsbir_block_out_mask(dtype, y3, bn3, yd, bnd, identity, rows, C, out, nullptr, stream);
+                                 const void* identity, long long rows, int C, int nseg, void* out, void* stream) {
+  return artsbir_block_out_mask(dtype, y3, bn3, yd, bnd, identity, rows, C, nseg, out, nullptr, stream);
 }
 
 static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
@@ -778,16 +812,22 @@ static int fill_bnb(BnBwdArgs& a, const artsbir_bn_bwd_desc* d) {
   }
   a.gout = d->gout;
   a.B = d->B; a.H = d->H; a.W = d->W; a.C = d->C;
+  a.pstride = d->pstride; a.cstride = d->cstride; a.sstride = d->sstride;
+  if (d->nseg > 1 && (d->pstride < 4 * (long long)d->C || d->cstride < 3 * (long long)d->C ||
+                      d->sstride < 2LL * ARTSBIR_NSLOT * d->C)) {
+    set_error("bn_bwd: segment strides below one parameter block");
+    return -1;
+  }
   return 0;
 }
 
 static int g_deterministic = 0;  // artsbir_set_deterministic
 
 template <typename T>
-static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
+static void launch_bnb(const BnBwdArgs& a, int nseg, bool reduce, hipStream_t st) {
   const int P = (a.kind == 1 && a.pool > 1) ? a.pool : 1;
   if (reduce && g_deterministic) {
-#define BNB_DET(K, PP) hipLaunchKernelGGL((bn_bwd_reduce_det_kernel<T, K, PP>), dim3(1), dim3(256), 0, st, a)
+#define BNB_DET(K, PP) hipLaunchKernelGGL((bn_bwd_reduce_det_kernel<T, K, PP>), dim3(1, nseg), dim3(256), 0, st, a)
     if (a.kind == 0) BNB_DET(0, 1);
     else if (a.kind == 2) BNB_DET(2, 1);
     else if (a.kind == 3) BNB_DET(3, 1);
@@ -798,14 +838,14 @@ static void launch_bnb(const BnBwdArgs& a, bool reduce, hipStream_t st) {
   }
   const int units = a.B * (a.H / P) * (a.W / P);
   const int RL = 256 / (a.C / 8);
-  // ~2048 workgroups, each walking a contiguous range of units
-  int upb = (units + 2047) / 2048;
+  // ~2048 workgroups over all segments, each walking a contiguous range of units
+  int upb = (units * nseg + 2047) / 2048;
   if (upb < RL) upb = RL;
   const unsigned grid = (unsigned)((units + upb - 1) / upb);
 #define BNB_LAUNCH(K, PP)                                                                                     \
   do {                                                                                                       \
-    if (reduce) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K, PP>), dim3(grid), dim3(256), 0, st, a, upb);  \
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP>), dim3(grid), dim3(256), 0, st, a, upb);          \
+    if (reduce) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K, PP>), dim3(grid, nseg), dim3(256), 0, st, a, upb); \
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP>), dim3(grid, nseg), dim3(256), 0, st, a, upb);         \
   } while (0)
   if (a.kind == 0) BNB_LAUNCH(0, 1);
   else if (a.kind == 2) BNB_LAUNCH(2, 1);
@@ -824,7 +864,7 @@ extern "C" int artsbir_set_deterministic(int on) {
 extern "C" int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream) {
   BnBwdArgs a;
   if (fill_bnb(a, d)) return -1;
-  DISPATCH_T(d->dtype, launch_bnb<T>(a, true, (hipStream_t)stream));
+  DISPATCH_T(d->dtype, launch_bnb<T>(a, d->nseg > 1 ? d->nseg : 1, true, (hipStream_t)stream));
   ARTSBIR_CHECK_LAUNCH("bn_bwd_reduce");
   return 0;
 }
@@ -832,7 +872,7 @@ extern "C" int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream)
 extern "C" int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream) {
   BnBwdArgs a;
   if (fill_bnb(a, d)) return -1;
-  DISPATCH_T(d->dtype, launch_bnb<T>(a, false, (hipStream_t)stream));
+  DISPATCH_T(d->dtype, launch_bnb<T>(a, d->nseg > 1 ? d->nseg : 1, false, (hipStream_t)stream));
   ARTSBIR_CHECK_LAUNCH("bn_bwd_apply");
   return 0;
 }

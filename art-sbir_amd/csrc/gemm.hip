@@ -738,6 +738,7 @@ static int bnb_reduce_pass(const ConvArgs& a, const artsbir_bn_bwd_desc* bd, hip
   const long long es = bd->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
   for (int s = 0; s < a.nseg; ++s) {
     artsbir_bn_bwd_desc d = *bd;
+    d.nseg = 1;
     const long long eo = s * seg_m * a.Cout * es;  // byte offset of the segment's elements
     const long long po = s * a.bnb_pstride;
     d.pool = 0;
@@ -835,7 +836,11 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     p.x = a.x; p.x_elems = a.x_elems; p.sN = a.sN; p.sH = a.sH; p.sW = a.sW;
     p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
     p.Ho = a.Ho; p.Wo = a.Wo; p.w = a.w; p.Cout = a.Cout; p.K = a.K; p.M = a.M;
-    p.y = a.y; p.ldy = a.ldy; p.stats = a.stats; p.res = a.res; p.res_mode = a.res_mode; p.dbg = 0;
+    p.y = a.y; p.ldy = a.ldy; p.stats = a.stats; p.res = a.res; p.res_mode = a.res_mode;
+    {
+      static const int dbg = getenv("ARTSBIR_PG_DBG") ? atoi(getenv("ARTSBIR_PG_DBG")) : 0;
+      p.dbg = dbg;
+    }
     p.seg_m = a.nseg > 1 ? a.M / a.nseg : 0;
     p.seg_stride = (long long)ARTSBIR_NSLOT * 2 * a.Cout;
     if (bd) {

@@ -44,6 +44,13 @@ namespace artsbir {
 typedef __attribute__((address_space(3))) void* pg_lds_t;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v;
 
+// a wave-uniform 64-bit value the compiler cannot prove uniform (kept in SGPRs)
+__device__ __forceinline__ long long pg_uniform(long long v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(v & 0xffffffffLL));
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((unsigned long long)v >> 32));
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pg_rsrc(const void* base, long long bytes) {
   if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
   if (bytes < 0) bytes = 0;
@@ -63,6 +70,22 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, unsi
       "s_mov_b32 m0, %2\n\t"
       "s_nop 0\n\t"
       "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(base), "s"(r)
+      : "memory");
+}
+
+// the same with 4 B per lane (lds + 4 * lane)
+__device__ __forceinline__ void glds4(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(pg_lds_t)lds);
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dword %1, %3, 0 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(base), "s"(r)
@@ -169,6 +192,136 @@ __device__ __forceinline__ void loadf8v(const float* p, float (&v)[8]) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// ---- epilogue operands staged in LDS (after the main loop the stage ring is
+// free): the tile's [BPX pixels][BCH channels] slice of y_0, the residual, y_1
+// and the bf16 mask are brought in by LDS-DMA, every wave's instructions in
+// flight at once (one round trip per tile instead of one per pixel batch), then
+// read from LDS by the epilogue lanes.  Row r of an operand holds its BCH/8
+// 16-B chunks in slot order chunk ^ (r % (BCH/8)) (swizzle applied to the DMA
+// source addresses), so the epilogue's reads (16 rows x one chunk per
+// ds_read_b128 phase) hit 16 distinct 16-B bank groups.
+struct EpiStage {
+  const char* y0;   // nullptr: read from global memory
+  const char* res;
+  const char* y1;
+  const char* mk;
+  const unsigned char* bits;  // kind 3: [BPX][BCH/8] mask bytes
+  const float* prm;           // BNB: [2 segments][7][BCH] per-channel BN constants (pg_prm_fill)
+  long long seg0;             // segment of the tile's first pixel
+};
+
+// BN-backward constants of the tile's channels for its (at most two) segments,
+// in LDS before the main loop so the epilogue reads no global memory for them:
+// rows istd_0, mean_0, istd_1, mean_1, mask mean, mask scale, mask beta
+constexpr int PG_PRM_ROWS = 7;
+template <int BCH>
+constexpr int pg_prm_bytes() {  // padded to a whole number of 512-thread passes
+  return (2 * PG_PRM_ROWS * BCH + 511) / 512 * 512 * 4;
+}
+
+template <int BCH, int NT>
+__device__ __forceinline__ void pg_prm_fill(const PgArgs& a, float* prm, long long bpx, int bch, long long seg0) {
+  // a fixed trip count (a divergent loop exit here pushes the kernel's later
+  // uniform values into VGPRs, which the LDS-DMA asm cannot take)
+  constexpr int NE = 2 * PG_PRM_ROWS * BCH;
+  const long long nseg = a.seg_m > 0 ? a.M / a.seg_m : 1;
+  const bool two = a.bnb_nt == 2, msk = a.bnb == 1;
+  // the source rows as wave-uniform pointers (selecting among the fields of the
+  // by-value argument struct per lane would move it to scratch)
+  const float* rows[PG_PRM_ROWS];
+  rows[0] = reinterpret_cast<const float*>(pg_uniform((long long)a.bnb_istd[0]));
+  rows[1] = reinterpret_cast<const float*>(pg_uniform((long long)a.bnb_mean[0]));
+  rows[2] = two ? reinterpret_cast<const float*>(pg_uniform((long long)a.bnb_istd[1])) : rows[0];
+  rows[3] = two ? reinterpret_cast<const float*>(pg_uniform((long long)a.bnb_mean[1])) : rows[0];
+  const float* mb = msk ? reinterpret_cast<const float*>(pg_uniform((long long)a.bnb_mbn)) : rows[0];
+  rows[4] = mb;
+  rows[5] = msk ? mb + 2 * a.Cout : rows[0];
+  rows[6] = msk ? mb + 3 * a.Cout : rows[0];
+  static_assert(pg_prm_bytes<BCH>() / 4 % NT == 0, "whole passes");
+#pragma unroll
+  for (int k = 0; k < pg_prm_bytes<BCH>() / 4 / NT; ++k) {
+    const int i = k * NT + (int)threadIdx.x;
+    const int s = i / (PG_PRM_ROWS * BCH), r = (i / BCH) % PG_PRM_ROWS, c = i % BCH;
+    long long sg = seg0 + s;
+    if (sg >= nseg) sg = nseg - 1;
+    const int ch = bch + c;
+    const bool have = i < NE && ch < a.Cout && (r < 2 || (r < 4 && two) || (r >= 4 && msk));
+    // every lane loads from a valid address (channel 0 of row 0) and selects
+    const float* src = rows[0];
+#pragma unroll
+    for (int q = 1; q < PG_PRM_ROWS; ++q) src = r == q ? rows[q] : src;
+    const float v = src[have ? sg * a.bnb_pstride + ch : 0];
+    prm[i] = have ? v : 0.f;
+  }
+}
+
+// DMA of the tile's block-output mask bits (kind 3): row r = BCH/8 bytes
+template <int BPX, int BCH, int NW>
+__device__ __forceinline__ void stage_bits(const void* bits, unsigned char* lds, long long bpx, int bch,
+                                           const PgArgs& a, int wid, int lane) {
+  constexpr int LPR = BCH / 32;  // dwords (lanes) per row
+  constexpr int RPI = 64 / LPR;
+  constexpr int NI = (BPX + RPI - 1) / RPI;
+  const long long rowb = a.Cout >> 3;
+  const __amdgpu_buffer_rsrc_t r = pg_rsrc(reinterpret_cast<const unsigned char*>(pg_uniform((long long)bits)) +
+                                               pg_uniform(bpx) * rowb, (a.M - pg_uniform(bpx)) * rowb);
+  const int w = lane % LPR;
+#pragma unroll
+  for (int i = wid; i < NI; i += NW) {
+    const int row = i * RPI + lane / LPR;
+    const long long px = bpx + row;
+    const unsigned off = (row < BPX && px < a.M && bch + 32 * w < a.Cout)
+                             ? (unsigned)(row * rowb + (bch >> 3) + 4 * w) : PG_OOB;
+    glds4(r, reinterpret_cast<char*>(lds) + i * 256, off);
+  }
+}
+
+template <int BCH>
+__device__ __forceinline__ Vec16<bf16> stg_read(const char* base, int row, int chunk) {
+  constexpr int CPR = BCH / 8;
+  return ld16<bf16>(reinterpret_cast<const bf16*>(base + row * (BCH * 2) + ((chunk ^ (row & (CPR - 1))) << 4)));
+}
+
+// DMA of one operand slice: rows bpx .. bpx+BPX-1 (source row index src_row(px)),
+// channels bch .. bch+BCH-1 of a bf16 [rows][ld] tensor; res_pool: the
+// AvgPool2d(2)-backward residual, row px reads pooled row (img, oh/2, ow/2)
+template <int BPX, int BCH, int NW>
+__device__ __forceinline__ void stage_operand(const void* t, long long t_rows, int ld, char* lds, long long bpx,
+                                              int bch, const PgArgs& a, bool res_pool, int wid, int lane) {
+  constexpr int CPR = BCH / 8;
+  constexpr int RPI = 64 / CPR;  // rows per DMA instruction
+  constexpr int NI = BPX / RPI;
+  static_assert(CPR <= 64 && 64 % CPR == 0, "stage rows");
+  const int HoWo = a.Ho * a.Wo;
+  auto src_row = [&](long long px) -> long long {
+    if (!res_pool) return px;
+    const long long img = px / HoWo;
+    const int rem = (int)(px - img * HoWo);
+    const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+    return (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+  };
+  // lowest source row of the tile (pooled rows are not monotone inside an
+  // output row pair: row oh+1 maps back to pooled row oh/2), so start the
+  // descriptor at column 0 of the first pixel's row
+  long long r0;
+  {
+    const long long p0 = bpx < a.M ? bpx : a.M - 1;
+    r0 = pg_uniform(res_pool ? src_row(p0 - (p0 % HoWo) % a.Wo) : p0);
+  }
+  const __amdgpu_buffer_rsrc_t r =
+      pg_rsrc(reinterpret_cast<const bf16*>(pg_uniform((long long)t)) + r0 * ld, (t_rows - r0) * (long long)ld * 2);
+  const int pos = lane % CPR;
+#pragma unroll
+  for (int i = wid; i < NI; i += NW) {
+    const int row = i * RPI + lane / CPR;
+    const int c = pos ^ (row & (CPR - 1));
+    const long long px = bpx + row;
+    const int ch = bch + 8 * c;
+    const unsigned off = (px < a.M && ch < a.Cout) ? (unsigned)(((src_row(px) - r0) * ld + ch) * 2) : PG_OOB;
+    glds16(r, lds + i * 1024, off);
+  }
+}
+
 // LDS accumulator half of the wave's segment (0: the tile's first segment)
 __device__ __forceinline__ int stats_rseg(const PgArgs& a, long long bpx, long long wave_px0) {
   if (a.seg_m <= 0) return 0;
@@ -193,7 +346,8 @@ constexpr int pg_red_bytes() {
 // tile's LDS accumulator (stats_flush writes it out).
 template <bool BNB, int BCH, int MTC, int NTP, int WTPX, int WTCH, int EJB = 2>
 __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
-                                            int wpx, int wch, int fr, int fq, float* red) {
+                                            int wpx, int wch, int fr, int fq, float* red,
+                                            const EpiStage& sg = EpiStage{nullptr, nullptr, nullptr, nullptr}) {
   const int HoWo = a.Ho * a.Wo;
   const long long wpx0 = bpx + wpx * WTPX;
   float* rb = red + stats_rseg(a, bpx, wpx0) * 3 * BCH;
@@ -214,29 +368,38 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
     // a batch go out together and are waited for once, not one round trip each
     const int chc = chok ? ch0 : 0;
     // BN-backward per-channel constants: xhat_t = y * xa_t + xb_t; mask affine
-    float xa0[8], xb0[8], xa1[8], xb1[8], mm[8], ms[8], mh[8];
+    // xhat_t = (y - m_t) * xa_t (the mean subtracted first: f32-exact for |mean| >> std)
+    float xa0[8], m0[8], xa1[8], m1[8], mm[8], ms[8], mh[8];
     if constexpr (BNB) {
-      const long long po = wseg * a.bnb_pstride + chc;
-      float m0[8], m1[8];
-      loadf8v(a.bnb_istd[0] + po, xa0);
-      loadf8v(a.bnb_mean[0] + po, m0);
-      if (two) {
-        loadf8v(a.bnb_istd[1] + po, xa1);
-        loadf8v(a.bnb_mean[1] + po, m1);
+      if (sg.prm) {  // the tile's constants in LDS (pg_prm_fill)
+        const float* pp = sg.prm + (int)(wseg - sg.seg0) * PG_PRM_ROWS * BCH + (chc - bch);
+        loadf8v(pp, xa0);
+        loadf8v(pp + BCH, m0);
+        loadf8v(pp + 2 * BCH, xa1);
+        loadf8v(pp + 3 * BCH, m1);
+        loadf8v(pp + 4 * BCH, mm);
+        loadf8v(pp + 5 * BCH, ms);
+        loadf8v(pp + 6 * BCH, mh);
       } else {
+        const long long po = wseg * a.bnb_pstride + chc;
+        loadf8v(a.bnb_istd[0] + po, xa0);
+        loadf8v(a.bnb_mean[0] + po, m0);
+        if (two) {
+          loadf8v(a.bnb_istd[1] + po, xa1);
+          loadf8v(a.bnb_mean[1] + po, m1);
+        } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { xa1[e] = 0.f; m1[e] = 0.f; }
+          for (int e = 0; e < 8; ++e) { xa1[e] = 0.f; m1[e] = 0.f; }
+        }
+        if (a.bnb == 1) {  // parameter block of the BN feeding the ReLU: mean, -, scale, beta
+          loadf8v(a.bnb_mbn + po, mm);
+          loadf8v(a.bnb_mbn + po + 2 * a.Cout, ms);
+          loadf8v(a.bnb_mbn + po + 3 * a.Cout, mh);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { mm[e] = 0.f; ms[e] = 0.f; mh[e] = 0.f; }
+        }
       }
-      if (a.bnb == 1) {  // parameter block of the BN feeding the ReLU: mean, -, scale, beta
-        loadf8v(a.bnb_mbn + po, mm);
-        loadf8v(a.bnb_mbn + po + 2 * a.Cout, ms);
-        loadf8v(a.bnb_mbn + po + 3 * a.Cout, mh);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { mm[e] = 0.f; ms[e] = 0.f; mh[e] = 0.f; }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { xb0[e] = -m0[e] * xa0[e]; xb1[e] = -m1[e] * xa1[e]; }
     }
     // pixel tiles in batches of EJ: loads of the batch first, then the math
     constexpr int EJ = NTP >= EJB ? EJB : 1;
@@ -249,24 +412,35 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
       for (int u = 0; u < EJ; ++u) {
         const long long px = wpx0 + (j0 + u) * 16 + fr;
         const long long pc = px < a.M ? px : a.M - 1;
-        rsc[u] = 1.f;
+        const int srow = (int)(pc - bpx), schunk = chok ? (chc - bch) >> 3 : 0;  // staged-operand coordinates
+        rsc[u] = a.res_mode == 2 ? 0.25f : 1.f;
         if (a.res_mode) {
-          long long ri = pc;
-          if (a.res_mode == 2) {
-            const long long img = pc / HoWo;
-            const int rem = (int)(pc - img * HoWo);
-            const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-            ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
-            rsc[u] = 0.25f;
+          if (sg.res) {
+            rv[u] = stg_read<BCH>(sg.res, srow, schunk);
+          } else {
+            long long ri = pc;
+            if (a.res_mode == 2) {
+              const long long img = pc / HoWo;
+              const int rem = (int)(pc - img * HoWo);
+              const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+              ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+            }
+            rv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + chc);
           }
-          rv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + chc);
         }
         if constexpr (BNB) {
           const long long off = pc * a.ldy + chc;
-          y0v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + off);
-          if (a.bnb == 2) mkv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + off);
-          if (a.bnb == 3) mbits[u] = reinterpret_cast<const unsigned char*>(a.bnb_mask)[pc * (a.Cout >> 3) + (chc >> 3)];
-          if (two) y1v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + off);
+          y0v[u] = sg.y0 ? stg_read<BCH>(sg.y0, srow, schunk)
+                         : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + off);
+          if (a.bnb == 2)
+            mkv[u] = sg.mk ? stg_read<BCH>(sg.mk, srow, schunk)
+                           : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + off);
+          if (a.bnb == 3)
+            mbits[u] = sg.bits ? sg.bits[srow * (BCH / 8) + schunk]
+                               : reinterpret_cast<const unsigned char*>(a.bnb_mask)[pc * (a.Cout >> 3) + (chc >> 3)];
+          if (two)
+            y1v[u] = sg.y1 ? stg_read<BCH>(sg.y1, srow, schunk)
+                           : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + off);
         }
       }
 #pragma unroll
@@ -294,11 +468,11 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
                                              : to_f(mkv[u].v[e]) > 0.f;
               v[e] = keep ? v[e] : 0.f;
               s1[e] += v[e];
-              s2[e] += v[e] * (yv * xa0[e] + xb0[e]);
+              s2[e] += v[e] * ((yv - m0[e]) * xa0[e]);
             }
             if (two) {
 #pragma unroll
-              for (int e = 0; e < 8; ++e) s3[e] += v[e] * (to_f(y1v[u].v[e]) * xa1[e] + xb1[e]);
+              for (int e = 0; e < 8; ++e) s3[e] += v[e] * ((to_f(y1v[u].v[e]) - m1[e]) * xa1[e]);
             }
           }
           Vec16<bf16> o;
@@ -330,8 +504,147 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
   }
 }
 
-template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB>
+// The epilogue of pgemm_kernel, specialised at compile time on what the launch
+// fuses (the generic pg_epilogue above decides per element at run time, which
+// cost ~840 scalar branches in the unrolled epilogue and most of the fused
+// kernels' time).  BK: 0 plain (forward statistics / data gradient, residual at
+// run time), 1 ACT (mask (y_0 - m) * s + b > 0, no residual), 2 / 3 RES (block-
+// output mask as bf16 / as bits, residual always present); TWO: a second BN
+// target; S_RES / S_Y1 / S_MK: that operand is staged in LDS (else read from
+// global memory in batches of EJB pixel tiles); y_0 and the mask bits of BK 3
+// are always staged, the BN constants always come from the LDS table.
+template <int BK, bool TWO, bool S_RES, bool S_Y1, bool S_MK, int BCH, int MTC, int NTP, int WTPX, int WTCH,
+          int EJB = 2>
+__device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
+                                              int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg) {
+  constexpr bool BNB = BK != 0;
+  constexpr bool RESK = BK == 2 || BK == 3;
+  const int HoWo = a.Ho * a.Wo;
+  const long long wpx0 = bpx + wpx * WTPX;
+  float* rb = red + stats_rseg(a, bpx, wpx0) * 3 * BCH;
+  const long long wseg = a.seg_m > 0 ? (wpx0 < a.M ? wpx0 : a.M - 1) / a.seg_m : 0;
+  const bool sums = BNB || a.stats != nullptr;
+  const bool res = RESK || (BK == 0 && a.res_mode != 0);
+  const float rsc = a.res_mode == 2 ? 0.25f : 1.f;
+#pragma unroll
+  for (int p = 0; p < MTC / 2; ++p) {
+    const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+    const bool chok = ch0 < a.Cout;
+    const int chc = chok ? ch0 : 0;
+    const int schunk = chok ? (ch0 - bch) >> 3 : 0;
+    float s1[8], s2[8], s3[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+    // BN constants (LDS table): xhat_t = (y - m_t) * xa_t; ACT mask (y - mm) * ms + mh > 0
+    float xa0[8], m0[8], xa1[8], m1[8], mm[8], ms[8], mh[8];
+    if constexpr (BNB) {
+      const float* pp = sg.prm + (int)(wseg - sg.seg0) * PG_PRM_ROWS * BCH + (chc - bch);
+      loadf8v(pp, xa0);
+      loadf8v(pp + BCH, m0);
+      if constexpr (TWO) { loadf8v(pp + 2 * BCH, xa1); loadf8v(pp + 3 * BCH, m1); }
+      if constexpr (BK == 1) { loadf8v(pp + 4 * BCH, mm); loadf8v(pp + 5 * BCH, ms); loadf8v(pp + 6 * BCH, mh); }
+    }
+    constexpr bool GLOBAL_OPS = (RESK && !S_RES) || (TWO && !S_Y1) || (BK == 2 && !S_MK) || BK == 0;
+    constexpr int EJ = (GLOBAL_OPS && NTP >= EJB) ? EJB : 1;
+#pragma unroll
+    for (int j0 = 0; j0 < NTP; j0 += EJ) {
+      Vec16<bf16> rv[EJ], y0v[EJ], mkv[EJ], y1v[EJ];
+      unsigned mbits[EJ];
+#pragma unroll
+      for (int u = 0; u < EJ; ++u) {  // operands of the batch (global loads issued together)
+        const long long px = wpx0 + (j0 + u) * 16 + fr;
+        const long long pc = px < a.M ? px : a.M - 1;
+        const int srow = (int)(pc - bpx);
+        if (RESK || BK == 0) {
+          if (S_RES && RESK) {
+            rv[u] = stg_read<BCH>(sg.res, srow, schunk);
+          } else if (BK == 0 && sg.res) {  // plain data gradient: residual staged at run time
+            rv[u] = stg_read<BCH>(sg.res, srow, schunk);
+          } else if (res) {
+            long long ri = pc;
+            if (a.res_mode == 2) {
+              const long long img = pc / HoWo;
+              const int rem = (int)(pc - img * HoWo);
+              const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+              ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+            }
+            rv[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + chc);
+          }
+        }
+        if constexpr (BNB) {
+          y0v[u] = stg_read<BCH>(sg.y0, srow, schunk);
+          if constexpr (BK == 2)
+            mkv[u] = S_MK ? stg_read<BCH>(sg.mk, srow, schunk)
+                          : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + pc * a.ldy + chc);
+          if constexpr (BK == 3) mbits[u] = sg.bits[srow * (BCH / 8) + schunk];
+          if constexpr (TWO)
+            y1v[u] = S_Y1 ? stg_read<BCH>(sg.y1, srow, schunk)
+                          : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + pc * a.ldy + chc);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EJ; ++u) {
+        const long long px = wpx0 + (j0 + u) * 16 + fr;
+        const bool ok = px < a.M && chok;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j0 + u][r]; v[4 + r] = acc[2 * p + 1][j0 + u][r]; }
+        if (RESK || (BK == 0 && res)) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += rsc * to_f(rv[u].v[e]);
+        }
+        if constexpr (BNB) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float yv = to_f(y0v[u].v[e]);
+            bool keep;
+            if constexpr (BK == 1) keep = (yv - mm[e]) * ms[e] + mh[e] > 0.f;
+            else if constexpr (BK == 3) keep = ((mbits[u] >> e) & 1u) != 0u;
+            else keep = to_f(mkv[u].v[e]) > 0.f;
+            v[e] = (keep && ok) ? v[e] : 0.f;  // tail rows/channels add nothing to the sums
+            s1[e] += v[e];
+            s2[e] += v[e] * ((yv - m0[e]) * xa0[e]);
+            if constexpr (TWO) s3[e] += v[e] * ((to_f(y1v[u].v[e]) - m1[e]) * xa1[e]);
+          }
+        } else if (a.stats) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float w = ok ? v[e] : 0.f;
+            s1[e] += w;
+            s2[e] += w * w;
+          }
+        }
+        if (ok) {
+          Vec16<bf16> o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+          st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+        }
+      }
+    }
+    if (sums) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
+      if constexpr (TWO) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s3[e] = dpp_row_sum(s3[e]);
+      }
+      if (fr == 15 && chok) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(rb + (ch0 - bch) + e, s1[e]);
+          atomicAdd(rb + BCH + (ch0 - bch) + e, s2[e]);
+          if constexpr (TWO) atomicAdd(rb + 2 * BCH + (ch0 - bch) + e, s3[e]);
+        }
+      }
+    }
+  }
+}
+
+// BK (0 / 1 / 2 / 3, see pg_epilogue_k) and TWO select the fused epilogue.
+template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO>
 __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
+  constexpr bool BNB = BK != 0;
   constexpr int NW = WPX * WCH;
   constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
   constexpr int IPX = BPX / (8 * NW);
@@ -343,9 +656,14 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   constexpr int LPS_LO = IPX + ICH_TOT / NW;                   // ... waves with one fewer
   static_assert(IPX >= 1 && IPX * 8 * NW == BPX, "pixel loader");
   static_assert(MTC % 2 == 0 && WTCH % 32 == 0, "channel pairs");
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + pg_red_bytes<BCH>()];
+  // stage ring | BN statistics accumulator | (BNB) BN constants | (BNB) mask bits
+  constexpr int XTRA = BNB ? pg_prm_bytes<BCH>() + BPX * (BCH / 8) : 0;
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + pg_red_bytes<BCH>() + XTRA];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 6 * BCH * 4);
+  float* prm = reinterpret_cast<float*>(smem + NSTAGE * STAGE + pg_red_bytes<BCH>());
+  unsigned char* sbits = reinterpret_cast<unsigned char*>(smem + NSTAGE * STAGE + pg_red_bytes<BCH>() +
+                                                          pg_prm_bytes<BCH>());
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -355,6 +673,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   const long long lid = pg_xcd_remap(blockIdx.x, ntp * ntc);
   const long long bpx = (lid / ntc) * BPX;
   const int bch = (int)(lid % ntc) * BCH;
+  const long long seg0 = a.seg_m > 0 ? bpx / a.seg_m : 0;
+  if constexpr (BNB) pg_prm_fill<BCH, 64 * NW>(a, prm, bpx, bch, seg0);  // published by the main loop's barriers
   const int HoWo = a.Ho * a.Wo;
   const long long img0 = bpx / HoWo;
   const __amdgpu_buffer_rsrc_t xr =
@@ -484,9 +804,57 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     compute(kt % NSTAGE);
   }
 
-  // ---- epilogue from registers
+  // ---- epilogue operands into the (now free) stage ring by LDS-DMA: slot 0
+  // y_0, then the residual, y_1 and the bf16 mask as far as the ring holds them
+  constexpr int OPB = BPX * BCH * 2;            // bytes of one staged operand
+  constexpr int NOP = (NSTAGE * STAGE) / OPB;   // operands that fit
+  constexpr bool RESK = BK == 2 || BK == 3;
+  constexpr bool S_RES = RESK && NOP >= 2;
+  constexpr bool S_Y1 = TWO && NOP >= 2 + (S_RES ? 1 : 0);
+  constexpr bool S_MK = BK == 2 && NOP >= 2 + (S_RES ? 1 : 0) + (S_Y1 ? 1 : 0);
+  static_assert(!BNB || NOP >= 1, "y_0 must fit the stage ring");
+  EpiStage sg{nullptr, nullptr, nullptr, nullptr, nullptr, BNB ? prm : nullptr, seg0};
+  if constexpr (BNB) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is done reading the stages
+    const long long rows = a.M;
+    int n = 0;
+    sg.y0 = smem;
+    stage_operand<BPX, BCH, NW>(a.bnb_y[0], rows, a.ldy, smem, bpx, bch, a, false, wid, lane);
+    ++n;
+    if constexpr (S_RES) {
+      sg.res = smem + n * OPB;
+      stage_operand<BPX, BCH, NW>(a.res, a.res_mode == 2 ? rows / 4 : rows, a.ldy, smem + n * OPB, bpx, bch, a,
+                                  a.res_mode == 2, wid, lane);
+      ++n;
+    }
+    if constexpr (S_Y1) {
+      sg.y1 = smem + n * OPB;
+      stage_operand<BPX, BCH, NW>(a.bnb_y[1], rows, a.ldy, smem + n * OPB, bpx, bch, a, false, wid, lane);
+      ++n;
+    }
+    if constexpr (S_MK) {
+      sg.mk = smem + n * OPB;
+      stage_operand<BPX, BCH, NW>(a.bnb_mask, rows, a.ldy, smem + n * OPB, bpx, bch, a, false, wid, lane);
+      ++n;
+    }
+    if constexpr (BK == 3) {
+      sg.bits = sbits;
+      stage_bits<BPX, BCH, NW>(a.bnb_mask, sbits, bpx, bch, a, wid, lane);
+    }
+    vm_wait<0>();
+    __syncthreads();  // every wave's DMA has landed
+  } else if (a.res_mode) {  // plain data gradient with a residual: stage it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    sg.res = smem;
+    stage_operand<BPX, BCH, NW>(a.res, a.res_mode == 2 ? a.M / 4 : a.M, a.ldy, smem, bpx, bch, a, a.res_mode == 2,
+                                wid, lane);
+    vm_wait<0>();
+    __syncthreads();
+  }
   const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
-  pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
+  pg_epilogue_k<BK, TWO, S_RES, S_Y1, S_MK, BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, red, sg);
   if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
 }
 
@@ -1187,16 +1555,36 @@ static const PgCfg kCfgs[] = {
     {256, 32, 4 * (256 + 32) * 128, 512, 0.70f},    // 4: 256 x 32, 4 stages
 };
 
-template <bool MULTI, bool BNB>
+template <bool MULTI, int BK, bool TWO>
 static void pg_launch_cfg(int c, const PgArgs& a, long long tiles, hipStream_t st) {
   const dim3 g((unsigned)tiles);
   switch (c) {
-    case 0: hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 2, 2, MULTI, BNB>), g, dim3(512), 0, st, a); break;
-    case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, MULTI, BNB>), g, dim3(512), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, MULTI, BNB>), g, dim3(512), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, MULTI, BNB>), g, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI, BNB>), g, dim3(512), 0, st, a); break;
+    case 0: hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 2, 2, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, MULTI, BK, TWO>), g, dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
   }
+}
+
+// the fused-epilogue variant of a launch: ACT (kind 1, one target, no
+// residual) or RES (kinds 2/3, residual present, one or two targets)
+template <bool MULTI>
+static bool pg_launch_bnb(int c, const PgArgs& a, long long tiles, hipStream_t st) {
+  if (a.bnb == 1) {
+    if (a.bnb_nt != 1 || a.res_mode) return false;
+    pg_launch_cfg<MULTI, 1, false>(c, a, tiles, st);
+    return true;
+  }
+  if (MULTI || !a.res_mode) return false;  // RES dgrads: 1x1 convs over >= 64 channels, residual added
+  if (a.bnb == 3) {
+    if (a.bnb_nt == 2) pg_launch_cfg<false, 3, true>(c, a, tiles, st);
+    else pg_launch_cfg<false, 3, false>(c, a, tiles, st);
+  } else {
+    if (a.bnb_nt == 2) pg_launch_cfg<false, 2, true>(c, a, tiles, st);
+    else pg_launch_cfg<false, 2, false>(c, a, tiles, st);
+  }
+  return true;
 }
 
 template <bool MULTI, bool BNB>
@@ -1254,14 +1642,13 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
                                       "pgemm_kernel<128,128>", "pgemm_kernel<256,32>"},
                                      {"pgemm_kernel<256,256,bnb>", "pgemm_kernel<256,128,bnb>", "pgemm_kernel<256,64,bnb>",
                                       "pgemm_kernel<128,128,bnb>", "pgemm_kernel<256,32,bnb>"}};
-  set_last_kernel(names[a.bnb ? 1 : 0][c]);
   if (a.bnb) {
-    if (multi) pg_launch_cfg<true, true>(c, a, tiles, st);
-    else pg_launch_cfg<false, true>(c, a, tiles, st);
+    if (!(multi ? pg_launch_bnb<true>(c, a, tiles, st) : pg_launch_bnb<false>(c, a, tiles, st))) return false;
   } else {
-    if (multi) pg_launch_cfg<true, false>(c, a, tiles, st);
-    else pg_launch_cfg<false, false>(c, a, tiles, st);
+    if (multi) pg_launch_cfg<true, 0, false>(c, a, tiles, st);
+    else pg_launch_cfg<false, 0, false>(c, a, tiles, st);
   }
+  set_last_kernel(names[a.bnb ? 1 : 0][c]);
   return true;
 }
 

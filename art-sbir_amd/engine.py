@@ -66,6 +66,35 @@ def set_deterministic(on: bool = True) -> bool:
     return old
 
 
+# ARTSBIR_SIDE_CUS=K: the weight-gradient stream is restricted to K CUs (0: all)
+SIDE_CUS = [int(os.environ.get("ARTSBIR_SIDE_CUS", "0"))]
+# measurement switch (never set in a real step): leave the weight gradients out
+SKIP_WGRAD = [False]
+_MASKED_STREAMS = {}
+
+
+def cu_masked_stream(device, ncu):
+    """a torch stream over a hipExtStreamCreateWithCUMask stream using ncu CUs
+    spread evenly over the device's CUs (cached per (device, ncu))"""
+    key = (device.index if device.index is not None else 0, ncu)
+    st = _MASKED_STREAMS.get(key)
+    if st is not None:
+        return st
+    total = torch.cuda.get_device_properties(device).multi_processor_count
+    ncu = max(1, min(ncu, total))
+    words = (total + 31) // 32
+    mask = (ctypes.c_uint * words)()
+    for i in range(ncu):
+        cu = (i * total) // ncu
+        mask[cu // 32] |= 1 << (cu % 32)
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        call("artsbir_stream_create_cu_mask", mask, words, ctypes.byref(handle))
+    st = torch.cuda.ExternalStream(handle.value, device=device)
+    _MASKED_STREAMS[key] = st
+    return st
+
+
 def _fuse_bnb():
     """BN-backward reductions fused into the data-gradient epilogues (f32 atomics)
     except in the deterministic mode, which reduces them in a fixed order"""
@@ -281,11 +310,11 @@ class Engine:
         p = max(pool, 1)
         out = self._empty(B, H // p, W // p, C, device=x.device)
         G = bn.G if bn is not None else 1
-        Bs = B // G
-        for s in range(G):
-            sb = bn.seg(s) if bn is not None else None
-            call("artsbir_act_pool", self.dt, _at(x, s * Bs), ptr(sb.block) if sb else None, relu, pool, Bs, H, W,
-                 C, _at(out, s * Bs), _s())
+        # one launch for all G segments (segment s normalised with its own BN block)
+        call("artsbir_act_pool", self.dt, ptr(x), ptr(bn.block) if bn is not None else None, relu, pool, B, H, W,
+             C, G, ptr(out), _s(), kernel="act_pool_kernel",
+             nbytes=float(x.element_size() * B * C * (H * W + (H // p) * (W // p))),
+             tag=f"act_pool {B}x{H}x{W}x{C} pool{pool}")
         return out
 
     # ---------------------------------------------------------------- forward
@@ -367,13 +396,12 @@ class Engine:
         bits = None
         if train and _fuse_bnb() and MASK_BITS and self.dt == _hip.DT_BF16:
             bits = torch.empty(out.numel() // 8, dtype=torch.uint8, device=out.device)
-        for g in range(G):
-            s3 = b3.seg(g)
-            sd = bd.seg(g) if bd is not None else None
-            call("artsbir_block_out_mask", self.dt, _at(y3, g * Bs), ptr(s3.block),
-                 _at(yd, g * Bs), ptr(sd.block) if sd else None,
-                 None if yd is not None else _at(h, g * Bs), rows, C, _at(out, g * Bs),
-                 (bits.data_ptr() + g * rows * (C // 8)) if bits is not None else None, _s())
+        call("artsbir_block_out_mask", self.dt, ptr(y3), ptr(b3.block), ptr(yd), ptr(bd.block) if bd else None,
+             None if yd is not None else ptr(h), rows * G, C, G, ptr(out),
+             bits.data_ptr() if bits is not None else None, _s(),
+             kernel="block_out_kernel", nbytes=float(out.element_size() * rows * G * C * 3 + (rows * G * C // 8 if bits
+                                                                                                  is not None else 0)),
+             tag=f"block_out {rows * G}x{C}")
         ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, bits=bits, b1=b1, b2=b2, b3=b3,
                    bd=bd)
         return out, ctx
@@ -469,44 +497,52 @@ class Engine:
         call("artsbir_tokens_bwd", self.dt, ptr(dtok), B, P, C, ptr(dh), _s())
         return dh
 
+    def _seg_desc(self, kind, pool, targets, Bs, H, W, C):
+        """a BN-backward descriptor covering all G segments in one launch
+        (tensors advance by Bs images per segment, parameters by one block)"""
+        desc = _hip.BnBwdDesc()
+        desc.dtype = self.dt
+        desc.kind = kind
+        desc.pool = pool
+        desc.ntarget = len(targets)
+        for i, (y, st) in enumerate(targets):
+            desc.y[i] = ptr(y)
+            desc.mean[i] = ptr(st.mean)
+            desc.istd[i] = ptr(st.istd)
+        desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
+        desc.nseg = self._G
+        desc.pstride, desc.cstride, desc.sstride = 4 * C, 3 * C, 2 * NSLOT * C
+        return desc
+
     def _bn_bwd(self, kind, d, targets, bnmods, ws, grads, mask=None, mask_bn=None, pool=0, gout=None):
-        """BatchNorm backward as a reduce pass + apply pass per segment.
-        targets: list of (y, BNState); returns list of dy tensors"""
+        """BatchNorm backward as a reduce pass + apply pass, each one launch over
+        all G segments.  targets: list of (y, BNState); returns list of dy tensors"""
         y0 = targets[0][0]
         B, H, W, C = y0.shape
         G = self._G
         Bs = B // G
         dys = [torch.empty_like(y) for y, _ in targets]
-        per = 2 * NSLOT * C
         slots = [ws.take(C * G) for _ in targets]  # [G][NSLOT][2][C] per target
-        descs = []
-        for s in range(G):  # every segment's reduction first ...
-            desc = _hip.BnBwdDesc()
-            desc.dtype = self.dt
-            desc.kind = kind
-            desc.pool = pool
-            desc.d = _at(d, s * Bs)
-            desc.mask = _at(mask, s * Bs)
-            mb = mask_bn.seg(s) if mask_bn is not None else None
-            desc.mask_bn = ptr(mb.block) if mb else None
-            desc.ntarget = len(targets)
-            for i, (y, st) in enumerate(targets):
-                ss = st.seg(s)
-                desc.y[i] = _at(y, s * Bs)
-                desc.mean[i] = ptr(ss.mean)
-                desc.istd[i] = ptr(ss.istd)
-                desc.slots[i] = ptr(slots[i][s * per:])
-            desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
-            call("artsbir_bn_bwd_reduce", desc, _s())
-            descs.append(desc)
-        # ... then one finalisation per target for all segments, then the applies
+        desc = self._seg_desc(kind, pool, targets, Bs, H, W, C)
+        desc.d = ptr(d)
+        desc.mask = ptr(mask)
+        desc.mask_bn = ptr(mask_bn.block) if mask_bn is not None else None
+        for i in range(len(targets)):
+            desc.slots[i] = ptr(slots[i])
+        call("artsbir_bn_bwd_reduce", desc, _s(), kernel=f"bn_bwd_reduce_kernel<{kind}>",
+             nbytes=float(y0.element_size() * B * H * W * C * (1.0 / max(pool, 1) ** 2 + len(targets)
+                                                                 + (1 if kind == 0 else 0))),
+             tag=f"bn_bwd_reduce k{kind} {B}x{H}x{W}x{C} t{len(targets)}")
+        # one finalisation per target for all segments, then the apply
         coefs = self._bn_coefs(targets, bnmods, slots, grads, float(Bs * H * W))
-        for s, desc in enumerate(descs):
-            for i in range(len(targets)):
-                desc.coef[i] = ptr(coefs[i][s])
-                desc.dy[i] = _at(dys[i], s * Bs)
-            desc.gout = _at(gout, s * Bs)
-            call("artsbir_bn_bwd_apply", desc, _s())
+        for i in range(len(targets)):
+            desc.coef[i] = ptr(coefs[i])
+            desc.dy[i] = ptr(dys[i])
+        desc.gout = ptr(gout)
+        call("artsbir_bn_bwd_apply", desc, _s(), kernel=f"bn_bwd_apply_kernel<{kind}>",
+             nbytes=float(y0.element_size() * B * H * W * C * (1.0 / max(pool, 1) ** 2 + 2 * len(targets)
+                                                                 + (1 if gout is not None else 0))),
+             tag=f"bn_bwd_apply k{kind} {B}x{H}x{W}x{C} t{len(targets)}")
         return dys
 
     def _bn_coefs(self, targets, bnmods, slots, grads, count):
@@ -546,7 +582,8 @@ class Engine:
         return desc, slots, targets
 
     def _bn_finish(self, g, fused, bnmods, grads):
-        """apply pass of a fused BN-backward: g (masked) -> dy per target"""
+        """apply pass of a fused BN-backward: g (masked) -> dy per target, one
+        launch over all G segments"""
         _, slots, targets = fused
         y0 = targets[0][0]
         B, H, W, C = y0.shape
@@ -554,28 +591,27 @@ class Engine:
         Bs = B // G
         dys = [torch.empty_like(y) for y, _ in targets]
         coefs = self._bn_coefs(targets, bnmods, slots, grads, float(Bs * H * W))
-        for s in range(G):
-            desc = _hip.BnBwdDesc()
-            desc.dtype = self.dt
-            desc.kind = 2
-            desc.pool = 0
-            desc.d = _at(g, s * Bs)
-            desc.ntarget = len(targets)
-            for i, (y, st) in enumerate(targets):
-                ss = st.seg(s)
-                desc.y[i] = _at(y, s * Bs)
-                desc.mean[i] = ptr(ss.mean)
-                desc.istd[i] = ptr(ss.istd)
-                desc.coef[i] = ptr(coefs[i][s])
-                desc.dy[i] = _at(dys[i], s * Bs)
-            desc.B, desc.H, desc.W, desc.C = Bs, H, W, C
-            call("artsbir_bn_bwd_apply", desc, _s())
+        desc = self._seg_desc(2, 0, targets, Bs, H, W, C)
+        desc.d = ptr(g)
+        for i in range(len(targets)):
+            desc.coef[i] = ptr(coefs[i])
+            desc.dy[i] = ptr(dys[i])
+        call("artsbir_bn_bwd_apply", desc, _s(), kernel="bn_bwd_apply_kernel<2>",
+             nbytes=float(y0.element_size() * B * H * W * C * (1 + 2 * len(targets))),
+             tag=f"bn_bwd_apply k2 {B}x{H}x{W}x{C} t{len(targets)}")
         return dys
 
     def _side_stream(self, device):
+        """the weight-gradient stream; with SIDE_CUS > 0 it may only use that many
+        CUs (spread evenly over the chip), so the main stream's HBM-bound chain
+        always finds free CUs while the MFMA-bound weight gradients run beside it"""
         st = getattr(self, "_side", None)
-        if st is None or st.device != device:
-            st = self._side = torch.cuda.Stream(device=device)
+        if st is None or st.device != device or getattr(self, "_side_cus", None) != SIDE_CUS[0]:
+            if SIDE_CUS[0] > 0:
+                st = self._side = cu_masked_stream(device, SIDE_CUS[0])
+            else:
+                st = self._side = torch.cuda.Stream(device=device)
+            self._side_cus = SIDE_CUS[0]
         return st
 
     def _wgrad(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):
@@ -583,6 +619,8 @@ class Engine:
         input and accumulates into its own slice of the gradient buffer, so it
         runs concurrently with the (HBM-bound) data-gradient / BatchNorm chain
         of the main stream; backward() joins the streams at the end."""
+        if SKIP_WGRAD[0]:  # measurement only (tools/cu_mask_sweep.py): the main stream's critical path
+            return
         if not OVERLAP_WGRAD:
             return self._wgrad_sync(dy, a, conv, stride, pad, grads, ci_pad)
         main = torch.cuda.current_stream()

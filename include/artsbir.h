@@ -42,6 +42,12 @@ const char* artsbir_last_kernel(void);
  * launches).  load returns the number of entries read, or -1. */
 int artsbir_tune_save(const char* path);
 int artsbir_tune_load(const char* path);
+/* A HIP stream restricted to the CUs set in mask (bit i of word w = CU 32w+i;
+ * hipExtStreamCreateWithCUMask) and its release.  The training step runs its
+ * MFMA-bound weight gradients on such a stream beside the HBM-bound data-gradient
+ * chain (engine.py).  *out receives the hipStream_t. */
+int artsbir_stream_create_cu_mask(const unsigned* mask, int nwords, void** out);
+int artsbir_stream_destroy(void* stream);
 
 /* ---- convolution / linear (models.py:198-221,310-319 nn.Conv2d; models.py:243-246 nn.Linear) */
 
@@ -138,17 +144,19 @@ int artsbir_bn_finalize_seg(const float* stats, int nseg, long long seg_stride, 
  * run to run (the conv epilogues' atomics are not). */
 int artsbir_bn_stats_det(int dtype, const void* y, int nseg, long long rows, int C, float* stats,
                          long long seg_stride, void* stream);
-/* out = avgpool_pool( relu?(bn(x)) ), bn = a [4][C] parameter block (NULL: no affine). */
+/* out = avgpool_pool( relu?(bn(x)) ), bn = a [4][C] parameter block (NULL: no affine).
+ * nseg segments of B/nseg images (the triplet branches): segment s uses bn + s*4*C. */
 int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W, int C,
-                     void* out, void* stream);
-/* Bottleneck tail (models.py:234-235): out = relu(bn3(y3) + (bn_d(yd) | identity)). */
+                     int nseg, void* out, void* stream);
+/* Bottleneck tail (models.py:234-235): out = relu(bn3(y3) + (bn_d(yd) | identity));
+ * nseg segments of rows/nseg rows, segment s with the blocks + s*4*C. */
 int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
-                      const void* identity, long long rows, int C, void* out, void* stream);
+                      const void* identity, long long rows, int C, int nseg, void* out, void* stream);
 /* The same, also writing the block output's ReLU mask as bits: mask_bits[row][C/8],
  * bit e of byte c = out[row][8c+e] > 0 (the backward's kind-3 mask: 1/16 of the
  * bytes of re-reading out). */
 int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
-                           const void* identity, long long rows, int C, void* out, unsigned char* mask_bits,
+                           const void* identity, long long rows, int C, int nseg, void* out, unsigned char* mask_bits,
                            void* stream);
 
 /* BatchNorm2d(train) backward, see elementwise.hip for the math. */
@@ -169,7 +177,12 @@ struct artsbir_bn_bwd_desc {
   const float* coef[2];   /* apply: [3][C] from artsbir_bn_bwd_finalize */
   void* dy[2];            /* apply outputs */
   void* gout;             /* apply: optional copy of g */
-  int B, H, W, C;
+  int B, H, W, C;         /* per segment */
+  /* nseg > 1: one launch for nseg consecutive segments (the triplet branches):
+   * tensors advance by B*H*W*C elements per segment (d by its pooled size, mask
+   * bits by /8), mean/istd/mask_bn by pstride, coef by cstride, slots by sstride floats */
+  int nseg;
+  long long pstride, cstride, sstride;
 };
 int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
 /* Deterministic mode for parity runs: artsbir_bn_bwd_reduce then sums

@@ -276,9 +276,9 @@ def test_block_out_mask_bits(C, dev):
     out1 = torch.empty_like(y3)
     bits = torch.full((rows, C // 8), 77, dtype=torch.uint8, device=dev)
     _hip.call("artsbir_block_out", _hip.DT_BF16, y3.data_ptr(), bn.data_ptr(), None, None,
-              idn.data_ptr(), rows, C, out0.data_ptr(), _hip.stream())
+              idn.data_ptr(), rows, C, 1, out0.data_ptr(), _hip.stream())
     _hip.call("artsbir_block_out_mask", _hip.DT_BF16, y3.data_ptr(), bn.data_ptr(), None, None,
-              idn.data_ptr(), rows, C, out1.data_ptr(), bits.data_ptr(), _hip.stream())
+              idn.data_ptr(), rows, C, 1, out1.data_ptr(), bits.data_ptr(), _hip.stream())
     torch.cuda.synchronize()
     assert torch.equal(out0, out1)
     ref = torch.relu((y3.float() - bn[0]) * bn[2] + bn[3] + idn.float()).bfloat16()

@@ -6,7 +6,7 @@ mkdir -p $R/gpurun_out
 cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/gpu_tests.log
-bash gpurun_pmc.sh || exit 1
+bash tools/gpu/pmc_traffic.sh || exit 1
 python3 profiles/summarize_pmc.py gpurun_out/pmc_train gpurun_out/pmc_retr profiles/r1_pmc_traffic.json
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { echo BENCH_FAILED; tail -20 gpurun_out/bench_full.err; exit 1; }
 cp profiles/r1_pmc_traffic.json gpurun_out/r1_pmc_traffic.json
