@@ -356,7 +356,7 @@ __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, lo
   }
 }
 
-template <typename T, int KIND, int POOL>
+template <typename T, int KIND, int POOL, int NT>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int units_per_block) {
   bnb_seg<T, POOL>(a);
   constexpr int NQ = POOL * POOL;
@@ -367,16 +367,17 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
   const int units = a.B * (a.H / POOL) * (a.W / POOL);
   const int u0 = blockIdx.x * units_per_block;
   const int u1 = min(u0 + units_per_block, units);
-  float acc[2][2][8];
+  float acc[NT][2][8];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[t][q][e] = 0.f;
   if (rl < RL) {
-    float mn[2][8], is[2][8], mm[8], ms[8], mh[8];
-    for (int t = 0; t < a.ntarget; ++t) { loadf8(a.mean[t] + cg * 8, mn[t]); loadf8(a.istd[t] + cg * 8, is[t]); }
+    float mn[NT][8], is[NT][8], mm[8], ms[8], mh[8];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) { loadf8(a.mean[t] + cg * 8, mn[t]); loadf8(a.istd[t] + cg * 8, is[t]); }
     if constexpr (KIND == 1) load_bn8(a.mbn, a.C, cg * 8, mm, ms, mh);
     for (int u = u0 + rl; u < u1; u += RL) {
       long long offs[NQ];
@@ -386,8 +387,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
         if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + offs[0], g[0]);
       }
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        if (t >= a.ntarget) break;
+      for (int t = 0; t < NT; ++t) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
           float y[8];
@@ -404,7 +404,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
   // reduce over unit lanes in LDS, then one atomic per channel per block
   __shared__ float red[256 * 8];
   const int slot = blockIdx.x % ARTSBIR_NSLOT;
-  for (int t = 0; t < a.ntarget; ++t)
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
     for (int q = 0; q < 2; ++q) {
       __syncthreads();
 #pragma unroll
@@ -494,7 +496,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_det_kernel(BnBwdArgs a) {
     }
 }
 
-template <typename T, int KIND, int POOL>
+// NT (targets) is a template parameter so every per-target array is indexed
+// statically (a run-time target count put them in scratch memory)
+template <typename T, int KIND, int POOL, int NT>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int units_per_block) {
   bnb_seg<T, POOL>(a);
   constexpr int NQ = POOL * POOL;
@@ -506,8 +510,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
   const int units = a.B * (a.H / POOL) * (a.W / POOL);
   const int u0 = blockIdx.x * units_per_block;
   const int u1 = min(u0 + units_per_block, units);
-  float mn[2][8], is[2][8], c1[2][8], c2[2][8], c3[2][8], mm[8], ms[8], mh[8];
-  for (int t = 0; t < a.ntarget; ++t) {
+  const T* yp[NT];
+  T* dyp[NT];
+  float mn[NT][8], is[NT][8], c1[NT][8], c2[NT][8], c3[NT][8], mm[8], ms[8], mh[8];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    yp[t] = reinterpret_cast<const T*>(a.y[t]);
+    dyp[t] = reinterpret_cast<T*>(a.dy[t]);
     loadf8(a.mean[t] + cg * 8, mn[t]);
     loadf8(a.istd[t] + cg * 8, is[t]);
     loadf8(a.coef[t] + cg * 8, c1[t]);
@@ -515,25 +524,40 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
     loadf8(a.coef[t] + 2 * a.C + cg * 8, c3[t]);
   }
   if constexpr (KIND == 1) load_bn8(a.mbn, a.C, cg * 8, mm, ms, mh);
-  for (int u = u0 + rl; u < u1; u += RL) {
-    long long offs[NQ];
-    float g[NQ][8];
-    bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, mm, ms, mh);
-    if (a.gout) {
+  T* const gout = reinterpret_cast<T*>(a.gout);
+  // UN units per trip, every load of the trip issued before its first store
+  // (the compiler cannot prove the stores alias none of the loads), so a lane
+  // keeps UN units' bytes in flight instead of one
+  constexpr int UN = POOL == 1 ? (NT == 1 ? 4 : 2) : 1;
+  for (int ub = u0 + rl; ub < u1; ub += RL * UN) {
+    long long offs[UN][NQ];
+    float g[UN][NQ][8], y[UN][NT][NQ][8];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) store8<T>(reinterpret_cast<T*>(a.gout) + offs[q], g[q]);
+    for (int i = 0; i < UN; ++i) {
+      const int u = min(ub + i * RL, u1 - 1);  // clamped: a tail unit recomputes the last one, stored once
+      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs[i], g[i], mm, ms, mh);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) load8<T>(yp[t] + offs[i][q], y[i][t][q]);
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (t >= a.ntarget) break;
+    for (int i = 0; i < UN; ++i) {
+      if (ub + i * RL >= u1) break;
+      if (gout) {
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float y[8], o[8];
-        load8<T>(reinterpret_cast<const T*>(a.y[t]) + offs[q], y);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = c1[t][e] * (g[q][e] - c2[t][e] - (y[e] - mn[t][e]) * is[t][e] * c3[t][e]);
-        store8<T>(reinterpret_cast<T*>(a.dy[t]) + offs[q], o);
+        for (int q = 0; q < NQ; ++q) store8<T>(gout + offs[i][q], g[i][q]);
       }
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          float o[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            o[e] = c1[t][e] * (g[i][q][e] - c2[t][e] - (y[i][t][q][e] - mn[t][e]) * is[t][e] * c3[t][e]);
+          store8<T>(dyp[t] + offs[i][q], o);
+        }
     }
   }
 }
@@ -844,8 +868,12 @@ static void launch_bnb(const BnBwdArgs& a, int nseg, bool reduce, hipStream_t st
   const unsigned grid = (unsigned)((units + upb - 1) / upb);
 #define BNB_LAUNCH(K, PP)                                                                                     \
   do {                                                                                                       \
-    if (reduce) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K, PP>), dim3(grid, nseg), dim3(256), 0, st, a, upb); \
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP>), dim3(grid, nseg), dim3(256), 0, st, a, upb);         \
+    if (reduce && a.ntarget == 2)                                                                            \
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K, PP, 2>), dim3(grid, nseg), dim3(256), 0, st, a, upb);   \
+    else if (reduce) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, K, PP, 1>), dim3(grid, nseg), dim3(256), 0, st, a, upb); \
+    else if (a.ntarget == 2)                                                                                 \
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP, 2>), dim3(grid, nseg), dim3(256), 0, st, a, upb);    \
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, K, PP, 1>), dim3(grid, nseg), dim3(256), 0, st, a, upb); \
   } while (0)
   if (a.kind == 0) BNB_LAUNCH(0, 1);
   else if (a.kind == 2) BNB_LAUNCH(2, 1);

@@ -641,6 +641,88 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
   }
 }
 
+// ---- BN statistics carried across the tiles of a persistent workgroup.  A
+// lane's channels (wch, p, fq) are the same in every tile of the workgroup that
+// shares the tile's channel block bch, so the lane adds its pixels' y and y^2
+// into registers tile after tile; only when the wave's (segment, bch) changes,
+// and at the end, are the 16 pixel lanes reduced (DPP) and added to the global
+// statistics slot.  Per tile that leaves 2 FMAs per output value instead of the
+// DPP reduction, LDS atomics and the block flush of pg_epilogue.
+template <int NP>
+struct WaveStats {
+  float s1[NP][8], s2[NP][8];
+  int seg;  // -1: empty
+  int bch;
+};
+
+template <int NP>
+__device__ __forceinline__ void wstats_zero(WaveStats<NP>& w) {
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { w.s1[p][e] = 0.f; w.s2[p][e] = 0.f; }
+}
+
+template <int NP, int WTCH>
+__device__ __forceinline__ void wstats_flush(WaveStats<NP>& w, const PgArgs& a, int wch, int fr, int fq, int slot) {
+  if (w.seg < 0) return;
+  const long long so = (long long)w.seg * a.seg_stride + (long long)slot * 2 * a.Cout;
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int ch0 = w.bch + wch * WTCH + 32 * p + 8 * fq;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { w.s1[p][e] = dpp_row_sum(w.s1[p][e]); w.s2[p][e] = dpp_row_sum(w.s2[p][e]); }
+    if (fr == 15 && ch0 < a.Cout) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(a.stats + so + ch0 + e, w.s1[p][e]);
+        atomicAdd(a.stats + so + a.Cout + ch0 + e, w.s2[p][e]);
+      }
+    }
+  }
+  wstats_zero(w);
+  w.seg = -1;
+}
+
+// forward epilogue with carried statistics: store the tile, add its values to w
+template <int BCH, int MTC, int NTP, int WTPX, int WTCH>
+__device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
+                                                int wpx, int wch, int fr, int fq, WaveStats<MTC / 2>& w, int slot) {
+  const long long wpx0 = bpx + wpx * WTPX;
+  if (wpx0 >= a.M) return;  // a wave past the last pixel of the tail tile
+  const int seg = a.seg_m > 0 ? (int)(wpx0 / a.seg_m) : 0;
+  if (seg != w.seg || bch != w.bch) {
+    wstats_flush<MTC / 2, WTCH>(w, a, wch, fr, fq, slot);
+    w.seg = seg;
+    w.bch = bch;
+  }
+#pragma unroll
+  for (int p = 0; p < MTC / 2; ++p) {
+    const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+    const bool chok = ch0 < a.Cout;
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const long long px = wpx0 + j * 16 + fr;
+      const bool ok = px < a.M && chok;
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float u = ok ? v[e] : 0.f;
+        w.s1[p][e] += u;
+        w.s2[p][e] += u * u;
+      }
+      if (ok) {
+        Vec16<bf16> o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+        st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+      }
+    }
+  }
+}
+
 // BK (0 / 1 / 2 / 3, see pg_epilogue_k) and TWO select the fused epilogue.
 template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO>
 __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
@@ -868,7 +950,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
 // tile's epilogue stores drain, which is what the low-K layers (1-5 K-steps
 // per tile) need to stream at HBM rate.
 // ---------------------------------------------------------------------------
-template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB>
+// FWDS: forward with BN statistics (carried across tiles, pg_epilogue_fwd)
+template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS>
 __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int BPX = 256, NWC = 8, NWL = 4;
   static_assert(WPX * WCH == NWC, "compute waves");
@@ -993,7 +1076,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   }
 
   // -------------------------------------------------------------- compute
-  const bool sums = BNB || a.stats != nullptr;
+  const bool sums = !FWDS && (BNB || a.stats != nullptr);
   if (sums) {  // ordered before any use by the first stage barrier
     for (int i = tid; i < 6 * BCH; i += 64 * NWC) red[i] = 0.f;
     if (tid == 0) *red_cnt = 0;
@@ -1005,6 +1088,11 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   for (int i = 0; i < MTC; ++i)
 #pragma unroll
     for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  WaveStats<MTC / 2> ws;  // forward statistics carried across tiles (pg_epilogue_fwd)
+  wstats_zero(ws);
+  ws.seg = -1;
+  ws.bch = -1;
+  const int wslot = (int)((blockIdx.x * NWC + wid) % ARTSBIR_NSLOT);
   for (int s = 0; s < total; ++s) {
     // retire this wave's LDS reads of the slot the next issue overwrites
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1041,15 +1129,20 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
     const long long bpx = (t / ntc) * BPX;
     const int bch = (int)(t % ntc) * BCH;
     const int slot = (int)(t % ARTSBIR_NSLOT);
-    pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH, 1>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
-    // the flushing wave zeroes red before it reaches the next stage barrier,
-    // and no wave adds for tile ti+1 before passing that barrier
-    if (sums) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane, bpx, BPX);
+    if constexpr (FWDS) {
+      pg_epilogue_fwd<BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, ws, wslot);
+    } else {
+      pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH, 1>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
+      // the flushing wave zeroes red before it reaches the next stage barrier,
+      // and no wave adds for tile ti+1 before passing that barrier
+      if (sums) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane, bpx, BPX);
+    }
 #pragma unroll
     for (int i = 0; i < MTC; ++i)
 #pragma unroll
       for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  if constexpr (FWDS) wstats_flush<MTC / 2, WTCH>(ws, a, wch, fr, fq, wslot);
 }
 
 // ---------------------------------------------------------------------------
@@ -1587,11 +1680,13 @@ static bool pg_launch_bnb(int c, const PgArgs& a, long long tiles, hipStream_t s
   return true;
 }
 
-template <bool MULTI, bool BNB>
+template <bool MULTI, bool BNB, bool FWDS>
 static void pstream_launch(int bch, const PgArgs& a, int grid, int ntl, hipStream_t st) {
-  if (bch == 32) hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, MULTI, BNB>), dim3(grid), dim3(768), 0, st, a, ntl);
-  else if (bch == 64) hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, MULTI, BNB>), dim3(grid), dim3(768), 0, st, a, ntl);
-  else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, MULTI, BNB>), dim3(grid), dim3(768), 0, st, a, ntl);
+  if (bch == 32)
+    hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, MULTI, BNB, FWDS>), dim3(grid), dim3(768), 0, st, a, ntl);
+  else if (bch == 64)
+    hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, MULTI, BNB, FWDS>), dim3(grid), dim3(768), 0, st, a, ntl);
+  else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, MULTI, BNB, FWDS>), dim3(grid), dim3(768), 0, st, a, ntl);
 }
 
 static bool pg_supported(const PgArgs& a, bool& multi) {
@@ -1626,11 +1721,14 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
                                        {"pstream_kernel<32,bnb>", "pstream_kernel<64,bnb>", "pstream_kernel<128,bnb>"}};
     set_last_kernel(pnames[a.bnb ? 1 : 0][bch == 32 ? 0 : bch == 64 ? 1 : 2]);
     if (a.bnb) {
-      if (multi) pstream_launch<true, true>(bch, a, grid, ntl, st);
-      else pstream_launch<false, true>(bch, a, grid, ntl, st);
+      if (multi) pstream_launch<true, true, false>(bch, a, grid, ntl, st);
+      else pstream_launch<false, true, false>(bch, a, grid, ntl, st);
+    } else if (a.stats) {
+      if (multi) pstream_launch<true, false, true>(bch, a, grid, ntl, st);
+      else pstream_launch<false, false, true>(bch, a, grid, ntl, st);
     } else {
-      if (multi) pstream_launch<true, false>(bch, a, grid, ntl, st);
-      else pstream_launch<false, false>(bch, a, grid, ntl, st);
+      if (multi) pstream_launch<true, false, false>(bch, a, grid, ntl, st);
+      else pstream_launch<false, false, false>(bch, a, grid, ntl, st);
     }
     return true;
   }
