@@ -173,7 +173,7 @@ __device__ __forceinline__ void stats_flush(float* red, int* cnt, int last_count
       const int ch = bch + i - m * BCH;
       const float v = rr[i];
       rr[i] = 0.f;
-      if (ch >= a.Cout) continue;
+      if (ch >= a.Cout || (a.dbg & 1)) continue;  // dbg 1: timing experiment without the global atomics
       if (!a.bnb) {
         atomicAdd(a.stats + so + m * a.Cout + ch, v);
       } else if (m == 0) {
@@ -622,7 +622,7 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
         }
       }
     }
-    if (sums) {
+    if (sums && !(a.dbg & 2)) {  // dbg 2: timing experiment without the statistics reduction
 #pragma unroll
       for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
       if constexpr (TWO) {

@@ -14,7 +14,13 @@
                         by crc32(path)): photos uniform [0,1), sketches 90 % white
                         / 10 % black strokes correlated with their photo, both
                         through the CLIP normalize of models.py:294.
-  get_datasets          data_preparation.py:796-848 factory ("Synthetic*").
+  SyntheticKaggleInferenceDataset  stands in for KaggleInferenceDatasetV1
+                        (data_preparation.py:696-722): sketches only ("data/kaggle/
+                        <sketch_type>/<photo-stem>-k<n>.png", every tenth one for a
+                        photo outside the gallery), __getitem__ -> [sketch]
+  get_datasets          data_preparation.py:796-848 factory ("Synthetic*" — the name
+                        may carry "Kaggle" / "Mixed", which selects the reference's
+                        Kaggle/Mixed behaviour downstream — and "KaggleInferenceV1").
 """
 from __future__ import annotations
 
@@ -70,8 +76,9 @@ class InferenceDataset(Dataset):
 
 class SyntheticTripletDataset(Dataset):
     def __init__(self, n: int = 256, resolution: int = 224, mode: str = "train", split_ratio: float = 0.1,
-                 size: float = 1.0, seed: int = 42, transform=None, dups: int = 1):
+                 size: float = 1.0, seed: int = 42, transform=None, dups: int = 1, name: str = None):
         super().__init__()
+        self.name = name or self.__class__.__name__
         if mode not in ("train", "test"):
             raise ValueError("invalid mode: [train, test]")
         random.seed(seed)
@@ -103,16 +110,54 @@ class SyntheticTripletDataset(Dataset):
 
     @property
     def state_dict(self) -> Dict:
-        return {"dataset": f"{self.__class__.__name__}", "size": self.size, "img_number": len(self),
+        return {"dataset": self.name, "size": self.size, "img_number": len(self),
                 "img_type": "synthetic", "img_format": "jpg", "sketch_format": "png", "seed": self.seed,
                 "split_ratio": self.split_ratio, "mode": self.mode, "transform": str(self.transform)}
+
+
+class SyntheticKaggleInferenceDataset(Dataset):
+    def __init__(self, photo_paths: List[Path], sketch_type: str = 'sketches', sketch_format: str = 'png',
+                 transform=None, resolution: int = 224):
+        super().__init__()
+        self.sketch_type, self.sketch_format, self.transform = sketch_type, sketch_format, transform
+        self.resolution = resolution
+        root = Path("data/kaggle") / sketch_type
+        photos = list(dict.fromkeys(photo_paths))
+        self.sketch_paths, self.photo_of = [], []
+        for i, p in enumerate(photos):
+            stem = Path(p).stem if i % 10 != 9 else f"nogallery{i:05d}"
+            self.sketch_paths.append(root / f"{stem}-k{i % 3 + 1}.{sketch_format}")
+            self.photo_of.append(p)
+
+    def __len__(self):
+        return len(self.sketch_paths)
+
+    def sketch(self, idx):
+        return synthetic_sketch(self.sketch_paths[idx], self.photo_of[idx], self.resolution)
+
+    def __getitem__(self, idx):
+        return [self.sketch(idx)]
+
+    @property
+    def state_dict(self):
+        return {"dataset": "KaggleInferenceDatasetV1", "img_number": len(self), "sketch_type": self.sketch_type,
+                "sketch_format": self.sketch_format, "transform": str(self.transform), "date": "synthetic"}
+
+
+_LAST_TEST = [None]  # the gallery the Kaggle inference sketches refer to (the reference: data/kaggle on disk)
 
 
 def get_datasets(dataset: str = "Synthetic", size: float = 1.0, sketch_format: str = 'png', img_format: str = 'jpg',
                  sketch_type: str = 'placeholder', img_type: str = 'photos', split_ratio: float = 0.1, seed: int = 42,
                  transform=None, n: int = 256, resolution: int = 224, **kw):
     if dataset.startswith("Synthetic"):
-        tr = SyntheticTripletDataset(n, resolution, "train", split_ratio, size, seed, transform)
-        te = SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform)
+        name = None if dataset == "Synthetic" else dataset  # e.g. "SyntheticKaggleV1", "SyntheticMixedV1"
+        tr = SyntheticTripletDataset(n, resolution, "train", split_ratio, size, seed, transform, name=name)
+        te = SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform, name=name)
+        _LAST_TEST[0] = te
         return tr, te
+    if dataset in ('KaggleInferenceV1', 'KaggleInferencedatasetV1'):
+        te = _LAST_TEST[0] or SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform)
+        return None, SyntheticKaggleInferenceDataset(te.photo_paths, sketch_type, sketch_format, transform,
+                                                     te.resolution)
     raise Exception(f"{dataset} is not available (no datasets ship with this build; use Synthetic)")

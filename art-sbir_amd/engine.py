@@ -178,6 +178,9 @@ class Engine:
         self._packed_key = None
         self.dtype = torch.float32
         self._G = 1
+        # ddp.OverlappedReducer (or None): told which gradient ranges are final
+        # as the backward proceeds, so the data-parallel all-reduce overlaps it
+        self.grad_hook = None
 
     # ------------------------------------------------------------------ utils
     @property
@@ -450,13 +453,28 @@ class Engine:
         grads = self.grad_buffer(dev)
         ws = _Arena(torch.zeros(max(2 * NSLOT * m.total_bn_channels() * 2 * G, 1), dtype=torch.float32, device=dev),
                     NSLOT * 2)
+        # the hook only sees a backward that carries every branch of the step
+        # (one batched multi-branch pass); per-branch backwards accumulate and
+        # are reduced after the last one by the hook's finish()
+        hook = self.grad_hook if G > 1 else None
+        streams = [torch.cuda.current_stream()] + ([self._side_stream(dev)] if OVERLAP_WGRAD else [])
+        if hook is not None:
+            hook.begin(grads.flat)
         dh = self._attnpool_bwd(m.attnpool, pk, ctx["attn"], dout.contiguous().float(), grads)
         blocks, bps, cs = m.blocks(), pk["blocks"], ctx["blocks"]
+        if hook is not None:
+            hook.ready(_param_ranges(grads, m.attnpool.parameters()), streams)
         fused = None
         for i in reversed(range(len(blocks))):
             prev = (blocks[i - 1], cs[i - 1]) if i > 0 else None
             dh, fused = self._block_bwd(blocks[i], bps[i], cs[i], dh, grads, ws, fused, prev)
+            # block i+1 is final once block i is enqueued (block i's backward
+            # still finishes the BN reduction handed over by block i+1)
+            if hook is not None and i + 1 < len(blocks):
+                hook.ready(_param_ranges(grads, blocks[i + 1].parameters()), streams)
         self._stem_bwd(m, pk, ctx["stem"], dh, grads, ws)
+        if hook is not None:
+            hook.end(streams)  # block 0, the stem and anything unreported
         if OVERLAP_WGRAD:
             torch.cuda.current_stream().wait_stream(self._side_stream(dev))
         return grads
@@ -768,6 +786,18 @@ class _Arena:
         if self.off > self.buf.numel():
             raise RuntimeError("statistics arena overflow")
         return v
+
+
+def _param_ranges(grads, params):
+    """[lo, hi) element ranges of the gradient buffer holding params' gradients"""
+    base = grads.flat.data_ptr()
+    es = grads.flat.element_size()
+    out = []
+    for p in params:
+        v = grads[p]
+        lo = (v.data_ptr() - base) // es
+        out.append((lo, lo + v.numel()))
+    return out
 
 
 class GradBuffer:

@@ -6,7 +6,9 @@ Same functions and result dictionary as the reference:
   compute_image_features inference.py:72-92   (eval-mode gallery embedding, batches of 50)
   process_inference      inference.py:94-136  (rank+1, MRR, topk_acc, describe() stats,
                                                10 retrieval samples chosen by random.seed(11))
-  run_inference          inference.py:140-165
+  run_inference          inference.py:140-165 (+ the Kaggle/Mixed second pass with the
+                                               Kaggle inference sketches, inference.py:154-163)
+  run_inference_sharded  the same with the gallery sharded over ranks
   CLI                    inference.py:167-244 (--folder, -a/--all)
 The per-query loop of the reference (one model call, one O(N) distance pass
 and one full sort per sketch, with a device sync each) is replaced by batched
@@ -127,23 +129,19 @@ def pd_describe(values):
     return d
 
 
-def process_inference(model, dataset, inference_dataset, dataloader, image_features, start_time,
-                      with_classification, loss_type):
-    k = 10
-    random.seed(11)
-    random_indices = [random.randrange(0, len(dataset)) for _ in range(10)]
-    image_features = image_features.to(device)
-    model.to(device)
-    model.eval()
-    paths = inference_dataset.image_paths
-    with torch.no_grad():
-        sketch_features = _embed(model, dataloader, with_classification)
-    positives = []
+def _positives(dataset, paths):
+    out = []
     for sp in dataset.sketch_paths:
         name = sketch_target_name(sp, paths)
-        positives.append(utils.find_image_index(paths, name) if name is not None else -1)
-    pos_t = torch.tensor(positives, dtype=torch.int64, device=device)
-    idx, dist, rank, _ = _search(sketch_features, image_features, k, pos_t, loss_type)
+        out.append(utils.find_image_index(paths, name) if name is not None else -1)
+    return out
+
+
+def _stats(dataset, inference_dataset, positives, idx, dist_, rank, start_time, k=10):
+    """inference.py:94-136 from the batched search results"""
+    random.seed(11)
+    random_indices = [random.randrange(0, len(dataset)) for _ in range(10)]
+    paths = inference_dataset.image_paths
     ranks = [int(r) if p >= 0 else len(paths) for r, p in zip(rank.tolist(), positives)]
     for sp, p in zip(dataset.sketch_paths, positives):
         if p < 0:
@@ -152,16 +150,138 @@ def process_inference(model, dataset, inference_dataset, dataloader, image_featu
     for i in sorted(set(random_indices)):
         for _ in range(random_indices.count(i)):
             samples.append({str(dataset.sketch_paths[i]): [(str(paths[j]), float(d))
-                                                           for j, d in zip(idx[i].tolist(), dist[i].tolist())]})
+                                                           for j, d in zip(idx[i].tolist(), dist_[i].tolist())]})
     stats = {"mean_reciprocal_rank": None, "size": len(inference_dataset), "inference_time": timer() - start_time}
     stats.update(retrieval_stats(ranks, k))
     stats["retrieval_samples"] = samples
     return stats
 
 
+def process_inference(model, dataset, inference_dataset, dataloader, image_features, start_time,
+                      with_classification, loss_type):
+    k = 10
+    image_features = image_features.to(device)
+    model.to(device)
+    model.eval()
+    with torch.no_grad():
+        sketch_features = _embed(model, dataloader, with_classification)
+    positives = _positives(dataset, inference_dataset.image_paths)
+    pos_t = torch.tensor(positives, dtype=torch.int64, device=device)
+    idx, dist_, rank, _ = _search(sketch_features, image_features, k, pos_t, loss_type)
+    return _stats(dataset, inference_dataset, positives, idx, dist_, rank, start_time, k)
+
+
+# ------------------------------------------------- gallery sharded over ranks
+# the reference embeds the gallery in one loop
+# (inference.py:72-92); with one process per GPU each rank embeds a contiguous
+# shard of the (sorted, de-duplicated) gallery, keeps it resident, and the
+# retrieval runs shard-parallel (knn.knn_sharded: exact top-k per shard,
+# all-gather of k (key, index) pairs per query, merge).  Queries are sharded
+# the same way and all-gathered (they are few).  Only rank 0 writes the feature
+# file, from the gathered gallery.
+
+def shard_bounds(n: int, world: int) -> List[int]:
+    """contiguous ragged shards: rank r owns rows [b[r], b[r+1])"""
+    return [n * r // world for r in range(world + 1)]
+
+
+def gather_rows(local: torch.Tensor, bounds: List[int]) -> torch.Tensor:
+    """all-gather of ragged row shards (rank r holds bounds[r+1]-bounds[r] rows)
+    into the full [bounds[-1], ...] tensor on every rank"""
+    import torch.distributed as dist
+    world = len(bounds) - 1
+    rows = max(bounds[r + 1] - bounds[r] for r in range(world))
+    pad = torch.zeros((rows,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[:local.shape[0]] = local
+    out = torch.empty((world * rows,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, pad)
+    return torch.cat([out[r * rows:r * rows + bounds[r + 1] - bounds[r]] for r in range(world)])
+
+
+def _embed_shard(model, ds, with_classification, batch_size=50):
+    import torch.distributed as dist
+    b = shard_bounds(len(ds), dist.get_world_size())
+    r = dist.get_rank()
+    loader = DataLoader(torch.utils.data.Subset(ds, range(b[r], b[r + 1])), batch_size=batch_size, num_workers=0,
+                        shuffle=False)
+    with torch.no_grad():
+        feats = _embed(model, loader, with_classification)
+    if feats.numel() == 0:  # an empty shard still needs the feature width for the gather
+        feats = feats.reshape(0, 0)
+    return feats, b
+
+
+def compute_image_features_sharded(model, dataset, with_classification: bool, save: bool = True):
+    """-> (inference_dataset, this rank's gallery rows, g_base, feature_path or None)"""
+    import torch.distributed as dist
+    inference_dataset = data_preparation.InferenceDataset(dataset.photo_paths, dataset.transform,
+                                                          getattr(dataset, "resolution", 224))
+    model.to(device)
+    model.eval()
+    feats, b = _embed_shard(model, inference_dataset, with_classification)
+    feature_path = None
+    if save:
+        full = gather_rows(_widen(feats, model, inference_dataset, with_classification), b)
+        if dist.get_rank() == 0:
+            feature_path = utils.save_image_features(model.__class__.__name__, dataset.state_dict['dataset'],
+                                                     inference_dataset, full.cpu())
+    return inference_dataset, feats, b[dist.get_rank()], feature_path
+
+
+def _widen(feats, model, ds, with_classification):
+    """an empty shard as [0, D] (D from one probe embedding) so every rank gathers the same width"""
+    if feats.shape[0] > 0 or len(ds) == 0:
+        return feats
+    with torch.no_grad():
+        probe = _embed(model, DataLoader(torch.utils.data.Subset(ds, [0]), batch_size=1), with_classification)
+    return probe[:0]
+
+
+def process_inference_sharded(model, dataset, inference_dataset, sketches, shard_features, g_base, start_time,
+                              with_classification, loss_type, **search):
+    """process_inference with the gallery sharded over the ranks (every rank
+    returns the same stats).  ``search``: knn.knn_sharded's stand-in hooks (tests)."""
+    k = 10
+    if loss_type not in ('euclidean', 'cosine'):
+        raise Exception(f"loss type not correct {loss_type}")
+    model.to(device)
+    model.eval()
+    q_local, qb = _embed_shard(model, sketches, with_classification)
+    queries = gather_rows(_widen(q_local, model, sketches, with_classification), qb).float()
+    positives = _positives(dataset, inference_dataset.image_paths)
+    pos_t = torch.tensor(positives, dtype=torch.int64, device=queries.device)
+    kk = min(k, len(inference_dataset))
+    idx, dist_, rank = knn.knn_sharded(queries.contiguous(), shard_features.float().contiguous(), g_base, kk, pos_t,
+                                       metric=loss_type, **search)
+    return _stats(dataset, inference_dataset, positives, idx, dist_, rank, start_time, k)
+
+
+def _second_pass(model, dataset, inference_dataset, image_features, first, with_classification, loss_type,
+                 sharded=None, **search):
+    """inference.py:154-165: Kaggle / Mixed test sets are also ranked with the
+    Kaggle inference sketches (sketch_type 'sketches') against the same gallery"""
+    _, dataset2 = data_preparation.get_datasets('KaggleInferenceV1', sketch_type='sketches',
+                                                transform=dataset.transform)
+    if sharded is not None:
+        shard, g_base = sharded
+        return process_inference_sharded(model, dataset2, inference_dataset, _Sketches(dataset2), shard, g_base,
+                                         first['inference_time'], with_classification, loss_type, **search)
+    loader2 = DataLoader(_Sketches(dataset2), batch_size=50, num_workers=0, shuffle=False)
+    return process_inference(model, dataset2, inference_dataset, loader2, image_features, first['inference_time'],
+                             with_classification, loss_type)
+
+
+def _needs_second_pass(dataset) -> bool:
+    name = dataset.state_dict['dataset']
+    return 'Kaggle' in name or 'Mixed' in name
+
+
 def run_inference(model, dataset, folder_name: str = None, loss_type='euclidean') -> Dict:
     start_time = timer()
     with_classification = 'with_classification' in type(model).__name__
+    import ddp
+    if ddp.is_distributed() and not folder_name:
+        return run_inference_sharded(model, dataset, loss_type, start_time)
     if folder_name:
         image_paths, image_features = utils.load_image_features(folder_name)
         inference_dataset = data_preparation.InferenceDataset(image_paths, getattr(model, "transform", None))
@@ -172,8 +292,34 @@ def run_inference(model, dataset, folder_name: str = None, loss_type='euclidean'
     dataloader = DataLoader(_Sketches(dataset), batch_size=50, num_workers=0, shuffle=False)
     inference_dict = process_inference(model, dataset, inference_dataset, dataloader, image_features, start_time,
                                        with_classification, loss_type)
-    inference_dict['image_features'] = feature_folder
-    return inference_dict
+    if not _needs_second_pass(dataset):
+        inference_dict['image_features'] = feature_folder
+        return inference_dict
+    inference_dict2 = _second_pass(model, dataset, inference_dataset, image_features, inference_dict,
+                                   with_classification, loss_type)
+    return {'image_features': feature_folder, 'drawing_stats': inference_dict, 'sketch_stats': inference_dict2}
+
+
+def run_inference_sharded(model, dataset, loss_type='euclidean', start_time=None, **search) -> Dict:
+    """run_inference with one process per GPU: sharded gallery embedding and
+    shard-parallel retrieval; every rank returns the same dictionary, rank 0
+    wrote the feature file (its path is broadcast)."""
+    import torch.distributed as dist
+    start_time = timer() if start_time is None else start_time
+    with_classification = 'with_classification' in type(model).__name__
+    inference_dataset, shard, g_base, feature_path = compute_image_features_sharded(model, dataset,
+                                                                                    with_classification)
+    box = [str(feature_path) if feature_path is not None else None]
+    dist.broadcast_object_list(box, src=0)
+    feature_folder = box[0]
+    first = process_inference_sharded(model, dataset, inference_dataset, _Sketches(dataset), shard, g_base,
+                                      start_time, with_classification, loss_type, **search)
+    if not _needs_second_pass(dataset):
+        first['image_features'] = feature_folder
+        return first
+    second = _second_pass(model, dataset, inference_dataset, None, first, with_classification, loss_type,
+                          sharded=(shard, g_base), **search)
+    return {'image_features': feature_folder, 'drawing_stats': first, 'sketch_stats': second}
 
 
 class _Sketches(torch.utils.data.Dataset):

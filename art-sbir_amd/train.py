@@ -69,6 +69,7 @@ def triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, opt
 def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
                    stale_eval=False):
     start_time = timer()
+    reducer = ddp.attach_overlapped_reducer(model)
     train_losses, test_losses, itrain_losses, itest_losses = [], [], [], []
     iteration_loss_frequency = 10000 // train_dataloader.batch_size if epochs <= 6 else 0
     itest_size = max(1000 // test_dataloader.batch_size, 1)
@@ -77,12 +78,14 @@ def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, op
         itrain_loss = 0.0
         model.train()
         elements = None
+        if hasattr(train_dataloader.sampler, "set_epoch"):
+            train_dataloader.sampler.set_epoch(epoch)  # DistributedSampler: a new shuffle per epoch
         for batch, tup in enumerate(train_dataloader):
             elements = [e.to(device) for e in tup]
             loss = get_loss(loss_fn, model, elements)
             optimizer.zero_grad()
-            loss.backward()
-            ddp.allreduce_gradients(model)
+            loss.backward()  # gradient all-reduce buckets start inside (ddp.OverlappedReducer)
+            reducer.finish()
             optimizer.step()
             train_loss += loss.detach()
             if iteration_loss_frequency and batch and batch % iteration_loss_frequency == 0:

@@ -338,14 +338,16 @@ def main():
         model.load_state_dict(saved, strict=False)
         torch.cuda.empty_cache()
 
+    reducer = ddp.attach_overlapped_reducer(model)
+
     def step():
         # the three branch forwards of train.py:28-30 (per-branch BN statistics),
         # each GEMM launched once over the 3 x B images
         outs = model.forward_branches(batch) if args.batched else [model(x) for x in batch]
         loss = loss_fn(*outs)
         opt.zero_grad(set_to_none=False)
-        loss.backward()
-        ddp.allreduce_gradients(model)
+        loss.backward()  # N > 1: all-reduce buckets start inside the backward (ddp.OverlappedReducer)
+        reducer.finish()
         opt.step()
         return loss
 

@@ -49,3 +49,17 @@ def test_classification_model_step(dev):
     assert m.classifier.weight.grad is not None and m.classifier.weight.grad.abs().sum() > 0
     assert m.conv1.weight.grad.abs().sum() > 0
     opt.step()
+
+
+def test_kaggle_dataset_runs_second_inference_pass(tmp_path, dev, monkeypatch):
+    """inference.py:154-163: a Kaggle / Mixed dataset is also ranked with the
+    Kaggle inference sketches; the result nests both passes."""
+    import train
+    monkeypatch.chdir(tmp_path)
+    _, inf = train.main(TINY + ["--inference", "--no_training", "-d", "SyntheticKaggle", "--no_save"])
+    assert set(inf) == {"image_features", "drawing_stats", "sketch_stats"}
+    first, second = inf["drawing_stats"], inf["sketch_stats"]
+    assert first["size"] == second["size"] == 4
+    assert first["count"] == 4 and second["count"] == 4
+    assert 1 <= second["min"] <= second["max"] <= 4  # 1-based ranks within the 4-photo gallery
+    assert second["inference_time"] >= first["inference_time"]

@@ -9,6 +9,7 @@ import socket
 import types
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -150,3 +151,101 @@ def test_merge_topk_short_shards():
     b_d = torch.tensor([[0.5, 0.7, 0.9]], dtype=torch.float64)
     i, d = knn.merge_topk([a_i, b_i], [a_d, b_d], 3)
     assert i.tolist() == [[3, 7, 1]] and d.tolist() == [[0.5, 0.5, 0.7]]
+
+
+def _overlapped(rank):
+    """ddp.OverlappedReducer: ranges reported out of order, in pieces, some
+    never reported (swept by end()); every element is all-reduced exactly once
+    (a second reduction would show as a wrong scale) and buckets launch as soon
+    as bucket_bytes are pending, before end()."""
+    import ddp
+    n = 1000
+    flat = torch.arange(n, dtype=torch.float32) * (rank + 1)
+    r = ddp.OverlappedReducer(bucket_bytes=400)  # 100 floats
+    r.begin(flat)
+    r.ready([(900, 1000)])                 # the end of the buffer first (the attention pool)
+    assert r.launches == [(900, 1000)]     # one full bucket pending -> launched immediately
+    r.ready([(850, 900), (700, 760)])      # 110 pending -> launched, adjacent ranges kept apart
+    assert len(r.launches) == 3
+    r.ready([(0, 10)])                     # 10 pending: below the bucket, waits
+    assert len(r.launches) == 3
+    r.end()                                # (0,10) plus the unreported [10,700) and [760,850)
+    covered = sorted(r.launches)
+    lo = 0
+    for a, b in covered:
+        assert a == lo, covered
+        lo = b
+    assert lo == n
+    r.finish()
+    want = torch.arange(n, dtype=torch.float32) * 1.5
+    assert torch.allclose(flat, want), (flat - want).abs().max()
+    # a step whose backward never drove the reducer: finish() falls back to the plain all-reduce
+    flat2 = torch.ones(50) * (rank + 1)
+    model = types.SimpleNamespace(_hip_engine=types.SimpleNamespace(_grads=types.SimpleNamespace(flat=flat2)))
+    r2 = ddp.OverlappedReducer(bucket_bytes=64, model=model)
+    r2.finish()
+    assert torch.allclose(flat2, torch.full((50,), 1.5))
+
+
+def test_overlapped_reducer_protocol():
+    _run(_overlapped)
+
+
+class _ProjModel(torch.nn.Module):
+    """CPU stand-in encoder for the sharded-inference protocol: 4x4 average pool
+    then a fixed random projection (the protocol is model-agnostic)."""
+
+    def __init__(self, res, dim=8):
+        super().__init__()
+        g = torch.Generator().manual_seed(7)
+        self.w = torch.randn(3 * (res // 4) ** 2, dim, generator=g)
+        self.transform = None
+
+    def forward(self, x):
+        return torch.nn.functional.avg_pool2d(x, 4).flatten(1) @ self.w
+
+
+def _sharded_inference(rank, tmp, metric):
+    import data_preparation
+    import inference
+    import knn
+    from oracle import retrieval as oret
+    os.chdir(tmp)
+    res = 16
+    model = _ProjModel(res)
+    _, test = data_preparation.get_datasets("SyntheticKaggle", n=130, resolution=res)  # 13 photos, 3+ shards ragged
+    out = inference.run_inference_sharded(
+        model, test, metric, local_search=_cpu_local_search, positive_keys=_cpu_positive_keys,
+        merge=lambda d, i, kk: knn.merge_topk(list(i), list(d), kk))
+    assert set(out) == {"image_features", "drawing_stats", "sketch_stats"}  # Kaggle -> second pass
+    # unsharded expectation: every photo / sketch embedded in one process, exact oracle search
+    ids = data_preparation.InferenceDataset(test.photo_paths, None, res)
+    with torch.no_grad():
+        g = torch.cat([model(ids[i][None]) for i in range(len(ids))]).numpy()
+    feats = np.load(os.path.join("data/image_features", out["image_features"], "image_features.npy"))
+    np.testing.assert_allclose(feats, g, rtol=1e-6, atol=1e-6)  # rank 0 saved the gathered gallery
+    _, kag = data_preparation.get_datasets("KaggleInferenceV1", sketch_type="sketches")
+    for ds, stats in ((test, out["drawing_stats"]), (kag, out["sketch_stats"])):
+        with torch.no_grad():
+            q = torch.cat([model(inference._Sketches(ds)[i][None]) for i in range(len(ds))]).numpy()
+        pos = inference._positives(ds, ids.image_paths)
+        ranks = []
+        for i in range(len(ds)):
+            d = oret.distances(q[i], g, metric)
+            ranks.append(oret.rank_of(d, pos[i]) if pos[i] >= 0 else len(g))
+        want = inference.retrieval_stats(ranks, 10)
+        assert stats["mean_reciprocal_rank"] == pytest.approx(want["mean_reciprocal_rank"], rel=1e-12)
+        assert stats["topk_acc"] == pytest.approx(want["topk_acc"])
+        assert stats["size"] == len(g)
+        for sample in stats["retrieval_samples"]:
+            (sp, top), = sample.items()
+            i = [str(p) for p in ds.sketch_paths].index(sp)
+            ti, td = oret.topk(oret.distances(q[i], g, metric), min(10, len(g)))
+            assert [p for p, _ in top] == [str(ids.image_paths[j]) for j in ti]
+            np.testing.assert_allclose([d for _, d in top], td, rtol=1e-9)
+    assert any(p < 0 for p in inference._positives(kag, ids.image_paths))  # sketches without a gallery photo
+
+
+@pytest.mark.parametrize("metric", ["euclidean", "cosine"])
+def test_sharded_gallery_inference_matches_unsharded(tmp_path, metric):
+    _run(_sharded_inference, str(tmp_path), metric)
