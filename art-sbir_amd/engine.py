@@ -788,6 +788,73 @@ class _Arena:
         return v
 
 
+def _module_grad_order(mod):
+    """gradient-buffer order of a standalone submodule: an attention pool keeps
+    k/v weights and biases adjacent (its fused K|V GEMMs write both at once)"""
+    kv = []
+    if hasattr(mod, "k_proj") and hasattr(mod, "v_proj"):
+        kv = [mod.k_proj.weight, mod.v_proj.weight, mod.k_proj.bias, mod.v_proj.bias]
+    ids = {id(p) for p in kv}
+    return kv + [p for p in mod.parameters() if id(p) not in ids]
+
+
+class ModuleEngine(Engine):
+    """A Bottleneck or AttentionPool2d called on its own — the reference's
+    submodule forwards (models.py:223-236, 249-272), e.g. a block probed in
+    isolation — runs on the same kernels as the encoder: NCHW f32 in and out
+    (NHWC compute layout inside), one autograd node per call, parameter
+    gradients accumulated into param.grad (views of a per-module buffer)."""
+
+    def _pack_all(self):
+        m = self.model
+        if hasattr(m, "conv3"):  # Bottleneck
+            d = {"conv1": self._pack_conv(m.conv1), "conv2": self._pack_conv(m.conv2),
+                 "conv3": self._pack_conv(m.conv3)}
+            if m.downsample is not None:
+                d["down"] = self._pack_conv(m.downsample[1])
+            return d
+        dev = m.k_proj.weight.device
+        return {"kv": self._pack_linear_pair([m.k_proj, m.v_proj], dev), "q": self._pack_linear_pair([m.q_proj], dev),
+                "c": self._pack_linear_pair([m.c_proj], dev)}
+
+    def module_forward(self, x, train: bool):
+        if not x.is_cuda:
+            raise RuntimeError("libartsbir_hip modules run on the GPU: move module and input to cuda")
+        if x.dim() != 4:
+            raise ValueError(f"expected NCHW input, got shape {tuple(x.shape)}")
+        self._G = 1
+        _hip.lib().artsbir_set_deterministic(1 if DETERMINISTIC else 0)
+        m = self.model
+        pk = self.packed()
+        h = x.detach().permute(0, 2, 3, 1).contiguous().to(self.dtype)
+        if hasattr(m, "conv3"):
+            nbn = sum(b.num_features for b in m.modules() if isinstance(b, torch.nn.BatchNorm2d))
+            stats = _Arena(torch.zeros(max(2 * NSLOT * nbn, 1), dtype=torch.float32, device=x.device), NSLOT * 2)
+            out, c = self._block_fwd(m, pk, h, train, stats)
+            return out.permute(0, 3, 1, 2).float().contiguous(), {"train": train, "c": c}
+        out, c = self._attnpool_fwd(m, pk, h)
+        return out.float(), {"train": train, "c": c}
+
+    def module_backward(self, state, dout):
+        if not state["train"]:
+            raise NotImplementedError("backward is implemented for train-mode BatchNorm (as in train.py)")
+        m = self.model
+        pk = self.packed()
+        self._G = 1
+        dev = dout.device
+        grads = self.grad_buffer(dev)
+        if hasattr(m, "conv3"):
+            nbn = sum(b.num_features for b in m.modules() if isinstance(b, torch.nn.BatchNorm2d))
+            ws = _Arena(torch.zeros(max(2 * NSLOT * nbn * 2, 1), dtype=torch.float32, device=dev), NSLOT * 2)
+            d = dout.permute(0, 2, 3, 1).contiguous().to(self.dtype)
+            dh, _ = self._block_bwd(m, pk, state["c"], d, grads, ws, None, None)
+        else:
+            dh = self._attnpool_bwd(m, pk, state["c"], dout.contiguous().float(), grads)
+        if OVERLAP_WGRAD:
+            torch.cuda.current_stream().wait_stream(self._side_stream(dev))
+        return dh.permute(0, 3, 1, 2).float().contiguous()
+
+
 def _param_ranges(grads, params):
     """[lo, hi) element ranges of the gradient buffer holding params' gradients"""
     base = grads.flat.data_ptr()
@@ -810,7 +877,7 @@ class GradBuffer:
     both at once."""
 
     def __init__(self, model, device):
-        self.order = model.grad_order()
+        self.order = model.grad_order() if hasattr(model, "grad_order") else _module_grad_order(model)
         total = sum(p.numel() for p in self.order)
         self.flat = torch.zeros(total, dtype=torch.float32, device=device)
         self.views = {}

@@ -367,6 +367,8 @@ def main(argv=None):
         inference_dict = run_inference(model, test_dataset, None, param_dict.get('loss_type', 'euclidean'))
         with open(Path("results") / folder / "inference_updated.json", "w") as f:
             json.dump(inference_dict, f, indent=4)
+        import visualization
+        visualization.visualize(Path("results") / folder, None, inference_dict)  # inference.py:242
         print(f"RUN INFERENCE FOR {folder}", flush=True)
 
 

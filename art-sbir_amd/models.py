@@ -85,8 +85,9 @@ class Bottleneck(nn.Module):
                 ("1", nn.BatchNorm2d(out))]))
 
     def forward(self, x):
-        raise NotImplementedError(
-            "Bottleneck executes inside ModifiedResNet on libartsbir_hip; call the encoder")
+        # inside ModifiedResNet the encoder runs every block itself; called on
+        # its own the block runs on the same kernels (engine.ModuleEngine)
+        return _module_call(self, x)
 
 
 class AttentionPool2d(nn.Module):
@@ -100,8 +101,43 @@ class AttentionPool2d(nn.Module):
         self.num_heads = num_heads
 
     def forward(self, x):
-        raise NotImplementedError(
-            "AttentionPool2d executes inside ModifiedResNet on libartsbir_hip; call the encoder")
+        return _module_call(self, x)
+
+
+class _ModuleFunction(torch.autograd.Function):
+    """one autograd node per standalone Bottleneck / AttentionPool2d call"""
+
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        eng = _module_engine(mod)
+        out, state = eng.module_forward(x, mod.training)
+        ctx.state, ctx.mod, ctx.dtype, ctx.nparams = state, mod, eng.dtype, len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        eng = _module_engine(ctx.mod)
+        eng.dtype = ctx.dtype
+        dx = eng.module_backward(ctx.state, dout)
+        ctx.state = None
+        return (dx, None) + (None,) * ctx.nparams
+
+
+def _module_engine(mod):
+    eng = mod.__dict__.get("_hip_engine")
+    if eng is None:
+        eng = _engine.ModuleEngine(mod)
+        object.__setattr__(mod, "_hip_engine", eng)
+    eng.dtype = getattr(mod, "compute_dtype", torch.float32)
+    return eng
+
+
+def _module_call(mod, x):
+    params = tuple(mod.parameters())
+    if torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in params)):
+        return _ModuleFunction.apply(x, mod, *params)
+    out, _ = _module_engine(mod).module_forward(x, mod.training)
+    return out
 
 
 class _EncoderFunction(torch.autograd.Function):

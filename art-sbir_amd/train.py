@@ -33,6 +33,7 @@ import losses
 import models
 import optim
 import utils
+import visualization
 
 device = "cuda" if torch.cuda.is_available() else "cpu"
 
@@ -216,7 +217,8 @@ def main(argv=None):
         inference_dict = inference.run_inference(model, test_dataset, args.feature_folder, args.loss_type)
         print({k: v for k, v in inference_dict.items() if k != "retrieval_samples"}, flush=True)
     if rank0 and not args.no_save:
-        utils.save_model(model, data_dict, training_dict, param_dict, inference_dict)
+        folder = utils.save_model(model, data_dict, training_dict, param_dict, inference_dict)
+        visualization.visualize(folder, training_dict, inference_dict)  # train.py:195
     return training_dict, inference_dict
 
 

@@ -107,3 +107,26 @@ def test_train_cli_keeps_reference_flags():
     assert (a.epochs, a.batch_size, a.learning_rate, a.dsize, a.weight_decay) == (2, 8, 1e-4, 0.5, 0.01)
     assert a.inference and a.no_training and a.loss_type == "cosine" and a.loss_margin == 0.3
     assert a.feature_folder == "ff"
+
+
+def test_visualize_writes_reference_figures(tmp_path, monkeypatch):
+    """visualization.visualize (visualization.py:262-273): the figure files of a
+    one-pass and of a Kaggle/Mixed (nested) result, synthetic images rendered."""
+    import data_preparation
+    import visualization
+    monkeypatch.chdir(tmp_path)
+    _, te = data_preparation.get_datasets("Synthetic", n=40, resolution=32)
+    photos = [str(p) for p in te.photo_paths]
+    samples = [{str(te.sketch_paths[i]): [(p, 0.1 * j) for j, p in enumerate(photos)]} for i in range(2)]
+    one = {"mean_reciprocal_rank": 0.5, "size": 4, "inference_time": 1.0, "topk_acc": [0.5] * 10,
+           "retrieval_samples": samples}
+    training = {"train_losses": [0.3, 0.2], "test_losses": [0.35, 0.25], "itrain_losses": [0.3], "itest_losses": [0.3],
+                "iteration_loss_frequency": 312}
+    visualization.visualize(tmp_path / "run1", training, one)
+    for f in ("loss_curves", "loss_curves_iter", "retrieval_samples", "retrieval_samples_original", "topk_accuracy"):
+        assert (tmp_path / "run1" / f"{f}.png").stat().st_size > 1000, f
+    nested = {"image_features": "x", "drawing_stats": one, "sketch_stats": one}
+    visualization.visualize(tmp_path / "run2", None, nested)
+    for f in ("retrieval_samples_drawings", "retrieval_samples_sketches", "topk_accuracy_drawings",
+              "topk_accuracy_sketches"):
+        assert (tmp_path / "run2" / f"{f}.png").stat().st_size > 1000, f
