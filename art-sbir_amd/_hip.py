@@ -43,11 +43,23 @@ class AdamTensor(ctypes.Structure):
     _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("numel", _c_ll)]
 
 
+class ImageDesc(ctypes.Structure):
+    """artsbir_image_desc (include/artsbir.h)"""
+    _fields_ = [("src", ctypes.c_void_p), ("H", ctypes.c_int), ("W", ctypes.c_int), ("C", ctypes.c_int),
+                ("pitch", ctypes.c_int), ("rw", ctypes.c_int), ("rh", ctypes.c_int), ("left", ctypes.c_int),
+                ("top", ctypes.c_int)]
+
+
 _P = ctypes.POINTER(ConvDesc)
+_PI = ctypes.POINTER(ImageDesc)
 _PB = ctypes.POINTER(BnBwdDesc)
 
 # name -> argtypes (restype is always int status unless listed in _RESTYPES)
 SIGNATURES = {
+    "artsbir_clip_preprocess_workspace": [ctypes.c_int, _PI, ctypes.c_int],
+    "artsbir_clip_preprocess": [ctypes.c_int, _PI, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                                ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                                ctypes.c_void_p],
     "artsbir_version": [],
     "artsbir_last_error": [],
     "artsbir_last_kernel": [],
@@ -127,7 +139,8 @@ SIGNATURES = {
     "artsbir_hinge_bwd": [_vp, _vp, _c_int, _c_float, _vp, _vp, _vp, _vp],
 }
 _RESTYPES = {"artsbir_last_error": ctypes.c_char_p, "artsbir_last_kernel": ctypes.c_char_p, "artsbir_adam_table_blocks": _c_ll,
-             "artsbir_knn_candidates_per_query": _c_int, "artsbir_pairwise_l2_topk_workspace": _c_ll}
+             "artsbir_knn_candidates_per_query": _c_int, "artsbir_pairwise_l2_topk_workspace": _c_ll,
+             "artsbir_clip_preprocess_workspace": _c_ll}
 
 _lib = None
 

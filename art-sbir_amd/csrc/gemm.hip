@@ -779,7 +779,7 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   const size_t per = (size_t)a.nseg * ARTSBIR_NSLOT * 2 * a.Cout;
   const size_t need = bd ? per * bd->ntarget : (a.stats ? per : 0);
   if (need > g_tune_stats_n) {
-    if (g_tune_stats) hipFree(g_tune_stats);
+    if (g_tune_stats) (void)hipFree(g_tune_stats);
     g_tune_stats = nullptr;
     g_tune_stats_n = 0;
     if (hipMalloc(&g_tune_stats, need * sizeof(float)) != hipSuccess) return pgemm_default_cfg(p);
@@ -795,8 +795,8 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
     at.bnb_desc = &bt;
   }
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
   // time the candidates on a quiet device: work queued on other streams (the
   // caller's overlapped weight gradients) would otherwise share the chip with
   // some trials and not others and make the choice noisy
@@ -808,18 +808,18 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
     if (!run_candidate(c, at, pt, st)) continue;  // also the warm-up
     float ms = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
-      hipEventRecord(e0, st);
+      (void)hipEventRecord(e0, st);
       run_candidate(c, at, pt, st);
-      hipEventRecord(e1, st);
-      hipEventSynchronize(e1);
+      (void)hipEventRecord(e1, st);
+      (void)hipEventSynchronize(e1);
       float t = 0.f;
-      hipEventElapsedTime(&t, e0, e1);
+      (void)hipEventElapsedTime(&t, e0, e1);
       if (t < ms) ms = t;
     }
     if (ms < best_ms) { best_ms = ms; best = c; }
   }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   return best;
 }
 
@@ -869,7 +869,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
       } else {
         const char* tune = getenv("ARTSBIR_TUNE");
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        hipStreamIsCapturing(st, &cs);
+        (void)hipStreamIsCapturing(st, &cs);
         if ((tune && atoi(tune) == 0) || cs != hipStreamCaptureStatusNone) {
           choice = pgemm_default_cfg(p);
           if (choice < 0) choice = -2;
@@ -1099,7 +1099,7 @@ static bool run_wg_candidate(int c, WgradArgs& a, hipStream_t st) {
 static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   const size_t need = (size_t)a.Cout * a.K;
   if (need > g_tune_dw_n) {
-    if (g_tune_dw) hipFree(g_tune_dw);
+    if (g_tune_dw) (void)hipFree(g_tune_dw);
     g_tune_dw = nullptr;
     g_tune_dw_n = 0;
     if (hipMalloc(&g_tune_dw, need * sizeof(float)) != hipSuccess) return -1;
@@ -1108,8 +1108,8 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   WgradArgs at = a;
   at.dw = g_tune_dw;
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
   (void)hipDeviceSynchronize();  // quiet device (see tune_conv)
   int best = -1;
   float best_ms = 1e30f;
@@ -1117,18 +1117,18 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
     if (!run_wg_candidate(c, at, st)) continue;
     float ms = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
-      hipEventRecord(e0, st);
+      (void)hipEventRecord(e0, st);
       run_wg_candidate(c, at, st);
-      hipEventRecord(e1, st);
-      hipEventSynchronize(e1);
+      (void)hipEventRecord(e1, st);
+      (void)hipEventSynchronize(e1);
       float t = 0.f;
-      hipEventElapsedTime(&t, e0, e1);
+      (void)hipEventElapsedTime(&t, e0, e1);
       if (t < ms) ms = t;
     }
     if (ms < best_ms) { best_ms = ms; best = c; }
   }
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   return best;
 }
 
@@ -1148,7 +1148,7 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
       } else {
         const char* tune = getenv("ARTSBIR_TUNE");
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        hipStreamIsCapturing(st, &cs);
+        (void)hipStreamIsCapturing(st, &cs);
         choice = ((tune && atoi(tune) == 0) || cs != hipStreamCaptureStatusNone) ? -1 : tune_wgrad(a, st);
         g_wg_choice[key] = choice;
       }

@@ -354,6 +354,27 @@ int artsbir_hinge_fwd(const float* dp, const float* dn, int B, float margin, flo
 int artsbir_hinge_bwd(const float* dp, const float* dn, int B, float margin, const float* gout, float* gdp, float* gdn,
                       void* stream);
 
+/* ---------------------------------------------------------- preprocessing
+ * The encoder's image transform on the GPU, replacing
+ * /root/reference/models.py:289-295 (torchvision Resize(res, BICUBIC) ->
+ * CenterCrop(res) -> convert('RGB') -> ToTensor -> Normalize(CLIP), applied by
+ * Pillow per image on the CPU).  Bit-identical to the Pillow/torch result:
+ * Pillow's fixed-point separable bicubic resampling (a horizontal pass into a
+ * uint8 intermediate, then vertical), only the cropped pixels computed.
+ * One descriptor per decoded image (device uint8 HWC rows, C = 1 'L' or 3
+ * 'RGB'); rw, rh = the resized size and left, top = the crop origin, computed
+ * by the caller as torchvision does (preprocess.py); rw == W (rh == H): that
+ * axis is not resampled.  out: device f32 [n][3][res][res].  workspace: device
+ * bytes, at least artsbir_clip_preprocess_workspace(); mean3 / std3: host. */
+typedef struct artsbir_image_desc {
+  const unsigned char* src;
+  int H, W, C, pitch;
+  int rw, rh, left, top;
+} artsbir_image_desc;
+long long artsbir_clip_preprocess_workspace(int n, const artsbir_image_desc* descs, int res);
+int artsbir_clip_preprocess(int n, const artsbir_image_desc* descs, int res, const float* mean3, const float* std3,
+                            float* out, void* workspace, long long ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

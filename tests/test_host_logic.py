@@ -130,3 +130,14 @@ def test_visualize_writes_reference_figures(tmp_path, monkeypatch):
     for f in ("retrieval_samples_drawings", "retrieval_samples_sketches", "topk_accuracy_drawings",
               "topk_accuracy_sketches"):
         assert (tmp_path / "run2" / f"{f}.png").stat().st_size > 1000, f
+
+
+def test_preprocess_plan_matches_torchvision_rules():
+    """preprocess.plan: torchvision's resized size (shorter side -> res, int()
+    of the long side) and centre-crop origin (round half to even)."""
+    import preprocess
+    assert preprocess.plan(300, 200, 224) == (336, 224, 56, 0)
+    assert preprocess.plan(224, 225, 224) == (224, 225, 0, 0)   # (225-224)/2 = 0.5 -> 0
+    assert preprocess.plan(224, 227, 224) == (224, 227, 0, 2)   # 1.5 -> 2
+    assert preprocess.plan(97, 331, 224) == (224, 764, 0, 270)
+    assert preprocess.plan(513, 1024, 224) == (224, 447, 0, 112)  # 111.5 -> 112
