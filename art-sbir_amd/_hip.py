@@ -50,6 +50,18 @@ class ImageDesc(ctypes.Structure):
                 ("top", ctypes.c_int)]
 
 
+class WarpDesc(ctypes.Structure):
+    """artsbir_warp_desc (include/artsbir.h)"""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("kind", ctypes.c_int),
+                ("coeffs", ctypes.c_double * 8), ("fill", ctypes.c_ubyte * 3)]
+
+
+class EraseDesc(ctypes.Structure):
+    """artsbir_erase_desc (include/artsbir.h)"""
+    _fields_ = [("src", ctypes.c_void_p), ("nrect", ctypes.c_int), ("rect", (ctypes.c_int * 4) * 4),
+                ("value", ctypes.c_float * 4)]
+
+
 _P = ctypes.POINTER(ConvDesc)
 _PI = ctypes.POINTER(ImageDesc)
 _PB = ctypes.POINTER(BnBwdDesc)
@@ -57,6 +69,13 @@ _PB = ctypes.POINTER(BnBwdDesc)
 # name -> argtypes (restype is always int status unless listed in _RESTYPES)
 SIGNATURES = {
     "artsbir_clip_preprocess_workspace": [ctypes.c_int, _PI, ctypes.c_int],
+    "artsbir_resize_u8": [ctypes.c_int, _PI, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
+                          ctypes.c_void_p],
+    "artsbir_warp_u8": [ctypes.c_int, ctypes.POINTER(WarpDesc), ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                        ctypes.c_longlong, ctypes.c_void_p],
+    "artsbir_erase_normalize": [ctypes.c_int, ctypes.POINTER(EraseDesc), ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_longlong, ctypes.c_void_p],
     "artsbir_clip_preprocess": [ctypes.c_int, _PI, ctypes.c_int, ctypes.POINTER(ctypes.c_float),
                                 ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_longlong,
                                 ctypes.c_void_p],

@@ -112,10 +112,11 @@ __global__ void __launch_bounds__(256) pp_horizontal_kernel(const PrepDev* __res
 __global__ void __launch_bounds__(256) pp_vertical_kernel(const PrepDev* __restrict__ imgs, int res,
                                                           const unsigned char* __restrict__ tmp, float m0, float m1,
                                                           float m2, float s0, float s1, float s2,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, unsigned char* __restrict__ out_u8) {
   const PrepDev d = imgs[blockIdx.y];
   const unsigned char* t = tmp + d.tmp_off;
-  float* o = out + (long long)blockIdx.y * 3 * res * res;
+  float* o = out ? out + (long long)blockIdx.y * 3 * res * res : nullptr;
+  unsigned char* o8 = out_u8 ? out_u8 + (long long)blockIdx.y * 3 * res * res : nullptr;
   const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
   for (int i = blockIdx.x * 256 + threadIdx.x; i < res * res; i += gridDim.x * 256) {
     const int y = i / res, x = i % res;
@@ -132,6 +133,10 @@ __global__ void __launch_bounds__(256) pp_vertical_kernel(const PrepDev* __restr
         for (int c = 0; c < d.C; ++c) acc[c] += (int)p[c] * w;
       }
       for (int c = 0; c < d.C; ++c) v[c] = pp_clip8(acc[c]);
+    }
+    if (o8) {  // uint8 RGB rows (the augmentation's input)
+      for (int c = 0; c < 3; ++c) o8[(long long)i * 3 + c] = v[d.C == 1 ? 0 : c];
+      continue;
     }
     for (int c = 0; c < 3; ++c) {
       const float f = (float)v[d.C == 1 ? 0 : c] / 255.0f;
@@ -206,10 +211,26 @@ extern "C" long long artsbir_clip_preprocess_workspace(int n, const artsbir_imag
   return bytes;
 }
 
+static int pp_run(int n, const artsbir_image_desc* descs, int res, const float* mean3, const float* std3, float* out,
+                  unsigned char* out_u8, void* workspace, long long ws_bytes, void* stream);
+
 extern "C" int artsbir_clip_preprocess(int n, const artsbir_image_desc* descs, int res, const float* mean3,
                                        const float* std3, float* out, void* workspace, long long ws_bytes,
                                        void* stream) {
-  if (n < 0 || res < 1 || !mean3 || !std3 || (n && (!out || !workspace))) {
+  if (!out && n) { set_error("clip_preprocess: bad arguments"); return -1; }
+  return pp_run(n, descs, res, mean3, std3, out, nullptr, workspace, ws_bytes, stream);
+}
+
+extern "C" int artsbir_resize_u8(int n, const artsbir_image_desc* descs, int res, unsigned char* out,
+                                 void* workspace, long long ws_bytes, void* stream) {
+  static const float zero3[3] = {0.f, 0.f, 0.f}, one3[3] = {1.f, 1.f, 1.f};
+  if (!out && n) { set_error("resize_u8: bad arguments"); return -1; }
+  return pp_run(n, descs, res, zero3, one3, nullptr, out, workspace, ws_bytes, stream);
+}
+
+static int pp_run(int n, const artsbir_image_desc* descs, int res, const float* mean3, const float* std3, float* out,
+                  unsigned char* out_u8, void* workspace, long long ws_bytes, void* stream) {
+  if (n < 0 || res < 1 || !mean3 || !std3 || (n && !workspace)) {
     set_error("clip_preprocess: bad arguments");
     return -1;
   }
@@ -233,7 +254,195 @@ extern "C" int artsbir_clip_preprocess(int n, const artsbir_image_desc* descs, i
   hipLaunchKernelGGL(pp_horizontal_kernel, dim3(gx * 4, n), dim3(256), 0, st, dimgs, res, tmp);
   ARTSBIR_CHECK_LAUNCH("clip_preprocess horizontal");
   hipLaunchKernelGGL(pp_vertical_kernel, dim3(gx, n), dim3(256), 0, st, dimgs, res, tmp, mean3[0], mean3[1],
-                     mean3[2], std3[0], std3[1], std3[2], out);
+                     mean3[2], std3[0], std3[1], std3[2], out, out_u8);
   ARTSBIR_CHECK_LAUNCH("clip_preprocess vertical");
+  return 0;
+}
+
+namespace artsbir {
+// ------------------------------------------------------------ augmentation
+// The sketch augmentation of /root/reference/transformations.py:18-34 (and the
+// V2 variant :37-56) on uint8 RGB rows of one size: Pillow's Image.transform as
+// torchvision's PIL backend calls it, bit-identical —
+//   kind 1  AFFINE, NEAREST, a[1] == a[3] == 0 (pure scale: RandomAffine with
+//           degrees 0 and no shear) -> Pillow's ImagingScaleAffine: source
+//           column / row by sequential double accumulation from the pixel
+//           centre, xo += a[0] per column, yo += a[4] per row;
+//   kind 2  AFFINE, NEAREST, general -> Pillow's 16.16 fixed-point affine
+//           (coefficients converted by the host, integer increments);
+//   kind 3  PERSPECTIVE, BILINEAR (RandomPerspective) -> Pillow's generic
+//           transform: pixel centre through the projective map, bilinear of
+//           the clipped neighbours in double, truncated to uint8;
+//   kind 0  copy.
+// Pixels mapped outside the source keep the fill colour (Image.transform with
+// fillcolor).  Then artsbir_erase_normalize: ToTensor, up to 4 RandomErasing
+// rectangles set to their value, Normalize.
+struct WarpDev {
+  const unsigned char* src;
+  unsigned char* dst;
+  int kind;
+  int fx[6];        // kind 2: a0, a1, a2', a3, a4, a5' in 16.16
+  double a[8];
+  unsigned char fill[3];
+};
+
+#pragma clang fp contract(off)
+__global__ void __launch_bounds__(256) warp_kernel(const WarpDev* __restrict__ ws, int H, int W) {
+  const WarpDev d = ws[blockIdx.y];
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < H * W; i += gridDim.x * 256) {
+    const int y = i / W, x = i % W;
+    unsigned char px[3] = {d.fill[0], d.fill[1], d.fill[2]};
+    if (d.kind == 0) {
+      for (int c = 0; c < 3; ++c) px[c] = d.src[(long long)i * 3 + c];
+    } else if (d.kind == 1) {
+      double xo = d.a[2] + d.a[0] * 0.5, yo = d.a[5] + d.a[4] * 0.5;
+      for (int k = 0; k < x; ++k) xo += d.a[0];
+      for (int k = 0; k < y; ++k) yo += d.a[4];
+      const int xin = xo < 0.0 ? -1 : (int)xo, yin = yo < 0.0 ? -1 : (int)yo;
+      if (xin >= 0 && xin < W && yin >= 0 && yin < H)
+        for (int c = 0; c < 3; ++c) px[c] = d.src[((long long)yin * W + xin) * 3 + c];
+    } else if (d.kind == 2) {
+      const int xx = d.fx[2] + y * d.fx[1] + x * d.fx[0];
+      const int yy = d.fx[5] + y * d.fx[4] + x * d.fx[3];
+      const int xin = xx >> 16, yin = yy >> 16;
+      if (xin >= 0 && xin < W && yin >= 0 && yin < H)
+        for (int c = 0; c < 3; ++c) px[c] = d.src[((long long)yin * W + xin) * 3 + c];
+    } else {
+      const double xi = x + 0.5, yi = y + 0.5;
+      const double den = d.a[6] * xi + d.a[7] * yi + 1;
+      double xs = (d.a[0] * xi + d.a[1] * yi + d.a[2]) / den;
+      double ys = (d.a[3] * xi + d.a[4] * yi + d.a[5]) / den;
+      if (xs >= 0.0 && xs < W && ys >= 0.0 && ys < H) {
+        xs -= 0.5;
+        ys -= 0.5;
+        const int x0 = xs < 0.0 ? (int)floor(xs) : (int)xs;
+        const int y0 = ys < 0.0 ? (int)floor(ys) : (int)ys;
+        const double dx = xs - x0, dy = ys - y0;
+        const int yc = y0 < 0 ? 0 : y0 >= H ? H - 1 : y0;
+        const int xa = x0 < 0 ? 0 : x0 >= W ? W - 1 : x0;
+        const int xb = x0 + 1 < 0 ? 0 : x0 + 1 >= W ? W - 1 : x0 + 1;
+        const bool y1ok = y0 + 1 >= 0 && y0 + 1 < H;
+        for (int c = 0; c < 3; ++c) {
+          const double a0 = d.src[((long long)yc * W + xa) * 3 + c], b0 = d.src[((long long)yc * W + xb) * 3 + c];
+          const double v1 = a0 + (b0 - a0) * dx;
+          double v2 = v1;
+          if (y1ok) {
+            const double a1 = d.src[((long long)(y0 + 1) * W + xa) * 3 + c];
+            const double b1 = d.src[((long long)(y0 + 1) * W + xb) * 3 + c];
+            v2 = a1 + (b1 - a1) * dx;
+          }
+          px[c] = (unsigned char)(v1 + (v2 - v1) * dy);
+        }
+      }
+    }
+    for (int c = 0; c < 3; ++c) d.dst[(long long)i * 3 + c] = px[c];
+  }
+}
+#pragma clang fp contract(on)
+
+struct EraseDev {
+  const unsigned char* src;
+  int nrect;
+  int rect[4][4];     // i, j, h, w
+  float value[4];
+};
+
+__global__ void __launch_bounds__(256) erase_normalize_kernel(const EraseDev* __restrict__ es, int H, int W, float m0,
+                                                              float m1, float m2, float s0, float s1, float s2,
+                                                              float* __restrict__ out) {
+  const EraseDev e = es[blockIdx.y];
+  const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
+  float* o = out + (long long)blockIdx.y * 3 * H * W;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < H * W; i += gridDim.x * 256) {
+    const int y = i / W, x = i % W;
+    int hit = -1;
+    for (int r = 0; r < e.nrect; ++r)  // later rectangles overwrite earlier ones
+      if (y >= e.rect[r][0] && y < e.rect[r][0] + e.rect[r][2] && x >= e.rect[r][1] && x < e.rect[r][1] + e.rect[r][3])
+        hit = r;
+    for (int c = 0; c < 3; ++c) {
+      const float f = hit >= 0 ? e.value[hit] : (float)e.src[(long long)i * 3 + c] / 255.0f;
+      o[(long long)c * H * W + i] = (f - mean[c]) / sd[c];
+    }
+  }
+}
+
+static int fix16(double v, int& out) {  // Pillow's FIX(): floor(v * 65536 + 0.5)
+  const double t = v * 65536.0 + 0.5;
+  const double f = t < 0.0 ? floor(t) : (double)(long long)t;
+  if (f < -2147483648.0 || f > 2147483647.0) return -1;
+  out = (int)f;
+  return 0;
+}
+static bool check_fixed(const double* a, int x, int y) {
+  return fabs(x * a[0] + y * a[1] + a[2]) < 32768.0 && fabs(x * a[3] + y * a[4] + a[5]) < 32768.0;
+}
+}  // namespace artsbir
+
+extern "C" int artsbir_warp_u8(int n, const artsbir_warp_desc* descs, int H, int W, void* workspace,
+                               long long ws_bytes, void* stream) {
+  if (n < 0 || H < 1 || W < 1 || (n && (!descs || !workspace))) { set_error("warp_u8: bad arguments"); return -1; }
+  if (n == 0) return 0;
+  if ((long long)n * (long long)sizeof(WarpDev) > ws_bytes) { set_error("warp_u8: workspace too small"); return -1; }
+  WarpDev* w = new WarpDev[n];
+  for (int i = 0; i < n; ++i) {
+    const artsbir_warp_desc& s = descs[i];
+    WarpDev& d = w[i];
+    d.src = s.src; d.dst = s.dst; d.kind = s.kind;
+    for (int k = 0; k < 8; ++k) d.a[k] = s.coeffs[k];
+    for (int c = 0; c < 3; ++c) d.fill[c] = s.fill[c];
+    if (!s.src || !s.dst || s.kind < 0 || s.kind > 3) { delete[] w; set_error("warp_u8: image %d: bad descriptor", i); return -1; }
+    if (s.kind == 1 && (s.coeffs[1] != 0.0 || s.coeffs[3] != 0.0)) {
+      delete[] w; set_error("warp_u8: image %d: kind 1 is the pure-scale affine", i); return -1;
+    }
+    if (s.kind == 2) {
+      const double* a = s.coeffs;
+      if (!(check_fixed(a, 0, 0) && check_fixed(a, W, H) && check_fixed(a, 0, H) && check_fixed(a, W, 0))) {
+        delete[] w; set_error("warp_u8: image %d: affine outside Pillow's fixed-point range", i); return -1;
+      }
+      if (fix16(a[0], d.fx[0]) || fix16(a[1], d.fx[1]) || fix16(a[3], d.fx[3]) || fix16(a[4], d.fx[4]) ||
+          fix16(a[2] + a[1] * 0.5 + a[0] * 0.5, d.fx[2]) || fix16(a[5] + a[4] * 0.5 + a[3] * 0.5, d.fx[5])) {
+        delete[] w; set_error("warp_u8: image %d: coefficient overflow", i); return -1;
+      }
+    }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(workspace, w, sizeof(WarpDev) * n, hipMemcpyHostToDevice, st);
+  delete[] w;
+  if (e != hipSuccess) { set_error("warp_u8: descriptor upload: %s", hipGetErrorString(e)); return -2; }
+  const unsigned gx = (unsigned)((H * W + 255) / 256 < 128 ? (H * W + 255) / 256 : 128);
+  hipLaunchKernelGGL(warp_kernel, dim3(gx, n), dim3(256), 0, st, reinterpret_cast<const WarpDev*>(workspace), H, W);
+  ARTSBIR_CHECK_LAUNCH("warp_u8");
+  return 0;
+}
+
+extern "C" int artsbir_erase_normalize(int n, const artsbir_erase_desc* descs, int H, int W, const float* mean3,
+                                       const float* std3, float* out, void* workspace, long long ws_bytes,
+                                       void* stream) {
+  if (n < 0 || H < 1 || W < 1 || !mean3 || !std3 || (n && (!descs || !out || !workspace))) {
+    set_error("erase_normalize: bad arguments");
+    return -1;
+  }
+  if (n == 0) return 0;
+  if ((long long)n * (long long)sizeof(EraseDev) > ws_bytes) { set_error("erase_normalize: workspace too small"); return -1; }
+  EraseDev* ed = new EraseDev[n];
+  for (int i = 0; i < n; ++i) {
+    const artsbir_erase_desc& s = descs[i];
+    if (!s.src || s.nrect < 0 || s.nrect > 4) { delete[] ed; set_error("erase_normalize: image %d: bad descriptor", i); return -1; }
+    ed[i].src = s.src;
+    ed[i].nrect = s.nrect;
+    for (int r = 0; r < 4; ++r) {
+      for (int k = 0; k < 4; ++k) ed[i].rect[r][k] = s.rect[r][k];
+      ed[i].value[r] = s.value[r];
+    }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(workspace, ed, sizeof(EraseDev) * n, hipMemcpyHostToDevice, st);
+  delete[] ed;
+  if (e != hipSuccess) { set_error("erase_normalize: descriptor upload: %s", hipGetErrorString(e)); return -2; }
+  const unsigned gx = (unsigned)((H * W + 255) / 256 < 128 ? (H * W + 255) / 256 : 128);
+  hipLaunchKernelGGL(erase_normalize_kernel, dim3(gx, n), dim3(256), 0, st,
+                     reinterpret_cast<const EraseDev*>(workspace), H, W, mean3[0], mean3[1], mean3[2], std3[0],
+                     std3[1], std3[2], out);
+  ARTSBIR_CHECK_LAUNCH("erase_normalize");
   return 0;
 }

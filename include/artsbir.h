@@ -375,6 +375,43 @@ long long artsbir_clip_preprocess_workspace(int n, const artsbir_image_desc* des
 int artsbir_clip_preprocess(int n, const artsbir_image_desc* descs, int res, const float* mean3, const float* std3,
                             float* out, void* workspace, long long ws_bytes, void* stream);
 
+/* The same resize (exact target size: rw = rh = res, left = top = 0, as the
+ * sketch transforms' Resize((224, 224))) into uint8 RGB rows [n][res][res][3]
+ * — the input of the augmentation below. */
+int artsbir_resize_u8(int n, const artsbir_image_desc* descs, int res, unsigned char* out, void* workspace,
+                      long long ws_bytes, void* stream);
+
+/* Sketch augmentation (/root/reference/transformations.py:18-56, torchvision's
+ * RandomPerspective / RandomAffine through Pillow's Image.transform, and
+ * RandomErasing), bit-identical to Pillow for the same parameters (the random
+ * parameters are drawn on the host, preprocess.SketchAugment).  One descriptor
+ * per image, all images H x W uint8 RGB rows; src and dst must not overlap.
+ * kind: 0 copy, 1 AFFINE NEAREST pure scale (coeffs[1] == coeffs[3] == 0),
+ * 2 AFFINE NEAREST, 3 PERSPECTIVE BILINEAR; coeffs: Pillow's data tuple (6 or
+ * 8 values, the output -> input map); fill: colour of pixels mapped outside.
+ * workspace: device, >= n * 160 bytes. */
+typedef struct artsbir_warp_desc {
+  const unsigned char* src;
+  unsigned char* dst;
+  int kind;
+  double coeffs[8];
+  unsigned char fill[3];
+} artsbir_warp_desc;
+int artsbir_warp_u8(int n, const artsbir_warp_desc* descs, int H, int W, void* workspace, long long ws_bytes,
+                    void* stream);
+
+/* ToTensor + RandomErasing (up to 4 rectangles (i, j, h, w), later ones on top,
+ * pixels set to value) + Normalize: out f32 [n][3][H][W].  workspace: device,
+ * >= n * 96 bytes. */
+typedef struct artsbir_erase_desc {
+  const unsigned char* src;
+  int nrect;
+  int rect[4][4];
+  float value[4];
+} artsbir_erase_desc;
+int artsbir_erase_normalize(int n, const artsbir_erase_desc* descs, int H, int W, const float* mean3,
+                            const float* std3, float* out, void* workspace, long long ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,3 +51,61 @@ def test_gpu_preprocess_rejects_other_modes(dev):
     with pytest.raises(NotImplementedError):
         preprocess.ClipPreprocess(32, device=dev)([Image.new("P", (40, 40))])
     assert preprocess.ClipPreprocess(32, device=dev)([]).shape == (0, 3, 32, 32)
+
+
+def _pil_sketch_pipeline(img, ops, boxes, res):
+    """the reference's sketch transform for given random draws, on Pillow / torch
+    (transformations.py:18-34: Resize((res, res), BICUBIC), RGB, the warps through
+    Image.transform as torchvision's PIL backend calls it, ToTensor, erasing, Normalize)"""
+    import models
+    im = img.resize((res, res), Image.BICUBIC) if img.size != (res, res) else img
+    im = im.convert("RGB")
+    for what, co in ops:
+        if what == "perspective":
+            im = im.transform(im.size, Image.PERSPECTIVE, co, Image.BILINEAR, fillcolor=(255, 255, 255))
+        else:
+            im = im.transform(im.size, Image.AFFINE, co, Image.NEAREST, fillcolor=(255, 255, 255))
+    t = torch.from_numpy(np.asarray(im, dtype=np.float32).copy() / 255.0).permute(2, 0, 1).contiguous()
+    for i, j, h, w in boxes:
+        t[:, i:i + h, j:j + w] = 1.0
+    mean = torch.tensor(models.CLIP_MEAN)[:, None, None]
+    std = torch.tensor(models.CLIP_STD)[:, None, None]
+    return (t - mean) / std
+
+
+@pytest.mark.parametrize("version", ["V1", "V2"])
+def test_gpu_sketch_augmentation_bit_identical_to_pillow(version, dev):
+    import preprocess
+    res = 224
+    imgs = _images(7)[:8]
+    g = torch.Generator().manual_seed(123)
+    aug = preprocess.SketchAugment(version, res, device=dev, generator=g)
+    got = aug(imgs).cpu()
+    g2 = torch.Generator().manual_seed(123)  # the same draws again, for the Pillow pipeline
+    plans = [preprocess.sample_sketch_ops(aug.cfg, res, res, g2) for _ in imgs]
+    kinds = set()
+    for i, (im, (ops, boxes)) in enumerate(zip(imgs, plans)):
+        kinds |= {w if w == "perspective" else preprocess._affine_kind(c) for w, c in ops}
+        want = _pil_sketch_pipeline(im, ops, boxes, res)
+        diff = (got[i] != want).sum().item()
+        assert diff == 0, (i, [w for w, _ in ops], boxes, diff)
+    assert {"perspective", 1, 2} <= kinds  # every warp kind was exercised
+
+
+def test_gpu_warp_kinds_against_pillow(dev):
+    """each warp kind alone, at parameters beyond the random ranges (large shear,
+    strong perspective, scale-down), against Image.transform"""
+    import preprocess
+    res = 96
+    rng = np.random.default_rng(5)
+    src = Image.fromarray(rng.integers(0, 256, (res, res, 3), dtype=np.uint8))
+    cases = [("affine", preprocess.inverse_affine_matrix([48.0, 48.0], 0.0, [0, 0], 0.7, [0.0, 0.0])),
+             ("affine", preprocess.inverse_affine_matrix([48.0, 48.0], 33.0, [5, -9], 1.4, [20.0, -12.0])),
+             ("perspective", preprocess.perspective_coeffs([[0, 0], [95, 0], [95, 95], [0, 95]],
+                                                           [[20, 5], [70, 18], [90, 80], [3, 60]]))]
+    aug = preprocess.SketchAugment("V1", res, device=dev)
+    rgb = torch.from_numpy(np.asarray(src).copy())[None].to(dev)
+    for what, co in cases:
+        got = aug.apply(rgb, [([(what, co)], [])]).cpu()[0]
+        want = _pil_sketch_pipeline(src, [(what, co)], [], res)
+        assert (got != want).sum().item() == 0, what
