@@ -277,3 +277,25 @@ def test_knn_c4_gallery_sampled_queries(metric, dev):
     np.testing.assert_array_equal(rank.cpu().numpy(), rr)
     r1 = rr + 1
     assert np.mean(np.where(r1 <= k, 1.0 / r1, 0.0)) < 1.0  # a workload where ranks spread
+
+
+@pytest.mark.parametrize("compute", ["bf16", "f32"])
+def test_knn_against_committed_golden_fixture(compute, dev):
+    """tests/golden/retrieval.npz (duplicates at rows 0 / 4000, queries without a
+    positive) through the library: top-10, distances and ranks as committed."""
+    import os
+    import sys
+    import knn
+    golden = os.path.join(os.path.dirname(__file__), "golden")
+    sys.path.insert(0, golden)
+    import make_golden
+    gold = np.load(os.path.join(golden, "retrieval.npz"), allow_pickle=False)
+    g, qs, pos = make_golden.golden_gallery()
+    np.testing.assert_array_equal(gold["positives"], pos)
+    idx, dist, rank, _ = knn.knn(torch.from_numpy(qs).to(dev), torch.from_numpy(g).to(dev), 10,
+                                 torch.from_numpy(pos).to(dev), compute=compute)
+    np.testing.assert_array_equal(idx.cpu().numpy(), gold["topk_idx"])
+    np.testing.assert_allclose(dist.cpu().numpy(), gold["topk_dist"], rtol=1e-12)
+    r = rank.cpu().numpy()
+    want = gold["ranks"]
+    np.testing.assert_array_equal(np.where(pos >= 0, r, len(g)), want)
