@@ -106,6 +106,15 @@ SIGNATURES = {
     "artsbir_layernorm_fwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp],
     "artsbir_quickgelu": [_c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_mha_fwd_lse": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "artsbir_layernorm_bwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_quickgelu_bwd": [_c_int, _vp, _vp, _c_ll, _vp, _vp],
+    "artsbir_mha_bwd": [_c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
+    "artsbir_vit_patchify": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_quantize_fp8": [_c_int, _vp, _c_ll, _vp, _vp, _vp],
+    "artsbir_gemm_nt_fp8": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
+    "artsbir_vit_tokens": [_c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_vit_tokens_bwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_bn_finalize_seg": [_vp, _c_int, _c_ll, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float,
                                 _c_float, _c_int, _vp, _vp],
     "artsbir_bn_bwd_finalize_seg": [_vp, _c_int, _c_ll, _c_int, ctypes.c_double, _vp, _vp, _c_ll, _vp, _vp, _vp,

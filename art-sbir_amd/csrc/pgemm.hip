@@ -504,6 +504,51 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
   }
 }
 
+// ---- epilogue operands prefetched into registers (PF variants): every lane
+// issues the global loads of its own epilogue operands (residual, y_0, mask
+// bits, y_1 — the same addresses pg_epilogue_k reads) BEFORE the main loop, so
+// their latency runs under the tile's K-steps instead of as a separate
+// round trip after them.  They are older than the stage loads, so the manual
+// vmcnt counting of the stages only waits for them once (at the first stage).
+template <int NP, int NTP>
+struct EpiRegs {
+  Vec16<bf16> rv[NP][NTP], y0v[NP][NTP], y1v[NP][NTP];
+  unsigned mb[NP][NTP];
+};
+
+template <int BK, bool TWO, int MTC, int NTP, int WTPX, int WTCH>
+__device__ __forceinline__ void epi_prefetch(const PgArgs& a, EpiRegs<MTC / 2, NTP>& er, long long bpx, int bch,
+                                             int wpx, int wch, int fr, int fq) {
+  constexpr bool RESK = BK == 2 || BK == 3;
+  const int HoWo = a.Ho * a.Wo;
+  const long long wpx0 = bpx + wpx * WTPX;
+  const bool res = RESK || (BK == 0 && a.res_mode != 0);
+#pragma unroll
+  for (int p = 0; p < MTC / 2; ++p) {
+    const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+    const int chc = ch0 < a.Cout ? ch0 : 0;
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const long long px = wpx0 + j * 16 + fr;
+      const long long pc = px < a.M ? px : a.M - 1;
+      if (res) {
+        long long ri = pc;
+        if (a.res_mode == 2) {
+          const long long img = pc / HoWo;
+          const int rem = (int)(pc - img * HoWo);
+          const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+          ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+        }
+        er.rv[p][j] = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + chc);
+      }
+      if constexpr (BK != 0) er.y0v[p][j] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + pc * a.ldy + chc);
+      if constexpr (BK == 3)
+        er.mb[p][j] = reinterpret_cast<const unsigned char*>(a.bnb_mask)[pc * (a.Cout >> 3) + (chc >> 3)];
+      if constexpr (TWO) er.y1v[p][j] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + pc * a.ldy + chc);
+    }
+  }
+}
+
 // The epilogue of pgemm_kernel, specialised at compile time on what the launch
 // fuses (the generic pg_epilogue above decides per element at run time, which
 // cost ~840 scalar branches in the unrolled epilogue and most of the fused
@@ -514,9 +559,10 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
 // global memory in batches of EJB pixel tiles); y_0 and the mask bits of BK 3
 // are always staged, the BN constants always come from the LDS table.
 template <int BK, bool TWO, bool S_RES, bool S_Y1, bool S_MK, int BCH, int MTC, int NTP, int WTPX, int WTCH,
-          int EJB = 2>
+          bool REG = false, int EJB = 2>
 __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
-                                              int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg) {
+                                              int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg,
+                                              const EpiRegs<MTC / 2, NTP>* er = nullptr) {
   constexpr bool BNB = BK != 0;
   constexpr bool RESK = BK == 2 || BK == 3;
   const int HoWo = a.Ho * a.Wo;
@@ -544,7 +590,7 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
       if constexpr (TWO) { loadf8v(pp + 2 * BCH, xa1); loadf8v(pp + 3 * BCH, m1); }
       if constexpr (BK == 1) { loadf8v(pp + 4 * BCH, mm); loadf8v(pp + 5 * BCH, ms); loadf8v(pp + 6 * BCH, mh); }
     }
-    constexpr bool GLOBAL_OPS = (RESK && !S_RES) || (TWO && !S_Y1) || (BK == 2 && !S_MK) || BK == 0;
+    constexpr bool GLOBAL_OPS = !REG && ((RESK && !S_RES) || (TWO && !S_Y1) || (BK == 2 && !S_MK) || BK == 0);
     constexpr int EJ = (GLOBAL_OPS && NTP >= EJB) ? EJB : 1;
 #pragma unroll
     for (int j0 = 0; j0 < NTP; j0 += EJ) {
@@ -552,6 +598,13 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
       unsigned mbits[EJ];
 #pragma unroll
       for (int u = 0; u < EJ; ++u) {  // operands of the batch (global loads issued together)
+        if constexpr (REG) {  // prefetched before the main loop (epi_prefetch)
+          rv[u] = er->rv[p][j0 + u];
+          y0v[u] = er->y0v[p][j0 + u];
+          y1v[u] = er->y1v[p][j0 + u];
+          mbits[u] = er->mb[p][j0 + u];
+          continue;
+        }
         const long long px = wpx0 + (j0 + u) * 16 + fr;
         const long long pc = px < a.M ? px : a.M - 1;
         const int srow = (int)(pc - bpx);
@@ -724,9 +777,12 @@ __device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&a
 }
 
 // BK (0 / 1 / 2 / 3, see pg_epilogue_k) and TWO select the fused epilogue.
-template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO>
+// PF: epilogue operands prefetched into registers before the main loop
+// (epi_prefetch) instead of staged through LDS after it
+template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false>
 __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   constexpr bool BNB = BK != 0;
+  static_assert(!PF || BK != 2, "PF: the bf16 mask operand of kind 2 is not prefetched");
   constexpr int NW = WPX * WCH;
   constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
   constexpr int IPX = BPX / (8 * NW);
@@ -869,6 +925,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     for (int i = tid; i < 6 * BCH; i += 64 * NW) red[i] = 0.f;
     if (tid == 0) *red_cnt = 0;
   }
+  EpiRegs<MTC / 2, NTP> er;
+  if constexpr (PF) epi_prefetch<BK, TWO, MTC, NTP, WTPX, WTCH>(a, er, bpx, bch, wpx, wch, fr, fq);
   const int nk = (a.K + 63) / 64;
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
@@ -896,6 +954,13 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   constexpr bool S_MK = BK == 2 && NOP >= 2 + (S_RES ? 1 : 0) + (S_Y1 ? 1 : 0);
   static_assert(!BNB || NOP >= 1, "y_0 must fit the stage ring");
   EpiStage sg{nullptr, nullptr, nullptr, nullptr, nullptr, BNB ? prm : nullptr, seg0};
+  if constexpr (PF) {
+    const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
+    pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, true>(a, acc, bpx, bch, wpx, wch, fr, fq,
+                                                                                red, sg, &er);
+    if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
+    return;
+  }
   if constexpr (BNB) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();  // every wave is done reading the stages
@@ -1660,6 +1725,37 @@ static void pg_launch_cfg(int c, const PgArgs& a, long long tiles, hipStream_t s
   }
 }
 
+// PF variants (candidates 11 / 12 / 13 = tile shapes 1 / 2 / 3 with the
+// epilogue operands prefetched into registers)
+template <int BK, bool TWO>
+static void pg_launch_pf(int base, const PgArgs& a, long long tiles, hipStream_t st) {
+  const dim3 g((unsigned)tiles);
+  switch (base) {
+    case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, false, BK, TWO, true>), g, dim3(512), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, false, BK, TWO, true>), g, dim3(512), 0, st, a); break;
+    default: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, false, BK, TWO, true>), g, dim3(256), 0, st, a); break;
+  }
+}
+
+static bool pg_pf_launch(int c, const PgArgs& a, bool multi, hipStream_t st) {
+  const int base = c - 10;
+  if (multi || base < 1 || base > 3) return false;
+  if (a.bnb == 2 || (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) || (a.bnb == 3 && !a.res_mode)) return false;
+  if (!a.bnb && (!a.res_mode || a.stats)) return false;  // plain: the data gradient with a residual
+  const PgCfg& g = kCfgs[base];
+  const long long tiles = ((a.M + g.bpx - 1) / g.bpx) * ((a.Cout + g.bch - 1) / g.bch);
+  if (tiles > 0x7fffffffLL) return false;
+  if (a.bnb == 1) pg_launch_pf<1, false>(base, a, tiles, st);
+  else if (a.bnb == 3 && a.bnb_nt == 2) pg_launch_pf<3, true>(base, a, tiles, st);
+  else if (a.bnb == 3) pg_launch_pf<3, false>(base, a, tiles, st);
+  else pg_launch_pf<0, false>(base, a, tiles, st);
+  static const char* names[2][3] = {{"pgemm_kernel<256,128,pf>", "pgemm_kernel<256,64,pf>", "pgemm_kernel<128,128,pf>"},
+                                    {"pgemm_kernel<256,128,bnb,pf>", "pgemm_kernel<256,64,bnb,pf>",
+                                     "pgemm_kernel<128,128,bnb,pf>"}};
+  set_last_kernel(names[a.bnb ? 1 : 0][base - 1]);
+  return true;
+}
+
 // the fused-epilogue variant of a launch: ACT (kind 1, one target, no
 // residual) or RES (kinds 2/3, residual present, one or two targets)
 template <bool MULTI>
@@ -1711,6 +1807,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (c == 21) return hconv_launch(a, st);
   bool multi;
   if (!pg_supported(a, multi)) return false;
+  if (c >= 11 && c <= 13) return pg_pf_launch(c, a, multi, st);
   if (c == 10) {
     const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
     const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);

@@ -56,7 +56,8 @@ __global__ void quickgelu_kernel(const T* __restrict__ x, long long n, T* __rest
 // through LDS; lane d accumulates output dimension d over the keys
 template <typename T>
 __global__ void __launch_bounds__(256) mha_fwd_kernel(const T* __restrict__ qkv, int L, int N, int heads,
-                                                      const float* __restrict__ mask, T* __restrict__ out) {
+                                                      const float* __restrict__ mask, T* __restrict__ out,
+                                                      float* __restrict__ lse) {
   __shared__ float ps[4][256];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long item = blockIdx.x * 4LL + w;  // (i, n, h) with h fastest
@@ -92,7 +93,9 @@ __global__ void __launch_bounds__(256) mha_fwd_kernel(const T* __restrict__ qkv,
     s[u] = p;
     sum += p;
   }
-  const float inv = 1.f / warp_sum(sum);
+  const float tot = warp_sum(sum);
+  const float inv = 1.f / tot;
+  if (lse && lane == 0) lse[item] = m + __logf(tot);  // log-sum-exp of the row (backward)
 #pragma unroll
   for (int u = 0; u < 4; ++u) ps[w][lane + 64 * u] = s[u] * inv;
   // the wave reads its own row of ps (LDS operations of a wave complete in order)
@@ -102,6 +105,240 @@ __global__ void __launch_bounds__(256) mha_fwd_kernel(const T* __restrict__ qkv,
   const T* vc = qkv + (long long)n * ld + 2 * E + h * 64 + lane;
   for (int j = 0; j < L; ++j) o += ps[w][j] * to_f(vc[(long long)j * N * ld]);
   out[((long long)i * N + n) * E + h * 64 + lane] = from_f<T>(o);
+}
+
+// ------------------------------------------------------------- backward
+// LayerNorm backward, one wave per row (rows strided over the grid so every
+// lane keeps its columns' dgamma / dbeta partial sums in registers and adds
+// them once): xhat = (x - mean) istd, g = dy gamma,
+// dx = istd (g - mean(g) - xhat mean(g xhat)); dgamma += dy xhat, dbeta += dy.
+template <typename T, int CPL>
+__global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                            const T* __restrict__ dy, long long rows, int C, float eps,
+                                                            const T* dres, T* dx,
+                                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int lane = threadIdx.x & 63;
+  float pg[CPL], pb[CPL];
+#pragma unroll
+  for (int u = 0; u < CPL; ++u) { pg[u] = 0.f; pb[u] = 0.f; }
+  for (long long row = blockIdx.x * 4LL + (threadIdx.x >> 6); row < rows; row += gridDim.x * 4LL) {
+    const T* xr = x + row * C;
+    const T* gr = dy + row * C;
+    float xv[CPL], gv[CPL];
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+      const int c = lane + 64 * u;
+      xv[u] = c < C ? to_f(xr[c]) : 0.f;
+      gv[u] = c < C ? to_f(gr[c]) : 0.f;
+      s += xv[u];
+    }
+    const float mean = warp_sum(s) / (float)C;
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+      const float d = lane + 64 * u < C ? xv[u] - mean : 0.f;
+      v += d * d;
+    }
+    const float istd = rsqrtf(warp_sum(v) / (float)C + eps);
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < C) {
+        const float xh = (xv[u] - mean) * istd;
+        const float g = gv[u] * gamma[c];
+        a += g;
+        b += g * xh;
+        pg[u] += gv[u] * xh;
+        pb[u] += gv[u];
+        xv[u] = xh;
+        gv[u] = g;
+      }
+    }
+    a = warp_sum(a) / (float)C;
+    b = warp_sum(b) / (float)C;
+    T* o = dx + row * C;
+    const T* rr = dres ? dres + row * C : nullptr;
+#pragma unroll
+    for (int u = 0; u < CPL; ++u) {
+      const int c = lane + 64 * u;
+      if (c < C) o[c] = from_f<T>(istd * (gv[u] - a - xv[u] * b) + (rr ? to_f(rr[c]) : 0.f));
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < CPL; ++u) {
+    const int c = lane + 64 * u;
+    if (c < C) {
+      atomicAdd(dgamma + c, pg[u]);
+      atomicAdd(dbeta + c, pb[u]);
+    }
+  }
+}
+
+// QuickGELU backward: d/dx [x s(1.702 x)] = s + 1.702 x s (1 - s)
+template <typename T>
+__global__ void quickgelu_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy, long long n,
+                                     T* __restrict__ dx) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = to_f(x[i]);
+    const float sg = 1.f / (1.f + __expf(-1.702f * v));
+    dx[i] = from_f<T>(to_f(dy[i]) * (sg + 1.702f * v * sg * (1.f - sg)));
+  }
+}
+
+// attention backward, query side, one wave per (query i, batch n, head h):
+// D_i = dO_i . O_i; per key j (lane j, j + 64, ...): p = exp(q.k_j / 8 + mask -
+// lse_i), dp = dO_i . v_j, ds = p (dp - D_i) -> LDS; lane d: dq_i[d] =
+// sum_j ds_j k_j[d] / 8.  D goes out for the key-side kernel.
+template <typename T>
+__global__ void __launch_bounds__(256) mha_bwd_q_kernel(const T* __restrict__ qkv, const T* __restrict__ o,
+                                                        const T* __restrict__ dout, const float* __restrict__ lse,
+                                                        int L, int N, int heads, const float* __restrict__ mask,
+                                                        T* __restrict__ dqkv, float* __restrict__ Dout) {
+  __shared__ float dss[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long item = blockIdx.x * 4LL + w;
+  if (item >= (long long)L * N * heads) return;
+  const int h = (int)(item % heads);
+  const long long in = item / heads;
+  const int n = (int)(in % N), i = (int)(in / N);
+  const int E = heads * 64;
+  const long long ld = 3LL * E;
+  const long long orow = ((long long)i * N + n) * E + h * 64;
+  const float Di = warp_sum(to_f(dout[orow + lane]) * to_f(o[orow + lane]));
+  if (lane == 0) Dout[item] = Di;
+  const T* qr = qkv + ((long long)i * N + n) * ld + h * 64;
+  float q[64], g[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) { q[d] = to_f(qr[d]) * 0.125f; g[d] = to_f(dout[orow + d]); }
+  const float li = lse[item];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = lane + 64 * u;
+    float ds = 0.f;
+    if (j < L) {
+      const T* kr = qkv + ((long long)j * N + n) * ld + E + h * 64;
+      const T* vr = kr + E;
+      float sc = 0.f, dp = 0.f;
+#pragma unroll 8
+      for (int d = 0; d < 64; ++d) { sc += q[d] * to_f(kr[d]); dp += g[d] * to_f(vr[d]); }
+      if (mask) sc += mask[(long long)i * L + j];
+      const float p = sc == -INFINITY ? 0.f : __expf(sc - li);
+      ds = p * (dp - Di);
+    }
+    dss[w][j] = ds;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  float acc = 0.f;
+  const T* kc = qkv + (long long)n * ld + E + h * 64 + lane;
+  for (int j = 0; j < L; ++j) acc += dss[w][j] * to_f(kc[(long long)j * N * ld]);
+  dqkv[((long long)i * N + n) * ld + h * 64 + lane] = from_f<T>(acc * 0.125f);
+}
+
+// attention backward, key side, one wave per (key j, batch n, head h): per
+// query i (lane i, i + 64, ...): p = exp(q_i.k_j / 8 + mask - lse_i), dp =
+// dO_i . v_j, ds = p (dp - D_i) -> LDS; lane d: dv_j[d] = sum_i p dO_i[d],
+// dk_j[d] = sum_i ds q_i[d] / 8
+template <typename T>
+__global__ void __launch_bounds__(256) mha_bwd_kv_kernel(const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                         const float* __restrict__ lse, const float* __restrict__ Din,
+                                                         int L, int N, int heads, const float* __restrict__ mask,
+                                                         T* __restrict__ dqkv) {
+  __shared__ float pss[4][256], dss[4][256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long item = blockIdx.x * 4LL + w;  // (j, n, h)
+  if (item >= (long long)L * N * heads) return;
+  const int h = (int)(item % heads);
+  const long long jn = item / heads;
+  const int n = (int)(jn % N), j = (int)(jn / N);
+  const int E = heads * 64;
+  const long long ld = 3LL * E;
+  const T* kr = qkv + ((long long)j * N + n) * ld + E + h * 64;
+  float k[64], v[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) { k[d] = to_f(kr[d]); v[d] = to_f(kr[E + d]); }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = lane + 64 * u;
+    float p = 0.f, ds = 0.f;
+    if (i < L) {
+      const long long it = ((long long)i * N + n) * heads + h;
+      const T* qr = qkv + ((long long)i * N + n) * ld + h * 64;
+      const T* gr = dout + ((long long)i * N + n) * E + h * 64;
+      float sc = 0.f, dp = 0.f;
+#pragma unroll 8
+      for (int d = 0; d < 64; ++d) { sc += (to_f(qr[d]) * 0.125f) * k[d]; dp += to_f(gr[d]) * v[d]; }
+      if (mask) sc += mask[(long long)i * L + j];
+      p = sc == -INFINITY ? 0.f : __expf(sc - lse[it]);
+      ds = p * (dp - Din[it]);
+    }
+    pss[w][i] = p;
+    dss[w][i] = ds;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  float dk = 0.f, dv = 0.f;
+  const T* qc = qkv + (long long)n * ld + h * 64 + lane;
+  const T* gc = dout + (long long)n * E + h * 64 + lane;
+  for (int i = 0; i < L; ++i) {
+    dk += dss[w][i] * to_f(qc[(long long)i * N * ld]);
+    dv += pss[w][i] * to_f(gc[(long long)i * N * E]);
+  }
+  T* o = dqkv + ((long long)j * N + n) * ld + h * 64 + lane;
+  o[E] = from_f<T>(dk * 0.125f);
+  o[2 * E] = from_f<T>(dv);
+}
+
+// ViT patch embedding operand: image [B][3][R][R] f32 -> rows [B*P][3*16*16]
+// (row b*P + p, column c*256 + kh*16 + kw: the flattened conv1 weight order)
+template <typename T>
+__global__ void patchify_kernel(const float* __restrict__ img, int B, int R, int ps, T* __restrict__ out) {
+  const int G = R / ps, P = G * G, K = 3 * ps * ps;
+  const long long n = (long long)B * P * K;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(t % K);
+    const long long r = t / K;
+    const int p = (int)(r % P), b = (int)(r / P);
+    const int c = k / (ps * ps), kh = (k / ps) % ps, kw = k % ps;
+    const int y = (p / G) * ps + kh, x = (p % G) * ps + kw;
+    out[t] = from_f<T>(img[(((long long)b * 3 + c) * R + y) * R + x]);
+  }
+}
+
+// tokens [L = P + 1][B][E]: token 0 = class embedding, token 1 + p = patch p,
+// plus the positional embedding (CLIP VisionTransformer.forward)
+template <typename T>
+__global__ void vit_tokens_kernel(const T* __restrict__ patches, const float* __restrict__ cls,
+                                  const float* __restrict__ pos, int B, int P, int E, T* __restrict__ out) {
+  const long long n = (long long)(P + 1) * B * E;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+    const int e = (int)(t % E);
+    const long long r = t / E;
+    const int b = (int)(r % B), l = (int)(r / B);
+    const float v = l == 0 ? cls[e] : to_f(patches[((long long)b * P + (l - 1)) * E + e]);
+    out[t] = from_f<T>(v + pos[(long long)l * E + e]);
+  }
+}
+
+// its backward: dpatches[b*P+p] = dtok[1+p][b]; dcls = sum_b dtok[0][b];
+// dpos[l] = sum_b dtok[l][b] (one thread per (l, e), loop over b: fixed order)
+template <typename T>
+__global__ void vit_tokens_bwd_kernel(const T* __restrict__ dtok, int B, int P, int E, T* __restrict__ dpatches,
+                                      float* __restrict__ dcls, float* __restrict__ dpos) {
+  const long long n = (long long)(P + 1) * E;
+  for (long long t = blockIdx.x * (long long)blockDim.x + threadIdx.x; t < n; t += (long long)gridDim.x * blockDim.x) {
+    const int e = (int)(t % E), l = (int)(t / E);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float g = to_f(dtok[((long long)l * B + b) * E + e]);
+      s += g;
+      if (l > 0) dpatches[((long long)b * P + (l - 1)) * E + e] = from_f<T>(g);
+    }
+    dpos[t] += s;
+    if (l == 0) dcls[e] += s;
+  }
 }
 
 #define VIT_DISPATCH(dtype, ...)                    \
@@ -145,14 +382,98 @@ extern "C" int artsbir_quickgelu(int dtype, const void* x, long long n, void* y,
   return 0;
 }
 
+extern "C" int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int heads, const float* mask,
+                                   void* out, float* lse, void* stream);
+
 extern "C" int artsbir_mha_fwd(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out,
                                void* stream) {
+  return artsbir_mha_fwd_lse(dtype, qkv, L, N, heads, mask, out, nullptr, stream);
+}
+
+extern "C" int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int heads, const float* mask,
+                                   void* out, float* lse, void* stream) {
   if (L < 1 || L > 256) { set_error("mha_fwd: sequence length %d outside [1, 256]", L); return -1; }
   if (heads < 1 || N < 1) { set_error("mha_fwd: bad batch %d / heads %d", N, heads); return -1; }
   const long long items = (long long)L * N * heads;
   const unsigned grid = (unsigned)((items + 3) / 4);
   VIT_DISPATCH(dtype, hipLaunchKernelGGL(mha_fwd_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)qkv, L, N, heads, mask, (T*)out));
+                                       (const T*)qkv, L, N, heads, mask, (T*)out, lse));
   ARTSBIR_CHECK_LAUNCH("mha_fwd");
+  return 0;
+}
+
+extern "C" int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamma, const void* dy, long long rows,
+                                     int C, float eps, const void* dres, void* dx, float* dgamma, float* dbeta,
+                                     void* stream) {
+  if (rows <= 0) return 0;
+  if (C < 1 || C > 1024) { set_error("layernorm_bwd: C=%d outside [1, 1024]", C); return -1; }
+  long long g = (rows + 3) / 4;
+  const unsigned grid = (unsigned)(g > 2048 ? 2048 : g);
+  const int cpl = (C + 63) / 64;
+#define LNB(N) VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_bwd_kernel<T, N>), dim3(grid), dim3(256), 0,        \
+                                                     (hipStream_t)stream, (const T*)x, gamma, (const T*)dy, rows, C, \
+                                                     eps, (const T*)dres, (T*)dx, dgamma, dbeta))
+  if (cpl <= 2) LNB(2);
+  else if (cpl <= 4) LNB(4);
+  else if (cpl <= 8) LNB(8);
+  else if (cpl <= 12) LNB(12);
+  else LNB(16);
+#undef LNB
+  ARTSBIR_CHECK_LAUNCH("layernorm_bwd");
+  return 0;
+}
+
+extern "C" int artsbir_quickgelu_bwd(int dtype, const void* x, const void* dy, long long n, void* dx, void* stream) {
+  if (n <= 0) return 0;
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_bwd_kernel<T>, dim3(vit_grid(n)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)x, (const T*)dy, n, (T*)dx));
+  ARTSBIR_CHECK_LAUNCH("quickgelu_bwd");
+  return 0;
+}
+
+extern "C" int artsbir_mha_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse,
+                               int L, int N, int heads, const float* mask, void* dqkv, float* dscratch,
+                               void* stream) {
+  if (L < 1 || L > 256) { set_error("mha_bwd: sequence length %d outside [1, 256]", L); return -1; }
+  if (heads < 1 || N < 1 || !lse || !dscratch) { set_error("mha_bwd: bad arguments"); return -1; }
+  const long long items = (long long)L * N * heads;
+  const unsigned grid = (unsigned)((items + 3) / 4);
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(mha_bwd_q_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)qkv, (const T*)out, (const T*)dout, lse, L, N, heads, mask,
+                                       (T*)dqkv, dscratch));
+  ARTSBIR_CHECK_LAUNCH("mha_bwd_q");
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(mha_bwd_kv_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)qkv, (const T*)dout, lse, dscratch, L, N, heads, mask, (T*)dqkv));
+  ARTSBIR_CHECK_LAUNCH("mha_bwd_kv");
+  return 0;
+}
+
+extern "C" int artsbir_vit_patchify(int dtype, const float* img, int B, int R, int patch, void* out, void* stream) {
+  if (patch < 1 || R % patch) { set_error("vit_patchify: resolution %d not a multiple of patch %d", R, patch); return -1; }
+  const long long n = (long long)B * (R / patch) * (R / patch) * 3 * patch * patch;
+  if (n <= 0) return 0;
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(patchify_kernel<T>, dim3(vit_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                                       img, B, R, patch, (T*)out));
+  ARTSBIR_CHECK_LAUNCH("vit_patchify");
+  return 0;
+}
+
+extern "C" int artsbir_vit_tokens(int dtype, const void* patches, const float* cls, const float* pos, int B, int P,
+                                  int E, void* out, void* stream) {
+  const long long n = (long long)(P + 1) * B * E;
+  if (n <= 0) return 0;
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(vit_tokens_kernel<T>, dim3(vit_grid(n)), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)patches, cls, pos, B, P, E, (T*)out));
+  ARTSBIR_CHECK_LAUNCH("vit_tokens");
+  return 0;
+}
+
+extern "C" int artsbir_vit_tokens_bwd(int dtype, const void* dtok, int B, int P, int E, void* dpatches, float* dcls,
+                                      float* dpos, void* stream) {
+  const long long n = (long long)(P + 1) * E;
+  if (n <= 0) return 0;
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(vit_tokens_bwd_kernel<T>, dim3(vit_grid(n)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)dtok, B, P, E, (T*)dpatches, dcls, dpos));
+  ARTSBIR_CHECK_LAUNCH("vit_tokens_bwd");
   return 0;
 }

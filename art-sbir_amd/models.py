@@ -306,142 +306,5 @@ class ModifiedResNet_with_classification(ModifiedResNet):
         return [self._heads(f) for f in self.encode_branches(xs)]
 
 
-def _vit_dt(x: torch.Tensor) -> int:
-    if not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
-        raise RuntimeError("transformer block: CUDA (HIP) f32/bf16 tensors only; there is no CPU path")
-    return _hip.DT_BF16 if x.dtype == torch.bfloat16 else _hip.DT_F32
-
-
-def _vit_stream() -> int:
-    return torch.cuda.current_stream().cuda_stream
-
-
-def _layernorm_hip(x: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:
-    dt = _vit_dt(x)
-    x = x.contiguous()
-    C = x.shape[-1]
-    y = torch.empty_like(x)
-    _hip.call("artsbir_layernorm_fwd", dt, x.data_ptr(), ln.weight.detach().float().contiguous().data_ptr(),
-              ln.bias.detach().float().contiguous().data_ptr(), x.numel() // C, C, float(ln.eps), y.data_ptr(),
-              _vit_stream())
-    return y
-
-
-def _weight_as(w: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """f32 parameter -> the compute dtype of x (artsbir_cast; no copy for f32)"""
-    w = w.detach().float().contiguous()
-    if x.dtype == torch.float32:
-        return w
-    out = torch.empty(w.shape, dtype=x.dtype, device=x.device)
-    _hip.call("artsbir_cast", _hip.DT_F32, w.data_ptr(), _hip.DT_BF16, out.data_ptr(), w.numel(), _vit_stream())
-    return out
-
-
-def _cast_hip(x: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
-    if x.dtype == dtype:
-        return x.clone()
-    out = torch.empty(x.shape, dtype=dtype, device=x.device)
-    _hip.call("artsbir_cast", _vit_dt(x), x.data_ptr(), _vit_dt(out), out.data_ptr(), x.numel(), _vit_stream())
-    return out
-
-
-def _linear_hip(x2: torch.Tensor, lin: nn.Linear, out: torch.Tensor = None) -> torch.Tensor:
-    """x2 [M][K] @ W^T + b on the MFMA GEMM; with `out` (f32) given it accumulates (out += ...)"""
-    M, K = x2.shape
-    N = lin.weight.shape[0]
-    w = _weight_as(lin.weight, x2)
-    b = lin.bias.detach().float().contiguous() if lin.bias is not None else None
-    acc = out is not None
-    if out is None:
-        out = torch.empty(M, N, dtype=x2.dtype, device=x2.device)
-    _hip.call("artsbir_gemm_nt", _vit_dt(x2), M, N, K, x2.data_ptr(), K, w.data_ptr(), out.data_ptr(), N,
-              1 if acc else 0, 1 if acc else 0, b.data_ptr() if b is not None else None, None, _vit_stream())
-    return out
-
-
-class _NoBackward(torch.autograd.Function):
-    """forward-only marker: y (computed by the library) joins the autograd graph
-    of `inputs`, and a backward through it raises (the reference never trains
-    this block, SURVEY §8 a7: forward parity only)"""
-
-    @staticmethod
-    def forward(ctx, y, *inputs):
-        return y.view_as(y)
-
-    @staticmethod
-    def backward(ctx, g):
-        raise NotImplementedError("transformer block backward is not built (SURVEY §8 a7: forward parity only)")
-
-
-class LayerNorm(nn.LayerNorm):
-    """fp32-computing LayerNorm (models.py:382-388) -> artsbir_layernorm_fwd.
-    Block-level only: the reference has no ViT model."""
-
-    def forward(self, x: torch.Tensor):
-        return _NoBackward.apply(_layernorm_hip(x, self), x, self.weight)
-
-
-class QuickGELU(nn.Module):
-    """x * sigmoid(1.702 x) (models.py:391-393) -> artsbir_quickgelu"""
-
-    def forward(self, x: torch.Tensor):
-        x = x.contiguous()
-        y = torch.empty_like(x)
-        _hip.call("artsbir_quickgelu", _vit_dt(x), x.data_ptr(), x.numel(), y.data_ptr(), _vit_stream())
-        return _NoBackward.apply(y, x)
-
-
-class ResidualAttentionBlock(nn.Module):
-    """models.py:396-417, forward on libartsbir_hip: LayerNorm (fp32) ->
-    in-projection (MFMA GEMM) -> per-head softmax(q k^T/8 + mask) v
-    (artsbir_mha_fwd) -> out-projection accumulated onto the residual ->
-    LayerNorm -> c_fc -> QuickGELU -> c_proj accumulated onto the residual.
-    Sequence-first x [L, N, E] as nn.MultiheadAttention; head_dim 64.  Same
-    submodules and state-dict keys as the reference."""
-
-    def __init__(self, d_model: int, n_head: int, attn_mask: torch.Tensor = None):
-        super().__init__()
-        self.attn = nn.MultiheadAttention(d_model, n_head)
-        self.ln_1 = LayerNorm(d_model)
-        self.mlp = nn.Sequential(OrderedDict([
-            ("c_fc", nn.Linear(d_model, d_model * 4)),
-            ("gelu", QuickGELU()),
-            ("c_proj", nn.Linear(d_model * 4, d_model))]))
-        self.ln_2 = LayerNorm(d_model)
-        self.attn_mask = attn_mask
-
-    def _mask(self, x):
-        if self.attn_mask is None:
-            return None
-        m = self.attn_mask.to(device=x.device)
-        if m.dtype == torch.bool:  # True = not allowed (nn.MultiheadAttention)
-            m = torch.zeros(m.shape, device=x.device).masked_fill(m, float("-inf"))
-        return m.to(x.dtype).float().contiguous()  # the reference casts the mask to x.dtype
-
-    def forward(self, x):
-        L, N, E = x.shape
-        heads = self.attn.num_heads
-        if E != heads * 64:
-            raise RuntimeError(f"transformer block: head_dim must be 64 (E={E}, heads={heads})")
-        dt = _vit_dt(x)
-        x = x.contiguous()
-        h = _layernorm_hip(x, self.ln_1).view(L * N, E)
-        # in-projection (q | k | v columns) with its bias
-        wi = _weight_as(self.attn.in_proj_weight, x)
-        bi = self.attn.in_proj_bias.detach().float().contiguous()
-        qkv = torch.empty(L * N, 3 * E, dtype=x.dtype, device=x.device)
-        _hip.call("artsbir_gemm_nt", dt, L * N, 3 * E, E, h.data_ptr(), E, wi.data_ptr(), qkv.data_ptr(), 3 * E, 0,
-                  0, bi.data_ptr(), None, _vit_stream())
-        att = torch.empty(L * N, E, dtype=x.dtype, device=x.device)
-        mask = self._mask(x)
-        _hip.call("artsbir_mha_fwd", dt, qkv.data_ptr(), L, N, heads, mask.data_ptr() if mask is not None else None,
-                  att.data_ptr(), _vit_stream())
-        # the residual stream accumulates in f32 (the GEMM adds onto it)
-        x1 = _cast_hip(x.view(L * N, E), torch.float32)
-        _linear_hip(att, self.attn.out_proj, out=x1)  # x + attention(ln_1(x))
-        h2 = _layernorm_hip(_cast_hip(x1, x.dtype) if x.dtype != torch.float32 else x1, self.ln_2)
-        f = _linear_hip(h2, self.mlp.c_fc)
-        _hip.call("artsbir_quickgelu", dt, f.data_ptr(), f.numel(), f.data_ptr(), _vit_stream())
-        _linear_hip(f, self.mlp.c_proj, out=x1)  # + mlp(ln_2(x))
-        y = _cast_hip(x1, x.dtype) if x.dtype != torch.float32 else x1
-        return _NoBackward.apply(y.view(L, N, E), x, self.attn.in_proj_weight)
+# transformer pieces (models.py:382-417) and the ViT-B/16 encoder of C5: vit.py
+from vit import LayerNorm, QuickGELU, ResidualAttentionBlock, Transformer, VisionTransformer  # noqa: E402,F401

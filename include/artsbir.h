@@ -210,7 +210,7 @@ int artsbir_attnpool_fwd(int dtype, const float* q, const void* kv, int B, int C
 int artsbir_attnpool_bwd(int dtype, const float* q, const void* kv, const float* p, const float* dout,
                          int B, int C, int heads, int T, void* dq, void* dkv, void* stream);
 
-/* ---- transformer block (models.py:382-417; SURVEY a7, forward) --------- */
+/* ---- transformer block (models.py:382-417) ------------------- */
 /* LayerNorm computed in fp32 whatever the storage dtype (models.py:382-388):
  * y[r] = (x[r] - mean) / sqrt(var + eps) * gamma + beta, rows of C. */
 int artsbir_layernorm_fwd(int dtype, const void* x, const float* gamma, const float* beta, long long rows, int C,
@@ -223,6 +223,46 @@ int artsbir_quickgelu(int dtype, const void* x, long long n, void* y, void* stre
  * [L][L] additive f32 or NULL. */
 int artsbir_mha_fwd(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out,
                     void* stream);
+/* The same, also writing lse[(i*N + n)*heads + h] = the log-sum-exp of each
+ * score row (what the backward needs to rebuild the probabilities). */
+int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out,
+                        float* lse, void* stream);
+
+/* ---- transformer block backward (the ViT-B/16 configuration C5) --------- */
+/* LayerNorm backward: dx = the LayerNorm input gradient (+ dres, the residual
+ * branch's gradient, when not NULL; dx may alias dres), dgamma / dbeta
+ * ACCUMULATED (f32), C <= 1024. */
+int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamma, const void* dy, long long rows, int C,
+                          float eps, const void* dres, void* dx, float* dgamma, float* dbeta, void* stream);
+/* QuickGELU backward: dx = dy * (s + 1.702 x s (1 - s)), s = sigmoid(1.702 x). */
+int artsbir_quickgelu_bwd(int dtype, const void* x, const void* dy, long long n, void* dx, void* stream);
+/* Attention backward: dqkv [L*N][3E] (dq | dk | dv, overwritten) from qkv, the
+ * forward output out, its gradient dout and lse (artsbir_mha_fwd_lse);
+ * dscratch: f32 [L*N*heads] (the per-row dout . out). */
+int artsbir_mha_bwd(int dtype, const void* qkv, const void* out, const void* dout, const float* lse, int L, int N,
+                    int heads, const float* mask, void* dqkv, float* dscratch, void* stream);
+
+/* ---- fp8 projections (configuration C5, "ViT-B/16 768-d fp8") ----------
+ * q = e4m3fn(x / s) with s = amax|x| / 448 (1 when x is all zero) written to
+ * scale[0] (device f32); n elements of x (dtype f32 / bf16). */
+int artsbir_quantize_fp8(int dtype, const void* x, long long n, unsigned char* q, float* scale, void* stream);
+/* C[M][N] = sa[0] * sb[0] * sum_k A[m][k] B[n][k] (+ bias[n]) (+ C when accumulate;
+ * then out_dtype must be f32) on e4m3fn operands (block-scaled MFMA, unit
+ * block scales); K % 128 == 0; sa, sb, bias device f32. */
+int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, const unsigned char* b, const float* sa,
+                        const float* sb, const float* bias, void* c, int out_dtype, int accumulate, void* stream);
+
+/* ---- ViT-B/16 embedding (CLIP VisionTransformer: conv1 patch16, class
+ * token, positional embedding) ------------------------------------------ */
+/* img f32 [B][3][R][R] -> rows [B*P][3*patch*patch] in conv-weight order (the
+ * patch convolution as a GEMM). */
+int artsbir_vit_patchify(int dtype, const float* img, int B, int R, int patch, void* out, void* stream);
+/* tokens [P+1][B][E] (sequence-first): class embedding / patch rows, + pos. */
+int artsbir_vit_tokens(int dtype, const void* patches, const float* cls, const float* pos, int B, int P, int E,
+                       void* out, void* stream);
+/* its backward: dpatches [B*P][E] (overwritten), dcls [E] and dpos [P+1][E] ACCUMULATED. */
+int artsbir_vit_tokens_bwd(int dtype, const void* dtok, int B, int P, int E, void* dpatches, float* dcls,
+                           float* dpos, void* stream);
 
 /* ---- loss and optimizer (train.py:158,169) ------------------------------ */
 int artsbir_triplet_fwd(const float* a, const float* p, const float* n, int B, int D, float margin, float eps,

@@ -219,3 +219,26 @@ def synthetic_triplet(batch: int, res: int, seed: int = 0):
             img = rng.random((batch, 3, res, res), dtype=np.float32)
         out.append(torch.from_numpy(((img - mean) / std).astype(np.float32)))
     return tuple(out)
+
+
+def vision_transformer(x, sd, patch, n_head, eps=1e-5):
+    """CLIP's VisionTransformer.forward (the C5 encoder; the reference ships only
+    its blocks, models.py:382-417) on a state dict with CLIP's keys: conv1
+    patch embedding, class token, positional embedding, ln_pre, resblocks,
+    ln_post of the class token, proj.  x [B, 3, R, R] -> [B, output_dim]."""
+    B = x.shape[0]
+    t = F.conv2d(x, sd["conv1.weight"], stride=patch)                  # [B, E, G, G]
+    t = t.reshape(B, t.shape[1], -1).permute(0, 2, 1)                  # [B, P, E]
+    cls = sd["class_embedding"].to(t.dtype) + torch.zeros(B, 1, t.shape[-1], dtype=t.dtype)
+    t = torch.cat([cls, t], dim=1) + sd["positional_embedding"].to(t.dtype)
+    t = layernorm_fp32(t, sd["ln_pre.weight"], sd["ln_pre.bias"], eps)
+    t = t.permute(1, 0, 2)                                             # [L, B, E]
+    i = 0
+    while f"transformer.resblocks.{i}.ln_1.weight" in sd:
+        pre = f"transformer.resblocks.{i}."
+        t = residual_attention_block(t, {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)}, n_head,
+                                     eps=eps)
+        i += 1
+    t = t.permute(1, 0, 2)
+    c = layernorm_fp32(t[:, 0, :], sd["ln_post.weight"], sd["ln_post.bias"], eps)
+    return c @ sd["proj"]

@@ -73,11 +73,172 @@ def test_hip_block_matches_oracle(L, N, E, heads, masked, dtype, tol, dev):
     assert err < tol, float(err)
 
 
+def _block_oracle_grads(blk_sd, x, heads, mask, w):
+    """f64 oracle forward + autograd backward of sum(y * w)"""
+    sd = {k: v.double().clone().requires_grad_(True) for k, v in blk_sd.items()}
+    xr = x.double().clone().requires_grad_(True)
+    y = oenc.residual_attention_block(xr, sd, heads, mask.double() if mask is not None else None)
+    (y * w).sum().backward()
+    return y.detach(), xr.grad, {k: v.grad for k, v in sd.items()}
+
+
 @pytest.mark.gpu
-def test_hip_block_backward_refuses(dev):
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-4), (torch.bfloat16, 4e-2)])
+@pytest.mark.parametrize("L,N,E,heads,masked", [(9, 3, 128, 2, False), (197, 2, 768, 12, False),
+                                                 (17, 4, 256, 4, True)])
+def test_hip_block_backward_matches_oracle(L, N, E, heads, masked, dtype, tol, dev):
+    """input and parameter gradients of the block (artsbir_mha_bwd, layernorm_bwd,
+    quickgelu_bwd, the projection GEMMs) against float64 autograd of the oracle"""
     import models
-    blk = models.ResidualAttentionBlock(128, 2).to(dev)
-    x = torch.randn(5, 2, 128, device=dev, requires_grad=True)
-    y = blk(x)
-    with pytest.raises(NotImplementedError):
-        y.sum().backward()
+    torch.manual_seed(13)
+    mask = torch.triu(torch.full((L, L), float("-inf")), 1) if masked else None
+    blk = models.ResidualAttentionBlock(E, heads, attn_mask=mask)
+    for m in (blk.ln_1, blk.ln_2):
+        nn.init.normal_(m.weight, 1.0, 0.1)
+        nn.init.normal_(m.bias, 0.0, 0.1)
+    sd = {k: v.detach().clone() for k, v in blk.state_dict().items()}
+    x = torch.randn(L, N, E, generator=torch.Generator().manual_seed(14))
+    if dtype == torch.bfloat16:
+        x = x.bfloat16().float()
+    w = torch.randn(L, N, E, generator=torch.Generator().manual_seed(15), dtype=torch.float64)
+    y_ref, dx_ref, g_ref = _block_oracle_grads(sd, x, heads, mask, w)
+    blk = blk.to(dev)
+    xm = x.to(dev, dtype).requires_grad_(True)
+    y = blk(xm)
+    (y.float() * w.float().to(dev)).sum().backward()
+    rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(y.detach(), y_ref) < tol
+    assert rel(xm.grad, dx_ref) < tol * 2, rel(xm.grad, dx_ref)
+    named = dict(blk.named_parameters())
+    for k, g in g_ref.items():
+        e = rel(named[k].grad, g)
+        assert e < tol * 5, (k, e)
+
+
+@pytest.mark.gpu
+def test_fp8_gemm_matches_dequantized_reference(dev):
+    """artsbir_quantize_fp8 = torch's e4m3fn cast of x / (amax / 448) bit for bit;
+    artsbir_gemm_nt_fp8 = the f64 product of the dequantized operands (+ bias),
+    within f32 accumulation error; ragged M / N tiles"""
+    import _hip
+    import vit
+    g = torch.Generator(device=dev).manual_seed(3)
+    for M, N, K in [(200, 136, 256), (130, 2304, 768), (1, 1, 128)]:
+        a = torch.randn(M, K, device=dev, generator=g)
+        b = torch.randn(N, K, device=dev, generator=g) * 0.05
+        bias = torch.randn(N, device=dev, generator=g)
+        qa, sa = vit._fp8(a)
+        qb, sb = vit._fp8(b)
+        for t, q, s in ((a, qa, sa), (b, qb, sb)):
+            tc = t.cpu()  # the oracle on the CPU: IEEE f32 division, then torch's RNE e4m3fn cast
+            v = tc / (tc.abs().max() / 448.0)
+            want = v.to(torch.float8_e4m3fn).view(torch.uint8).to(dev)
+            bad = (q != want).nonzero()
+            if len(bad):
+                i = tuple(bad[0].tolist())
+                print("fp8 mismatch", len(bad), "of", q.numel(), "value", v[i].item(), "mine", q[i].item(),
+                      "torch", want[i].item())
+            assert torch.equal(q, want)
+            assert torch.allclose(s, t.abs().max().reshape(1) / 448.0, rtol=1e-7)
+        out = torch.empty(M, N, device=dev)
+        _hip.call("artsbir_gemm_nt_fp8", M, N, K, qa.data_ptr(), qb.data_ptr(), sa.data_ptr(), sb.data_ptr(),
+                  bias.data_ptr(), out.data_ptr(), _hip.DT_F32, 0, _hip.stream())
+        da = qa.view(torch.float8_e4m3fn).double().cpu() * sa.double().cpu()
+        db = qb.view(torch.float8_e4m3fn).double().cpu() * sb.double().cpu()
+        ref = da @ db.T + bias.double().cpu()
+        err = (out.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 5e-5, (M, N, K, err)  # f32 accumulation of up to 768 products
+
+
+def _vit_pair(seed, res=64, patch=16, width=128, layers=2, heads=2, out=64):
+    import models
+    torch.manual_seed(seed)
+    m = models.VisionTransformer(res, patch, width, layers, heads, out)
+    for blk in m.transformer.resblocks:
+        for ln in (blk.ln_1, blk.ln_2):
+            nn.init.normal_(ln.weight, 1.0, 0.1)
+            nn.init.normal_(ln.bias, 0.0, 0.1)
+    return m, {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,tol", [("f32", 3e-4), ("bf16", 5e-2), ("fp8", 1.5e-1)])
+def test_vit_encoder_matches_oracle(mode, tol, dev):
+    """the ViT encoder (patch GEMM, tokens, ln_pre, blocks, ln_post, proj) forward and
+    its gradients (fp8: forward GEMMs in e4m3, backward bf16) vs float64 autograd"""
+    m, sd = _vit_pair(21)
+    x = torch.randn(3, 3, 64, 64, generator=torch.Generator().manual_seed(22))
+    w = torch.randn(3, 64, generator=torch.Generator().manual_seed(23), dtype=torch.float64)
+    sdr = {k: v.double().clone().requires_grad_(True) for k, v in sd.items()}
+    y_ref = oenc.vision_transformer(x.double(), sdr, 16, 2)
+    (y_ref * w).sum().backward()
+    m = m.to(dev)
+    m.compute_dtype = {"f32": torch.float32, "bf16": torch.bfloat16, "fp8": "fp8"}[mode]
+    y = m(x.to(dev))
+    assert y.dtype == torch.float32 and y.shape == (3, 64)
+    (y * w.float().to(dev)).sum().backward()
+    rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(y.detach(), y_ref.detach()) < tol, rel(y.detach(), y_ref.detach())
+    named = dict(m.named_parameters())
+    worst = max((rel(named[k].grad, v.grad), k) for k, v in sdr.items())
+    assert worst[0] < tol * 5, worst
+
+
+@pytest.mark.gpu
+def test_vit_backward_kernels_individually(dev):
+    """artsbir_layernorm_bwd, artsbir_quickgelu_bwd and artsbir_mha_bwd each
+    against float64 autograd of their oracle op (f32 storage)"""
+    import _hip
+    g = torch.Generator().manual_seed(31)
+    st = _hip.stream()
+    # LayerNorm
+    rows, C = 37, 768
+    x = torch.randn(rows, C, generator=g)
+    gam, bet = 1 + 0.1 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(rows, C, generator=g)
+    res = torch.randn(rows, C, generator=g)
+    xr = x.double().requires_grad_(True)
+    gr, br = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    (oenc.layernorm_fp32(xr, gr, br) * dy.double()).sum().backward()
+    X, G, Dy, Rs = (t.to(dev) for t in (x, gam, dy, res))
+    dx = torch.empty_like(X)
+    dg = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    _hip.call("artsbir_layernorm_bwd", _hip.DT_F32, X.data_ptr(), G.data_ptr(), Dy.data_ptr(), rows, C, 1e-5,
+              Rs.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), st)
+    rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(dx, xr.grad + res.double()) < 1e-5
+    assert rel(dg, gr.grad) < 1e-5 and rel(db, br.grad) < 1e-5
+    # QuickGELU
+    v = torch.randn(1000, generator=g) * 3
+    vr = v.double().requires_grad_(True)
+    gv = torch.randn(1000, generator=g)
+    (oenc.quick_gelu(vr) * gv.double()).sum().backward()
+    V, GV = v.to(dev), gv.to(dev)
+    dv = torch.empty_like(V)
+    _hip.call("artsbir_quickgelu_bwd", _hip.DT_F32, V.data_ptr(), GV.data_ptr(), 1000, dv.data_ptr(), st)
+    assert rel(dv, vr.grad) < 1e-5
+    # attention core
+    L, N, heads = 9, 3, 2
+    E = 64 * heads
+    qkv = torch.randn(L * N, 3 * E, generator=g)
+    dO = torch.randn(L * N, E, generator=g)
+    qr = qkv.double().requires_grad_(True)
+    q, k, vv = qr.view(L, N, 3 * E).split(E, dim=-1)
+
+    def hd(t):
+        return t.reshape(L, N, heads, 64).permute(1, 2, 0, 3)
+    p = torch.softmax((hd(q) / 8.0) @ hd(k).transpose(-1, -2), dim=-1)
+    o = (p @ hd(vv)).permute(2, 0, 1, 3).reshape(L * N, E)
+    (o * dO.double()).sum().backward()
+    Q, DO = qkv.to(dev), dO.to(dev)
+    out = torch.empty(L * N, E, device=dev)
+    lse = torch.empty(L * N * heads, device=dev)
+    _hip.call("artsbir_mha_fwd_lse", _hip.DT_F32, Q.data_ptr(), L, N, heads, None, out.data_ptr(), lse.data_ptr(), st)
+    assert rel(out, o.detach()) < 1e-5
+    dq = torch.empty_like(Q)
+    dsc = torch.empty(L * N * heads, device=dev)
+    _hip.call("artsbir_mha_bwd", _hip.DT_F32, Q.data_ptr(), out.data_ptr(), DO.data_ptr(), lse.data_ptr(), L, N,
+              heads, None, dq.data_ptr(), dsc.data_ptr(), st)
+    for part, sl in (("q", slice(0, E)), ("k", slice(E, 2 * E)), ("v", slice(2 * E, 3 * E))):
+        assert rel(dq[:, sl], qr.grad[:, sl]) < 1e-5, part
