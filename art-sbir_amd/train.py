@@ -145,7 +145,7 @@ def parse_args(argv=None):
     p.add_argument("-l", "--learning_rate", type=float, default=0.00001)
     p.add_argument("-m", "--model", type=str, default='openResNet50m.pth')
     p.add_argument('--model_type', type=str, default='ModifiedResNet',
-                   choices=['ModifiedResNet', 'ModifiedResNet_with_classification'])
+                   choices=['ModifiedResNet', 'ModifiedResNet_with_classification', 'VisionTransformer'])
     p.add_argument("-d", "--dataset", type=str, default='Synthetic')
     p.add_argument("-s", "--dsize", type=float, default=1.0)
     p.add_argument("--inference", action="store_true")
@@ -158,7 +158,8 @@ def parse_args(argv=None):
     p.add_argument('--loss_type', default='euclidean', choices=['euclidean', 'cosine'])
     p.add_argument('--loss_margin', type=float, default=0.2)
     # additions
-    p.add_argument('--dtype', default='f32', choices=['f32', 'bf16'], help="encoder compute dtype")
+    p.add_argument('--dtype', default='f32', choices=['f32', 'bf16', 'fp8'],
+                   help="encoder compute dtype (fp8: the ViT's projection GEMMs)")
     p.add_argument('--layers', default='3,4,6,3', help="ModifiedResNet layers (reference: 3,4,6,3)")
     p.add_argument('--output_dim', type=int, default=1024)
     p.add_argument('--resolution', type=int, default=224)
@@ -184,7 +185,9 @@ def main(argv=None):
     if os.path.isfile(os.path.join("models", args.model)):
         model = utils.load_model(args.model, dataset=args.dataset, model_type=args.model_type)
     model.freeze_layers()
-    model.compute_dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    model.compute_dtype = {"bf16": torch.bfloat16, "f32": torch.float32, "fp8": "fp8"}[args.dtype]
+    if args.dtype == "fp8" and not isinstance(model, models.VisionTransformer):
+        raise SystemExit("--dtype fp8 applies to the ViT encoder (--model_type VisionTransformer)")
     model.to(device)
     ddp.broadcast_parameters(model)
     train_dataset, test_dataset = data_preparation.get_datasets(dataset=args.dataset, size=args.dsize,

@@ -113,7 +113,10 @@ DATASETS_V1 = ['SketchyV1', 'SketchyDatasetV1', 'Sketchy', 'KaggleV1', 'KaggleDa
 
 
 def build_model(dataset: str = None, model_type: str = None, layers=(3, 4, 6, 3), output_dim=1024, **kw) -> nn.Module:
-    """The ModifiedResNet branches of utils.load_model (utils.py:166-197)."""
+    """The ModifiedResNet branches of utils.load_model (utils.py:166-197), and the
+    ViT-B/16 encoder of configuration C5 (model_type 'VisionTransformer')."""
+    if model_type in ('VisionTransformer', 'ViT-B/16'):
+        return models.VisionTransformer(kw.get('input_resolution', 224), 16, 768, 12, 12, output_dim)
     if model_type == 'ModifiedResNet' or dataset in DATASETS_V1:
         return models.ModifiedResNet(layers=layers, output_dim=output_dim, **kw)
     if model_type == 'ModifiedResNet_with_classification' and dataset in ['SketchyV2', 'SketchyDatasetV2']:

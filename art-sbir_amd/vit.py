@@ -428,6 +428,8 @@ class VisionTransformer(nn.Module):
         self.proj = nn.Parameter(scale * torch.randn(width, output_dim))
         self.compute_dtype = torch.float32
         self.trained_layers = []
+        import models  # the encoder's image transform (models.py:289-295); imported late (models imports vit)
+        self.transform = models.ClipTransform(input_resolution)
 
     def freeze_layers(self):
         self.trained_layers.append('all')

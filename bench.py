@@ -281,6 +281,9 @@ def main():
     ap.add_argument("--unbatched", dest="batched", action="store_false",
                     help="three separate encoder calls per step instead of forward_branches")
     ap.add_argument("--no-embed", action="store_true", help="skip the embed-only (eval-BN) leg")
+    ap.add_argument("--c5", action="store_true",
+                    help="add the C5 leg: ViT-B/16 768-d triplet training step, fp8 projections, 512 triplets")
+    ap.add_argument("--c5-batch", type=int, default=512, help="C5 triplets per GPU per step")
     ap.add_argument("--no-loss-check", action="store_true", help="skip the f32 step-0 loss check")
     ap.add_argument("--tune-cache", default=None,
                     help="autotuner choices file: loaded first if it exists, written after the warm-up "
@@ -441,12 +444,15 @@ def main():
             "roofline": roof,
         }
     emb = None if args.no_embed else embed_leg(model, batch, args.dtype, world, args.steps)
+    c5 = c5_leg(dev, rank, world, args.c5_batch, max(2, args.steps // 2)) if args.c5 else None
     ret = None if args.no_retrieval else retrieval_leg(dev, rank, world)
     if rank == 0:
         if emb is not None:
             line["embed"] = emb
         if ret is not None:
             line["retrieval"] = ret
+        if c5 is not None:
+            line["c5"] = c5
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
             # C1 (BASELINE configs[0]): the "ResNet18 128-d" config = ModifiedResNet((2,2,2,2),128), batch 32
@@ -458,6 +464,56 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def c5_leg(dev, rank, world, B, steps, warmup=1):
+    """BASELINE configs[4] / SURVEY C5: ViT-B/16 (CLIP VisionTransformer, 224^2, patch 16,
+    12 x 768, 12 heads) -> 768-d, triplet step (3 branch calls as one batch: no
+    BatchNorm in a ViT), fp8 e4m3 projection GEMMs in the forward, bf16 elsewhere,
+    Adam; synthetic normalised images resident in HBM.  Algorithmic work: 3 x
+    (forward FLOPs) per image, forward = 35.1 GFLOP."""
+    import losses
+    import optim
+    import vit
+    torch.manual_seed(4321)
+    model = vit.VisionTransformer(224, 16, 768, 12, 12, 768).to(dev)
+    model.compute_dtype = "fp8"
+    model.train()
+    opt = optim.Adam(model.parameters(), lr=1e-5, weight_decay=0.002)
+    loss_fn = losses.TripletMarginLoss(margin=0.2)
+    g = torch.Generator(device=dev).manual_seed(200 + rank)
+    xs = [torch.randn(B, 3, 224, 224, device=dev, generator=g) for _ in range(3)]
+
+    def step():
+        outs = model.forward_branches(xs)
+        loss = loss_fn(*outs)
+        opt.zero_grad(set_to_none=False)
+        loss.backward()
+        if world > 1:
+            for p in model.parameters():
+                dist.all_reduce(p.grad, op=dist.ReduceOp.AVG)
+        opt.step()
+        return loss
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    images = 3 * B * world * steps
+    flops = 3 * 35.1e9 * images
+    return {"metric": "triplet-images/sec, ViT-B/16 768-d fp8 (C5)", "value": round(images / el, 2),
+            "unit": "triplet-images/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 2),
+            "triplets_per_gpu": B, "dtype": "fp8 e4m3 projections (forward), bf16 otherwise",
+            "tflops": round(flops / el / 1e12, 1), "loss": float(loss.item()), "data": "synthetic"}
 
 
 if __name__ == "__main__":
