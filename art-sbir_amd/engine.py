@@ -181,6 +181,7 @@ class Engine:
         # ddp.OverlappedReducer (or None): told which gradient ranges are final
         # as the backward proceeds, so the data-parallel all-reduce overlaps it
         self.grad_hook = None
+        self._side_keep = []  # tensors the weight-gradient stream still reads (released at the join)
 
     # ------------------------------------------------------------------ utils
     @property
@@ -477,6 +478,7 @@ class Engine:
             hook.end(streams)  # block 0, the stem and anything unreported
         if OVERLAP_WGRAD:
             torch.cuda.current_stream().wait_stream(self._side_stream(dev))
+        self._side_keep = []
         return grads
 
     def _attnpool_bwd(self, ap, pk, c, dout, grads):
@@ -647,9 +649,15 @@ class Engine:
         with torch.cuda.stream(side):
             self._wgrad_sync(dy, a, conv, stride, pad, grads, ci_pad)
         # the caching allocator must not hand these to the main stream before
-        # the side stream is done with them
-        dy.record_stream(side)
-        a.t.record_stream(side)
+        # the side stream is done with them: they stay referenced until the
+        # backward's final join (main waits for side), after which their blocks
+        # return to the main stream's pool in stream order.  (record_stream
+        # would instead tie every block to the side stream's progress, so the
+        # allocator keeps mallocing fresh blocks — ~60 hipMallocs a step, the
+        # pool creeping towards the 288 GB capacity, and an occasional
+        # seconds-long stall when the driver has to make room.)
+        self._side_keep.append(dy)
+        self._side_keep.append(a.t)
 
     def _wgrad_sync(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):
         B, H, W, C = a.shape
@@ -852,6 +860,7 @@ class ModuleEngine(Engine):
             dh = self._attnpool_bwd(m, pk, state["c"], dout.contiguous().float(), grads)
         if OVERLAP_WGRAD:
             torch.cuda.current_stream().wait_stream(self._side_stream(dev))
+        self._side_keep = []
         return dh.permute(0, 3, 1, 2).float().contiguous()
 
 

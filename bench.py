@@ -31,13 +31,14 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # MI355X dense (MI355X_MICROA
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s measured copy)
 # per-launch HBM bytes of each kernel from the committed rocprofv3 PMC passes
 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/summarize_pmc.py)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r1_pmc_traffic.json")
+PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r2_pmc_traffic.json"))
 
 
 def pmc_traffic(kernel):
     try:
         with open(PMC_TRAFFIC) as f:
-            k = json.load(f)["kernels"].get(kernel)
+            ks = json.load(f)["kernels"]
+        k = ks.get(kernel) or ks.get(kernel.split("<")[0])  # template arguments not in the profiler name
     except (OSError, ValueError, KeyError):
         return None
     return None if k is None else round(k["hbm_bytes_per_launch"])
@@ -281,6 +282,7 @@ def main():
     ap.add_argument("--unbatched", dest="batched", action="store_false",
                     help="three separate encoder calls per step instead of forward_branches")
     ap.add_argument("--no-embed", action="store_true", help="skip the embed-only (eval-BN) leg")
+    ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step")
     ap.add_argument("--c5", action="store_true",
                     help="add the C5 leg: ViT-B/16 768-d triplet training step, fp8 projections, 512 triplets")
     ap.add_argument("--c5-batch", type=int, default=512, help="C5 triplets per GPU per step")
@@ -365,6 +367,8 @@ def main():
         li = step()
         if i == 0:
             loss0 = float(li.item())
+        if args.sync_warmup:
+            torch.cuda.synchronize()
     torch.cuda.synchronize()
     if args.tune_cache and rank == 0:
         _hip.lib().artsbir_tune_save(args.tune_cache.encode())
@@ -372,22 +376,41 @@ def main():
         ddp.broadcast_buffers(model)
         dist.barrier()
     torch.cuda.synchronize()
-    prof = [] if not args.no_profile else None
-    _hip.PROFILE = prof
+    ms0 = torch.cuda.memory_stats(dev)
+    # the timed region: K steps, nothing recorded per launch (the per-launch HIP
+    # events of the profiling pass cost host time that shows up as GPU idle gaps
+    # once the step is this short)
+    step_ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    step_ev[0].record()
+    for i in range(args.steps):
         loss = step()
+        step_ev[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    _hip.PROFILE = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     last_loss = float(loss.item())
+    ms1 = torch.cuda.memory_stats(dev)
+    alloc = {"step_ms": [round(step_ev[i].elapsed_time(step_ev[i + 1]), 2) for i in range(args.steps)],
+             "retries_timed": ms1.get("num_alloc_retries", 0) - ms0.get("num_alloc_retries", 0),
+             "device_mallocs_timed": ms1.get("num_device_alloc", 0) - ms0.get("num_device_alloc", 0),
+             "reserved_peak_gb": round(ms1.get("reserved_bytes.all.peak", 0) / 2**30, 1),
+             "allocated_peak_gb": round(ms1.get("allocated_bytes.all.peak", 0) / 2**30, 1)}
+    # the roofline pass: the same K steps again, every launch bracketed by HIP
+    # events on the stream it runs on (kernel durations, not the step time)
+    prof = [] if not args.no_profile else None
+    if prof is not None:
+        _hip.PROFILE = prof
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        _hip.PROFILE = None
 
     if rank == 0:
         images = 3 * B * world * args.steps
@@ -442,6 +465,7 @@ def main():
             "loss_step0_rel_diff": (round(abs(loss0 - loss_f32) / max(abs(loss_f32), 1e-12), 6)
                                     if loss_f32 is not None else None),
             "roofline": roof,
+            "allocator": alloc,
         }
     emb = None if args.no_embed else embed_leg(model, batch, args.dtype, world, args.steps)
     c5 = c5_leg(dev, rank, world, args.c5_batch, max(2, args.steps // 2)) if args.c5 else None
