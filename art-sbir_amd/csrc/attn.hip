@@ -1,0 +1,366 @@
+// MFMA attention core of the ViT blocks (bf16 compute mode): softmax(q k^T / 8
+// + mask) v of nn.MultiheadAttention as ResidualAttentionBlock uses it
+// (/root/reference/models.py:396-417), forward and backward, for head_dim 64
+// and sequences up to 256 (ViT-B/16: 197 tokens).
+//
+// One workgroup per (batch n, head h); wave w owns the 32-row block w of the
+// sequence (nb = ceil(L / 32) waves).  The whole (L x 64) slices the block
+// needs sit in LDS as swizzled images of 128-B rows (16-B chunk c of row j at
+// chunk c ^ at_sw(j): conflict-free for both the row reads of the MFMA A
+// operand and the 4-row transposed reads ds_read_b64_tr_b16).
+//
+// Orientation (v_mfma_f32_32x32x16_bf16, C/D: column = lane & 31, rows in the
+// 16 registers): every score tile is computed so that the product that
+// follows sums over the tile's ROW index — then its registers, rounded to
+// bf16, are that product's B operand as they are (k order permuted: element j
+// of lane half hh is row 16s + 8(j >> 2) + 4hh + (j & 3) of k-step s), and the
+// other operand is read transposed from LDS in the same permuted order.
+//   forward (wave = 32 queries):   S^T = K Q^T, online softmax over the keys
+//                                  (rows), O^T += V^T P^T
+//   backward, query side:          S^T, dP^T = V dO^T, dS^T = P^T (dP^T - D),
+//                                  dQ^T += K^T dS^T;  D_i = dO_i . O_i
+//   backward, key side (32 keys):  S = Q K^T, dP = dO V^T, dS = P (dP - D),
+//                                  dV^T += dO^T P, dK^T += Q^T dS
+// P is recomputed from the forward's per-row log-sum-exp; nothing of size
+// L x L leaves the registers.
+#include "common.h"
+
+namespace artsbir {
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef short at_v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void* at_lds_t;
+typedef __attribute__((address_space(3))) at_v4s* at_lds_v4s;
+
+constexpr int AT_MAXB = 8;                  // 32-row blocks: L <= 256
+constexpr int AT_IMG = AT_MAXB * 32 * 128;  // one [256][64] bf16 image
+
+__device__ __forceinline__ int at_sw(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int at_off(int row, int chunk) { return row * 128 + ((chunk ^ at_sw(row)) << 4); }
+
+// rows [0, 32 nb) of two (L x 64) head slices (row strides lda / ldb elements)
+// -> swizzled images; rows >= L are zero.  nthr = 64 nb threads, 4 chunks each.
+__device__ __forceinline__ void at_stage2(const bf16* __restrict__ a, long long lda, const bf16* __restrict__ b,
+                                          long long ldb, int L, char* ia, char* ib, int tid, int nthr) {
+  uint4 va[4], vb[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = tid + u * nthr, row = c >> 3, ch = c & 7;
+    va[u] = make_uint4(0, 0, 0, 0);
+    vb[u] = make_uint4(0, 0, 0, 0);
+    if (row < L) {
+      va[u] = *reinterpret_cast<const uint4*>(a + row * lda + ch * 8);
+      vb[u] = *reinterpret_cast<const uint4*>(b + row * ldb + ch * 8);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int c = tid + u * nthr, row = c >> 3, ch = c & 7;
+    *reinterpret_cast<uint4*>(ia + at_off(row, ch)) = va[u];
+    *reinterpret_cast<uint4*>(ib + at_off(row, ch)) = vb[u];
+  }
+}
+
+// A operand (row read): row `row`, k-step s (d = 16 s .. 16 s + 15) of lane half hh
+__device__ __forceinline__ bf16x8 at_row(const char* img, int row, int s, int hh) {
+  return *reinterpret_cast<const bf16x8*>(img + at_off(row, 2 * s + hh));
+}
+
+__device__ __forceinline__ at_v4s at_tr(const char* img, int row, int col) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (at_lds_v4s)(at_lds_t)(img + row * 128 + (((col >> 3) ^ at_sw(row)) << 4) + ((col & 7) << 1)));
+}
+
+// A operand read transposed (X^T of an image X): A[row c0 + (lane & 31)][k]
+// with element j of lane half hh = image row m0 + 8 (j >> 2) + 4 hh + (j & 3)
+// — the permuted k order of an accumulator tile used as the B operand.
+// ds_read_b64_tr_b16: lane t of a 16-lane group gives the address of row
+// (t >> 2), columns 4 (t & 3) .. +3 of a 4 x 16 block and receives column t.
+__device__ __forceinline__ bf16x8 at_trfrag(const char* img, int m0, int c0, int lane) {
+  const int t = lane & 15, hh = lane >> 5, rb = lane & 16;
+  const int row = m0 + 4 * hh + (t >> 2);
+  const int col = c0 + rb + 4 * (t & 3);
+  const at_v4s lo = at_tr(img, row, col);
+  const at_v4s hi = at_tr(img, row + 8, col);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__device__ __forceinline__ f32x16 at_mfma(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 at_zero() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+__device__ __forceinline__ bf16x8 at_ld16(const bf16* p, bool ok) {
+  if (!ok) {
+    bf16x8 z;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z[i] = (bf16)0.f;
+    return z;
+  }
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// accumulator row of register rho for lane half hh
+__device__ __forceinline__ int at_crow(int rho, int hh) { return (rho & 3) + 8 * (rho >> 2) + 4 * hh; }
+
+// rows of C^T (d = 32 dt + at_crow) of column `col` (lane) -> dst[d], 8-byte stores
+__device__ __forceinline__ void at_store_t(bf16* dst, const f32x16& c0, const f32x16& c1, float scale, int hh) {
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const f32x16& c = dt ? c1 : c0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      __attribute__((ext_vector_type(4))) bf16 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = (bf16)(c[4 * g + e] * scale);
+      *reinterpret_cast<decltype(v)*>(dst + 32 * dt + 8 * g + 4 * hh) = v;
+    }
+  }
+}
+
+template <bool MASK>
+__global__ void __launch_bounds__(512) attn_fwd_kernel(const bf16* __restrict__ qkv, int L, int N, int heads,
+                                                       const float* __restrict__ mask, bf16* __restrict__ out,
+                                                       float* __restrict__ lse) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * AT_IMG];
+  char* kimg = smem;
+  char* vimg = smem + AT_IMG;
+  const int nb = (L + 31) >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = (int)(blockIdx.x % heads), n = (int)(blockIdx.x / heads);
+  const int E = heads * 64;
+  const long long ld = 3LL * E, rs = (long long)N * ld;
+  const bf16* base = qkv + (long long)n * ld + h * 64;
+  at_stage2(base + E, rs, base + 2 * E, rs, L, kimg, vimg, tid, nb * 64);
+  const int r = lane & 31, hh = lane >> 5;
+  const int q = 32 * w + r;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = at_ld16(base + q * rs + 16 * s + 8 * hh, q < L);
+  __syncthreads();
+
+  f32x16 o0 = at_zero(), o1 = at_zero();
+  float m = -INFINITY, l = 0.f;
+  for (int kb = 0; kb < nb; ++kb) {
+    f32x16 st = at_zero();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) st = at_mfma(at_row(kimg, 32 * kb + r, s, hh), qf[s], st);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) {
+      const int key = 32 * kb + at_crow(rho, hh);
+      float v = st[rho] * 0.125f;
+      if (MASK && key < L && q < L) v += mask[(long long)q * L + key];
+      if (key >= L) v = -INFINITY;
+      st[rho] = v;
+      mx = fmaxf(mx, v);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float mu = mn == -INFINITY ? 0.f : mn;
+    const float alpha = __expf(m - mu);
+    float sum = 0.f;
+    bf16x8 pf0, pf1;
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) {
+      const float p = __expf(st[rho] - mu);
+      sum += p;
+      if (rho < 8) pf0[rho] = (bf16)p;
+      else pf1[rho - 8] = (bf16)p;
+    }
+    sum += __shfl_xor(sum, 32, 64);
+    l = l * alpha + sum;
+    m = mn;
+    o0 *= alpha;
+    o1 *= alpha;
+    o0 = at_mfma(at_trfrag(vimg, 32 * kb, 0, lane), pf0, o0);
+    o0 = at_mfma(at_trfrag(vimg, 32 * kb + 16, 0, lane), pf1, o0);
+    o1 = at_mfma(at_trfrag(vimg, 32 * kb, 32, lane), pf0, o1);
+    o1 = at_mfma(at_trfrag(vimg, 32 * kb + 16, 32, lane), pf1, o1);
+  }
+  if (q < L) {
+    at_store_t(out + ((long long)q * N + n) * E + h * 64, o0, o1, 1.f / l, hh);
+    if (lse && hh == 0) lse[((long long)q * N + n) * heads + h] = m + __logf(l);
+  }
+}
+
+template <bool MASK>
+__global__ void __launch_bounds__(512) attn_bwd_q_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
+                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                         int L, int N, int heads, const float* __restrict__ mask,
+                                                         bf16* __restrict__ dqkv, float* __restrict__ Dout) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * AT_IMG];
+  char* kimg = smem;
+  char* vimg = smem + AT_IMG;
+  const int nb = (L + 31) >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = (int)(blockIdx.x % heads), n = (int)(blockIdx.x / heads);
+  const int E = heads * 64;
+  const long long ld = 3LL * E, rs = (long long)N * ld, ors = (long long)N * E;
+  const bf16* base = qkv + (long long)n * ld + h * 64;
+  at_stage2(base + E, rs, base + 2 * E, rs, L, kimg, vimg, tid, nb * 64);
+  const int r = lane & 31, hh = lane >> 5;
+  const int q = 32 * w + r;
+  const bool qok = q < L;
+  const long long orow = (long long)q * ors + (long long)n * E + h * 64;
+  bf16x8 qf[4], gf[4];
+  float D = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = at_ld16(base + q * rs + 16 * s + 8 * hh, qok);
+    gf[s] = at_ld16(dout + orow + 16 * s + 8 * hh, qok);
+    const bf16x8 of = at_ld16(o + orow + 16 * s + 8 * hh, qok);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) D += (float)gf[s][j] * (float)of[j];
+  }
+  D += __shfl_xor(D, 32, 64);
+  const long long item = ((long long)q * N + n) * heads + h;
+  const float lq = qok ? lse[item] : 0.f;
+  __syncthreads();
+
+  f32x16 dq0 = at_zero(), dq1 = at_zero();
+  for (int kb = 0; kb < nb; ++kb) {
+    f32x16 st = at_zero(), dpt = at_zero();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      st = at_mfma(at_row(kimg, 32 * kb + r, s, hh), qf[s], st);
+      dpt = at_mfma(at_row(vimg, 32 * kb + r, s, hh), gf[s], dpt);
+    }
+    bf16x8 df0, df1;
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) {
+      const int key = 32 * kb + at_crow(rho, hh);
+      float v = st[rho] * 0.125f;
+      if (MASK && key < L && qok) v += mask[(long long)q * L + key];
+      const float p = (key < L && qok) ? __expf(v - lq) : 0.f;
+      const float ds = p * (dpt[rho] - D);
+      if (rho < 8) df0[rho] = (bf16)ds;
+      else df1[rho - 8] = (bf16)ds;
+    }
+    dq0 = at_mfma(at_trfrag(kimg, 32 * kb, 0, lane), df0, dq0);
+    dq0 = at_mfma(at_trfrag(kimg, 32 * kb + 16, 0, lane), df1, dq0);
+    dq1 = at_mfma(at_trfrag(kimg, 32 * kb, 32, lane), df0, dq1);
+    dq1 = at_mfma(at_trfrag(kimg, 32 * kb + 16, 32, lane), df1, dq1);
+  }
+  if (qok) {
+    at_store_t(dqkv + (long long)q * rs + (long long)n * ld + h * 64, dq0, dq1, 0.125f, hh);
+    if (hh == 0) Dout[item] = D;
+  }
+}
+
+template <bool MASK>
+__global__ void __launch_bounds__(512) attn_bwd_kv_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ dout,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ Din, int L, int N, int heads,
+                                                          const float* __restrict__ mask, bf16* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * AT_IMG];
+  __shared__ __attribute__((aligned(16))) float ls[AT_MAXB * 32], ds_[AT_MAXB * 32];
+  char* qimg = smem;
+  char* gimg = smem + AT_IMG;
+  const int nb = (L + 31) >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = (int)(blockIdx.x % heads), n = (int)(blockIdx.x / heads);
+  const int E = heads * 64;
+  const long long ld = 3LL * E, rs = (long long)N * ld, ors = (long long)N * E;
+  const bf16* base = qkv + (long long)n * ld + h * 64;
+  at_stage2(base, rs, dout + (long long)n * E + h * 64, ors, L, qimg, gimg, tid, nb * 64);
+  for (int i = tid; i < nb * 32; i += nb * 64) {
+    const long long it = ((long long)i * N + n) * heads + h;
+    ls[i] = i < L ? lse[it] : 0.f;
+    ds_[i] = i < L ? Din[it] : 0.f;
+  }
+  const int r = lane & 31, hh = lane >> 5;
+  const int key = 32 * w + r;
+  const bool kok = key < L;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = at_ld16(base + E + key * rs + 16 * s + 8 * hh, kok);
+    vf[s] = at_ld16(base + 2 * E + key * rs + 16 * s + 8 * hh, kok);
+  }
+  __syncthreads();
+
+  f32x16 dk0 = at_zero(), dk1 = at_zero(), dv0 = at_zero(), dv1 = at_zero();
+  for (int qb = 0; qb < nb; ++qb) {
+    f32x16 sc = at_zero(), dp = at_zero();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sc = at_mfma(at_row(qimg, 32 * qb + r, s, hh), kf[s], sc);
+      dp = at_mfma(at_row(gimg, 32 * qb + r, s, hh), vf[s], dp);
+    }
+    bf16x8 pf0, pf1, df0, df1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int q0 = 32 * qb + 8 * g + 4 * hh;
+      const float4 l4 = *reinterpret_cast<const float4*>(&ls[q0]);
+      const float4 d4 = *reinterpret_cast<const float4*>(&ds_[q0]);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rho = 4 * g + e, qi = q0 + e;
+        float v = sc[rho] * 0.125f;
+        if (MASK && qi < L && kok) v += mask[(long long)qi * L + key];
+        const float p = (qi < L && kok) ? __expf(v - lv[e]) : 0.f;
+        const float d = p * (dp[rho] - dv[e]);
+        if (rho < 8) { pf0[rho] = (bf16)p; df0[rho] = (bf16)d; }
+        else { pf1[rho - 8] = (bf16)p; df1[rho - 8] = (bf16)d; }
+      }
+    }
+    dv0 = at_mfma(at_trfrag(gimg, 32 * qb, 0, lane), pf0, dv0);
+    dv0 = at_mfma(at_trfrag(gimg, 32 * qb + 16, 0, lane), pf1, dv0);
+    dv1 = at_mfma(at_trfrag(gimg, 32 * qb, 32, lane), pf0, dv1);
+    dv1 = at_mfma(at_trfrag(gimg, 32 * qb + 16, 32, lane), pf1, dv1);
+    dk0 = at_mfma(at_trfrag(qimg, 32 * qb, 0, lane), df0, dk0);
+    dk0 = at_mfma(at_trfrag(qimg, 32 * qb + 16, 0, lane), df1, dk0);
+    dk1 = at_mfma(at_trfrag(qimg, 32 * qb, 32, lane), df0, dk1);
+    dk1 = at_mfma(at_trfrag(qimg, 32 * qb + 16, 32, lane), df1, dk1);
+  }
+  if (kok) {
+    bf16* dst = dqkv + (long long)key * rs + (long long)n * ld + h * 64;
+    at_store_t(dst + E, dk0, dk1, 0.125f, hh);
+    at_store_t(dst + 2 * E, dv0, dv1, 1.f, hh);
+  }
+}
+
+// launchers (vit.hip's entry points route bf16 here): false if not applicable
+bool attn_fwd_mfma(const bf16* qkv, int L, int N, int heads, const float* mask, bf16* out, float* lse,
+                   hipStream_t st) {
+  if (L < 1 || L > 32 * AT_MAXB || N < 1 || heads < 1) return false;
+  const long long grid = (long long)N * heads;
+  if (grid > 0x7fffffffLL) return false;
+  const int nthr = ((L + 31) / 32) * 64;
+  if (mask)
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, L, N, heads, mask, out, lse);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, L, N, heads, mask, out,
+                       lse);
+  return true;
+}
+
+bool attn_bwd_mfma(const bf16* qkv, const bf16* o, const bf16* dout, const float* lse, int L, int N, int heads,
+                   const float* mask, bf16* dqkv, float* dscratch, hipStream_t st) {
+  if (L < 1 || L > 32 * AT_MAXB || N < 1 || heads < 1) return false;
+  const long long grid = (long long)N * heads;
+  if (grid > 0x7fffffffLL) return false;
+  const int nthr = ((L + 31) / 32) * 64;
+  if (mask) {
+    hipLaunchKernelGGL(attn_bwd_q_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, o, dout, lse, L, N,
+                       heads, mask, dqkv, dscratch);
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, dout, lse, dscratch, L,
+                       N, heads, mask, dqkv);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_q_kernel<false>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, o, dout, lse, L, N,
+                       heads, mask, dqkv, dscratch);
+    hipLaunchKernelGGL(attn_bwd_kv_kernel<false>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, dout, lse, dscratch,
+                       L, N, heads, mask, dqkv);
+  }
+  return true;
+}
+
+}  // namespace artsbir

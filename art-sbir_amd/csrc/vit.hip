@@ -6,8 +6,9 @@
 //
 // Layouts follow nn.MultiheadAttention (batch_first=False): x [L][N][E]
 // row-major, qkv [L*N][3E] = x @ in_proj_weight^T + in_proj_bias (q | k | v
-// columns), out [L*N][E] before out_proj.  head_dim == 64 (one lane per head
-// dimension), L <= 256 (four keys per lane).
+// columns), out [L*N][E] before out_proj.  head_dim == 64, L <= 256.  The
+// bf16 attention core runs on MFMA (attn.hip); the f32 parity mode keeps the
+// per-row kernels below (one lane per head dimension, four keys per lane).
 #include "common.h"
 #include "../../include/artsbir.h"
 
@@ -355,6 +356,12 @@ __global__ void vit_tokens_bwd_kernel(const T* __restrict__ dtok, int B, int P, 
     }                                               \
   } while (0)
 
+// MFMA attention for the bf16 mode (attn.hip)
+bool attn_fwd_mfma(const bf16* qkv, int L, int N, int heads, const float* mask, bf16* out, float* lse,
+                   hipStream_t st);
+bool attn_bwd_mfma(const bf16* qkv, const bf16* o, const bf16* dout, const float* lse, int L, int N, int heads,
+                   const float* mask, bf16* dqkv, float* dscratch, hipStream_t st);
+
 static inline unsigned vit_grid(long long n) {
   long long g = (n + 255) / 256;
   return (unsigned)(g > (1 << 20) ? (1 << 20) : g < 1 ? 1 : g);
@@ -394,6 +401,14 @@ extern "C" int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int
                                    void* out, float* lse, void* stream) {
   if (L < 1 || L > 256) { set_error("mha_fwd: sequence length %d outside [1, 256]", L); return -1; }
   if (heads < 1 || N < 1) { set_error("mha_fwd: bad batch %d / heads %d", N, heads); return -1; }
+  if (dtype == ARTSBIR_DT_BF16) {  // MFMA path (attn.hip)
+    if (!attn_fwd_mfma((const bf16*)qkv, L, N, heads, mask, (bf16*)out, lse, (hipStream_t)stream)) {
+      set_error("mha_fwd: batch %d x heads %d too large", N, heads);
+      return -1;
+    }
+    ARTSBIR_CHECK_LAUNCH("mha_fwd");
+    return 0;
+  }
   const long long items = (long long)L * N * heads;
   const unsigned grid = (unsigned)((items + 3) / 4);
   VIT_DISPATCH(dtype, hipLaunchKernelGGL(mha_fwd_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
@@ -436,6 +451,15 @@ extern "C" int artsbir_mha_bwd(int dtype, const void* qkv, const void* out, cons
                                void* stream) {
   if (L < 1 || L > 256) { set_error("mha_bwd: sequence length %d outside [1, 256]", L); return -1; }
   if (heads < 1 || N < 1 || !lse || !dscratch) { set_error("mha_bwd: bad arguments"); return -1; }
+  if (dtype == ARTSBIR_DT_BF16) {  // MFMA path (attn.hip)
+    if (!attn_bwd_mfma((const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, L, N, heads, mask, (bf16*)dqkv,
+                       dscratch, (hipStream_t)stream)) {
+      set_error("mha_bwd: batch %d x heads %d too large", N, heads);
+      return -1;
+    }
+    ARTSBIR_CHECK_LAUNCH("mha_bwd");
+    return 0;
+  }
   const long long items = (long long)L * N * heads;
   const unsigned grid = (unsigned)((items + 3) / 4);
   VIT_DISPATCH(dtype, hipLaunchKernelGGL(mha_bwd_q_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
