@@ -605,29 +605,62 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ slots, int C, d
 }
 
 // ------------------------------------------------------------------ colsum
-// out[c] += sum_{r<rows} x[r*ld + c]   (x is T or f32; 8 columns per thread)
+// out[c] += sum_{r<rows} x[r*ld + c]   (x is T or f32): a 256-thread block owns
+// 512 columns (64 lanes x 8) of a strip of rows; its 4 waves take every 4th
+// row, 4 rows in flight per lane, then one LDS reduction and ONE atomic per
+// column per block (few blocks per column: the atomics on one address
+// serialise in the memory-side atomic unit)
 template <typename T>
-__global__ void colsum_kernel(const T* __restrict__ x, long long rows, long long ld, long long C, long long rows_per_block,
-                              float* __restrict__ out) {
-  const long long c0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 8;
-  if (c0 >= C) return;
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, long long rows, long long ld, long long C,
+                                                     long long rows_per_block, float* __restrict__ out) {
+  __shared__ float red[3][512];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long c0 = (long long)blockIdx.x * 512 + lane * 8;
+  const bool cok = c0 < C;
   long long r0 = blockIdx.y * rows_per_block, r1 = r0 + rows_per_block;
   if (r1 > rows) r1 = rows;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (long long r = r0; r < r1; ++r) {
-    float v[8];
-    load8<T>(x + r * ld + c0, v);
+  if (cok) {
+    long long r = r0 + w;
+    for (; r + 28 < r1; r += 32) {
+      float v[8][8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      for (int u = 0; u < 8; ++u) load8<T>(x + (r + 4 * u) * ld + c0, v[u]);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        acc[e] += ((v[0][e] + v[1][e]) + (v[2][e] + v[3][e])) + ((v[4][e] + v[5][e]) + (v[6][e] + v[7][e]));
+    }
+    for (; r < r1; r += 4) {
+      float v[8];
+      load8<T>(x + r * ld + c0, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
   }
+  if (w > 0) {
 #pragma unroll
-  for (int e = 0; e < 8; ++e) atomicAdd(out + c0 + e, acc[e]);
+    for (int e = 0; e < 8; ++e) red[w - 1][lane * 8 + e] = acc[e];
+  }
+  __syncthreads();
+  if (w == 0 && cok) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      atomicAdd(out + c0 + e, acc[e] + red[0][lane * 8 + e] + red[1][lane * 8 + e] + red[2][lane * 8 + e]);
+  }
 }
 
 // ------------------------------------------------------------ casts / packs
 template <typename TI, typename TO>
 __global__ void cast_kernel(const TI* __restrict__ x, TO* __restrict__ y, long long n) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+  // 8 elements per 16/32-B access when both pointers are 16-B aligned
+  const long long n8 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) ? 0 : n / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    load8<TI>(x + i * 8, v);
+    store8<TO>(y + i * 8, v);
+  }
+  for (long long i = n8 * 8 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
     y[i] = from_f<TO>(to_f(x[i]));
 }
 
@@ -927,9 +960,13 @@ extern "C" int artsbir_colsum(int dtype, const void* x, long long rows, long lon
                               void* stream) {
   if (C % 8 || ld % 8) { set_error("colsum: C and ld must be multiples of 8"); return -1; }
   if (rows <= 0) return 0;
-  const unsigned gx = (unsigned)((C / 8 + 255) / 256);
-  long long rpb = 64;
-  long long gy = (rows + rpb - 1) / rpb;
+  const unsigned gx = (unsigned)((C + 511) / 512);
+  // about 1024 blocks in all, at least 64 rows each
+  long long gy = 1024 / gx;
+  if (gy < 1) gy = 1;
+  long long rpb = (rows + gy - 1) / gy;
+  if (rpb < 64) rpb = 64;
+  gy = (rows + rpb - 1) / rpb;
   if (gy > 65535) { rpb = (rows + 65534) / 65535; gy = (rows + rpb - 1) / rpb; }
   DISPATCH_T(dtype, hipLaunchKernelGGL(colsum_kernel<T>, dim3(gx, (unsigned)gy), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)x, rows, ld, C, rpb, out));
@@ -940,13 +977,13 @@ extern "C" int artsbir_colsum(int dtype, const void* x, long long rows, long lon
 extern "C" int artsbir_cast(int src_dtype, const void* x, int dst_dtype, void* y, long long n, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (src_dtype == ARTSBIR_DT_F32 && dst_dtype == ARTSBIR_DT_BF16)
-    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid_for(n)), dim3(256), 0, st, (const float*)x, (bf16*)y, n);
+    hipLaunchKernelGGL((cast_kernel<float, bf16>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, st, (const float*)x, (bf16*)y, n);
   else if (src_dtype == ARTSBIR_DT_BF16 && dst_dtype == ARTSBIR_DT_F32)
-    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (float*)y, n);
+    hipLaunchKernelGGL((cast_kernel<bf16, float>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, st, (const bf16*)x, (float*)y, n);
   else if (src_dtype == ARTSBIR_DT_F32 && dst_dtype == ARTSBIR_DT_F32)
-    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for(n)), dim3(256), 0, st, (const float*)x, (float*)y, n);
+    hipLaunchKernelGGL((cast_kernel<float, float>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, st, (const float*)x, (float*)y, n);
   else if (src_dtype == ARTSBIR_DT_BF16 && dst_dtype == ARTSBIR_DT_BF16)
-    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid_for(n)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n);
+    hipLaunchKernelGGL((cast_kernel<bf16, bf16>), dim3(grid_for((n + 7) / 8)), dim3(256), 0, st, (const bf16*)x, (bf16*)y, n);
   else { set_error("cast: bad dtypes"); return -1; }
   ARTSBIR_CHECK_LAUNCH("cast");
   return 0;

@@ -14,6 +14,8 @@
 // chunks sit at slot chunk ^ (row & 7), so the fragment reads (16 rows x one
 // 32-B k-slice per lane group) spread over the banks.  MFMA operand map:
 // lane l supplies row / column l & 15, k = 32 (l >> 4) .. +31 (32 bytes).
+#include <cstdlib>
+
 #include "common.h"
 #include "../../include/artsbir.h"
 
@@ -41,11 +43,29 @@ __device__ __forceinline__ float fp8_wave_max(float v) {
     }                                               \
   } while (0)
 
+__device__ __forceinline__ void fp8_load8(const bf16* p, float (&v)[8]) {
+  const bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)r[i];
+}
+__device__ __forceinline__ void fp8_load8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) fp8_amax_kernel(const T* __restrict__ x, long long n,
                                                        unsigned* __restrict__ amax_bits) {
   float m = 0.f;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += gridDim.x * 256LL) m = fmaxf(m, fabsf(to_f(x[i])));
+  const long long n8 = (reinterpret_cast<uintptr_t>(x) & 15) ? 0 : n / 8;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += gridDim.x * 256LL) {
+    float v[8];
+    fp8_load8(x + i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(v[e]));
+  }
+  for (long long i = n8 * 8 + blockIdx.x * 256LL + threadIdx.x; i < n; i += gridDim.x * 256LL)
+    m = fmaxf(m, fabsf(to_f(x[i])));
   m = fp8_wave_max(m);
   __shared__ float red[4];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -86,14 +106,20 @@ __global__ void __launch_bounds__(256) fp8_quant_kernel(const T* __restrict__ x,
                                                         unsigned char* __restrict__ q) {
   const float amax = __uint_as_float(*amax_bits);
   const float sc = amax > 0.f ? amax / 448.f : 1.f;  // x / s, correctly rounded (as the documented formula)
-  for (long long i = (blockIdx.x * 256LL + threadIdx.x) * 4; i < n; i += gridDim.x * 256LL * 4) {
-    float v[4];
+  const long long n8 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(q)) & 15) ? 0 : n / 8;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += gridDim.x * 256LL) {
+    float v[8];
+    fp8_load8(x + i * 8, v);
+    unsigned lo = 0, hi = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = i + e < n ? to_f(x[i + e]) / sc : 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (i + e < n) q[i + e] = fp8_e4m3_rne(v[e]);
+    for (int e = 0; e < 4; ++e) {
+      lo |= (unsigned)fp8_e4m3_rne(v[e] / sc) << (8 * e);
+      hi |= (unsigned)fp8_e4m3_rne(v[4 + e] / sc) << (8 * e);
+    }
+    *reinterpret_cast<uint2*>(q + i * 8) = make_uint2(lo, hi);
   }
+  for (long long i = n8 * 8 + blockIdx.x * 256LL + threadIdx.x; i < n; i += gridDim.x * 256LL)
+    q[i] = fp8_e4m3_rne(to_f(x[i]) / sc);
 }
 
 __global__ void fp8_scale_kernel(unsigned* amax_bits) {  // amax -> the scale s, in place
@@ -189,6 +215,169 @@ __global__ void __launch_bounds__(256) gemm_fp8_kernel(int M, int N, int K, cons
     }
 }
 
+// ---------------------------------------------------------------------------
+// 256 x 256 output tile per 512-thread workgroup (8 waves as 2 x 4, each
+// 128 x 64 = 8 x 4 MFMA tiles), K-step 128, operands moved HBM/L2 -> LDS by
+// LDS-DMA (buffer_load ... lds, no VGPR staging) into a 2-stage ring; the
+// next stage is in flight while this one is consumed.  4x the arithmetic
+// intensity of the 128 x 128 kernel above (its operand traffic, not the MFMA,
+// bounds it).  Workgroups are numbered so that the N tiles of one A panel run
+// on one XCD (the panel is read from HBM once and then from that XCD's L2).
+typedef __attribute__((address_space(3))) void* f8_lds_t;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t f8_rsrc(const void* base, long long bytes) {
+  if (bytes > 0x7fffffffLL) bytes = 0x7fffffffLL;
+  if (bytes < 0) bytes = 0;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+// LDS-DMA of 16 B per lane to lds + 16 * lane (M0 saved and restored inside)
+__device__ __forceinline__ void f8_glds16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(f8_lds_t)lds);
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(base), "s"(r)
+      : "memory");
+}
+
+__device__ __forceinline__ i32x8 f8_frag(const char* img, int row, int kq) {
+  const uint4 lo = *reinterpret_cast<const uint4*>(img + fp8_slot(row, 2 * kq));
+  const uint4 hi = *reinterpret_cast<const uint4*>(img + fp8_slot(row, 2 * kq + 1));
+  return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+}
+
+template <typename T>
+__global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
+                                                          const unsigned char* __restrict__ B,
+                                                          const float* __restrict__ sa, const float* __restrict__ sb,
+                                                          const float* __restrict__ bias, T* __restrict__ C,
+                                                          int accumulate) {
+  __shared__ __attribute__((aligned(16))) char smem[2][2][256 * 128];  // [stage][A | B]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_n = (N + 255) / 256;
+  const long long G = gridDim.x;
+  long long lid = blockIdx.x;
+  if (G >= 8) {  // consecutive tiles (one A panel) on one XCD
+    const long long q = G / 8, r = G % 8, x = lid % 8;
+    lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
+  }
+  const int m0 = (int)(lid / tiles_n) * 256, n0 = (int)(lid % tiles_n) * 256;
+  const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
+  const int nk = K / 128;
+  const __amdgpu_buffer_rsrc_t ra = f8_rsrc(A + (long long)m0 * K, (long long)(M - m0) * K);
+  const __amdgpu_buffer_rsrc_t rb = f8_rsrc(B + (long long)n0 * K, (long long)(N - n0) * K);
+  // loader: wave w moves 1-KB pieces w, w + 8, w + 16, w + 24 of each operand
+  // (8 rows each); lane l fills slot l & 7 of row l >> 3 with the chunk that
+  // belongs there under the swizzle
+  const int lrow = lane >> 3, lslot = lane & 7;
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int piece = wid + 8 * u, row = piece * 8 + lrow;
+      const unsigned off = (unsigned)(row * K + kt * 128 + ((lslot ^ (row & 7)) << 4));
+      f8_glds16(ra, &smem[buf][0][piece * 1024], off);
+      f8_glds16(rb, &smem[buf][1][piece * 1024], off);
+    }
+  };
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, kq = lane >> 4;
+  issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's pieces of stage kt landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // and its reads of stage kt-1 retired
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const char* ai = smem[buf][0];
+    const char* bi = smem[buf][1];
+    i32x8 bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(bi, wn + 16 * j + fr, kq);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const i32x8 af = f8_frag(ai, wm + 16 * i + fr, kq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af, bfr[j], acc[i][j], 0, 0, 0, 0x7f7f7f7f, 0,
+                                                                     0x7f7f7f7f);
+    }
+  }
+  // epilogue through LDS (the ring is free): per wave four passes of a 32 x 64
+  // f32 block, then row-contiguous 16-B reads and coalesced row stores
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  constexpr int EP = 68;  // f32 row pitch of a wave's block
+  float* eb = reinterpret_cast<float*>(&smem[0][0][0]) + wid * 32 * EP;
+  const float s = sa[0] * sb[0];
+  const int ec = (lane & 15) * 4, er = lane >> 4;  // this lane's 4 columns, row phase
+  float bn[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int n = n0 + wn + ec + e;
+    bn[e] = (bias && n < N) ? bias[n] : 0.f;
+  }
+#pragma unroll
+  for (int pass = 0; pass < 4; ++pass) {
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) eb[(16 * ii + 4 * kq + r) * EP + 16 * j + fr] = acc[2 * pass + ii][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+    for (int rr = 0; rr < 8; ++rr) {
+      const int lr = 4 * rr + er;
+      const int m = m0 + wm + 32 * pass + lr;
+      const int n = n0 + wn + ec;
+      const float4 v4 = *reinterpret_cast<const float4*>(eb + lr * EP + ec);
+      float v[4] = {v4.x * s + bn[0], v4.y * s + bn[1], v4.z * s + bn[2], v4.w * s + bn[3]};
+      if (m < M) {
+        T* p = C + (long long)m * N + n;
+        if (n + 3 < N && (N & 3) == 0) {
+          if (accumulate) {
+            if constexpr (sizeof(T) == 4) {
+              const float4 o = *reinterpret_cast<const float4*>(p);
+              v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += to_f(p[e]);
+            }
+          }
+          if constexpr (sizeof(T) == 4) {
+            *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+            __attribute__((ext_vector_type(4))) bf16 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+            *reinterpret_cast<decltype(o)*>(p) = o;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < N) p[e] = from_f<T>(accumulate ? v[e] + to_f(p[e]) : v[e]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 }  // namespace artsbir
 
 using namespace artsbir;
@@ -198,7 +387,7 @@ extern "C" int artsbir_quantize_fp8(int dtype, const void* x, long long n, unsig
   if (n <= 0 || !x || !q || !scale) { set_error("quantize_fp8: bad arguments"); return -1; }
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(scale, 0, sizeof(float), st) != hipSuccess) { set_error("quantize_fp8: memset"); return -2; }
-  long long g = (n + 1023) / 1024;
+  long long g = (n + 2047) / 2048;
   const unsigned grid = (unsigned)(g > 2048 ? 2048 : g < 1 ? 1 : g);
   unsigned* bits = reinterpret_cast<unsigned*>(scale);
   FP8_DISPATCH(dtype, hipLaunchKernelGGL(fp8_amax_kernel<T>, dim3(grid), dim3(256), 0, st, (const T*)x, n, bits));
@@ -217,8 +406,19 @@ extern "C" int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, 
   const long long tiles = (long long)((M + 127) / 128) * ((N + 127) / 128);
   if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8: too many tiles"); return -1; }
   hipStream_t st = (hipStream_t)stream;
-  FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K, a,
-                                           b, sa, sb, bias, (T*)c, accumulate));
+  const char* old = getenv("ARTSBIR_FP8_V1");
+  if (M >= 256 && N >= 256 && !(old && atoi(old))) {  // 256 x 256 LDS-DMA kernel
+    const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    if ((long long)M * K > 0x7fffffffLL || (long long)N * K > 0x7fffffffLL) {
+      set_error("gemm_nt_fp8: operand larger than 2 GiB");
+      return -1;
+    }
+    FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_v2_kernel<T>, dim3((unsigned)t2), dim3(512), 0, st, M, N, K,
+                                             a, b, sa, sb, bias, (T*)c, accumulate));
+  } else {
+    FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K,
+                                             a, b, sa, sb, bias, (T*)c, accumulate));
+  }
   ARTSBIR_CHECK_LAUNCH("gemm_nt_fp8");
   return 0;
 }

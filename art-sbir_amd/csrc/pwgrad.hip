@@ -8,10 +8,9 @@
 // of k (implicit im2col with per-row padding masks) — and the MFMA fragments,
 // which need 8 consecutive m per lane, are read with the gfx950 transposing
 // LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): no register
-// transposes.  LDS image: every operand tile is viewed as rows of 128
-// bf16 (256 B) with 16-B chunk ch of pseudo-row pr stored at slot
-// ch ^ (((pr & 3) << 2) | ((pr >> 2) & 3)) (guide T10 image (b)); the XOR is
-// applied to the per-lane LDS-DMA source address.  An NSTAGE ring with counted
+// transposes.  LDS image: row-major tile rows with the 16-B chunks of row m
+// XOR-swizzled by pw_f<width>(m) (conflict-free transposed reads at every tile
+// width; guide T10); the XOR is applied to the per-lane LDS-DMA source address.  An NSTAGE ring with counted
 // vmcnt keeps NSTAGE-2 stages in flight across the per-K-step barrier; the
 // reduction over m is split over workgroups (f32 atomics into dW).
 #include <cstdlib>
@@ -63,14 +62,32 @@ __device__ __forceinline__ void pw_wait_stages(int ahead) {
   pw_vm_wait<0>();
 }
 
-__device__ __forceinline__ int pw_swz(int pr) { return ((pr & 3) << 2) | ((pr >> 2) & 3); }
+// XOR swizzle of the 16-B chunks of tile row m (TW elements wide).  A
+// transposing read takes, per 32-lane half, 2 adjacent chunks of rows
+// {m0..m0+3, m0+8..m0+11} (m0 = 0 or 4 mod 16); the swizzle spreads those 16
+// chunks over the 16 bank groups of a 256-B LDS row: conflict-free for every
+// tile width (rows of 256 B and more: chunk ^ f; 128-B rows fill half a bank
+// row each, 64-B rows a quarter)
+template <int TW>
+__device__ __forceinline__ int pw_f(int m) {
+  if constexpr (TW >= 128) return ((m & 3) << 2) | ((m >> 2) & 3);
+  else if constexpr (TW == 64) return (((m >> 1) & 1) << 1) | (((m >> 3) & 1) << 2);
+  else return ((m >> 3) & 1) << 1;
+}
 
 // byte offset in a tile image of element (m, c) of a tile TW elements wide
 template <int TW>
 __device__ __forceinline__ int pw_off(int m, int c) {
-  const int f = m * TW + c;
-  const int pr = f >> 7, pc = f & 127;
-  return pr * 256 + (((pc >> 3) ^ pw_swz(pr)) << 4) + ((pc & 7) << 1);
+  return (m * TW + (((c >> 3) ^ pw_f<TW>(m)) << 3) + (c & 7)) * 2;
+}
+
+// the tile element (m, first column) whose 16-B chunk LDS-DMA slot (pr, slot)
+// of the image holds (the inverse of pw_off: XOR is an involution)
+template <int TW>
+__device__ __forceinline__ int pw_src(int pr, int slot) {
+  const int f0 = pr * 128 + slot * 8;
+  const int m = f0 / TW, ch = (f0 % TW) >> 3;
+  return m * TW + ((ch ^ pw_f<TW>(m)) << 3);
 }
 
 // 4 consecutive-m x 16-column block for the transposing read: lane t = 4q + p
@@ -135,7 +152,7 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
     const int g = u * NW + wid;
     a_on[u] = g < IA;
     const int pr = g * 4 + lpr;
-    const int f = pr * 128 + ((lslot ^ pw_swz(pr)) << 3);
+    const int f = pw_src<BCO>(pr, lslot);
     a_m[u] = f / BCO;
     const int co = co0 + f % BCO;
     a_col[u] = co < a.Cout ? (unsigned)(co * 2) : PW_OOB;
@@ -148,7 +165,7 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
   for (int u = 0; u < LB; ++u) {
     const int g = u * NW + wid;
     const int pr = g * 4 + lpr;
-    const int f = pr * 128 + ((lslot ^ pw_swz(pr)) << 3);
+    const int f = pw_src<BKK>(pr, lslot);
     b_m[u] = f / BKK;
     const int k = k0 + f % BKK;
     if (k >= a.K) {
@@ -218,6 +235,29 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int mb = kk * 32 + 8 * g;
+      if constexpr (MT * NT >= 32) {
+        // big wave tiles: the B fragments stay, one A fragment at a time, and
+        // the LDS addresses are recomputed per k-step (an opaque lane index
+        // keeps the compiler from hoisting 64 address registers out of the loop)
+        int tt = t;
+        asm volatile("" : "+v"(tt));
+        bf16x8 bv[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          const pw_v4s lo = pw_tr<BKK>(bs, mb, wkk * WTK + 16 * j, tt);
+          const pw_v4s hi = pw_tr<BKK>(bs, mb + 4, wkk * WTK + 16 * j, tt);
+          bv[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const pw_v4s lo = pw_tr<BCO>(as, mb, wco * WTCO + 16 * i, tt);
+          const pw_v4s hi = pw_tr<BCO>(as, mb + 4, wco * WTCO + 16 * i, tt);
+          const bf16x8 af = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bv[j], acc[i][j], 0, 0, 0);
+        }
+        continue;
+      }
       bf16x8 af[MT], bv[NT];
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
@@ -503,8 +543,10 @@ static const PwCfg kPw[] = {
     {64, 128, 256},   // 4: 4 waves 64x32, 4 stages
     {32, 128, 256},   // 5: 4 waves 32x32, 4 stages
     {64, 512, 512},   // 6: 8 waves 64x64, 2 stages
+    {256, 256, 512},  // 7: 8 waves 128x64, 2 stages (half the LDS-DMA issues per MFMA of 0-2)
+    {256, 256, 512},  // 8: 8 waves 64x128, 2 stages
 };
-constexpr int kNumPw = 7;
+constexpr int kNumPw = 9;
 
 template <bool DENSE>
 static void pw_launch_c(int c, const PwArgs& a, long long blocks, hipStream_t st) {
@@ -516,7 +558,9 @@ static void pw_launch_c(int c, const PwArgs& a, long long blocks, hipStream_t st
     case 3: hipLaunchKernelGGL((pwgrad_kernel<64, 256, 1, 8, 3, DENSE>), g, dim3(512), 0, st, a); break;
     case 4: hipLaunchKernelGGL((pwgrad_kernel<64, 128, 1, 4, 4, DENSE>), g, dim3(256), 0, st, a); break;
     case 5: hipLaunchKernelGGL((pwgrad_kernel<32, 128, 1, 4, 4, DENSE>), g, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((pwgrad_kernel<64, 512, 1, 8, 2, DENSE>), g, dim3(512), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((pwgrad_kernel<64, 512, 1, 8, 2, DENSE>), g, dim3(512), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((pwgrad_kernel<256, 256, 2, 4, 2, DENSE>), g, dim3(512), 0, st, a); break;
+    default: hipLaunchKernelGGL((pwgrad_kernel<256, 256, 4, 2, 2, DENSE>), g, dim3(512), 0, st, a); break;
   }
 }
 
@@ -569,7 +613,8 @@ bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
   if (blocks > 0x7fffffffLL) return false;
   static const char* names[] = {"pwgrad_kernel<128,128>", "pwgrad_kernel<128,256>", "pwgrad_kernel<256,128>",
                                 "pwgrad_kernel<64,256>",  "pwgrad_kernel<64,128>",  "pwgrad_kernel<32,128>",
-                                "pwgrad_kernel<64,512>"};
+                                "pwgrad_kernel<64,512>",  "pwgrad_kernel<256,256,w2x4>",
+                                "pwgrad_kernel<256,256,w4x2>"};
   set_last_kernel(names[c]);
   if (a.dense) pw_launch_c<true>(c, a, blocks, st);
   else pw_launch_c<false>(c, a, blocks, st);

@@ -20,6 +20,183 @@ __device__ __forceinline__ float vit_wave_max(float v) {
   return v;
 }
 
+// 8 consecutive elements <-> f32 (16-B accesses for bf16, 2 x 16 B for f32)
+__device__ __forceinline__ void vt_load8(const bf16* p, float (&v)[8]) {
+  const bf16x8 r = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)r[i];
+}
+__device__ __forceinline__ void vt_load8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void vt_store8(bf16* p, const float (&v)[8]) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (bf16)v[i];
+  *reinterpret_cast<bf16x8*>(p) = r;
+}
+__device__ __forceinline__ void vt_store8(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// LayerNorm forward with 8-column chunks per lane (C % 8 == 0; chunk lane + 64 u)
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) layernorm_v_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, long long rows, int C,
+                                                          float eps, T* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nch = C >> 3;
+  const T* xr = x + row * C;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int ch = lane + 64 * u;
+    if (ch < nch) vt_load8(xr + ch * 8, v[u]);
+    else
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[u][e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[u][e];
+  }
+  const float mean = warp_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u)
+    if (lane + 64 * u < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (v[u][e] - mean) * (v[u][e] - mean);
+  const float istd = rsqrtf(warp_sum(q) / (float)C + eps);
+  T* yr = y + row * C;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int ch = lane + 64 * u;
+    if (ch < nch) {
+      float g[8], b[8], o[8];
+      vt_load8(gamma + ch * 8, g);
+      vt_load8(beta + ch * 8, b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[u][e] - mean) * istd * g[e] + b[e];
+      vt_store8(yr + ch * 8, o);
+    }
+  }
+}
+
+// LayerNorm backward with 8-column chunks per lane; each block's 4 waves reduce
+// their dgamma / dbeta partials in LDS and add them with one atomic per column
+template <typename T, int NCH>
+__device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __restrict__ dy, const T* dres, T* dx,
+                                           long long row, int C, float eps, int lane, const float (&gm)[NCH][8],
+                                           float (&pg)[NCH][8], float (&pb)[NCH][8]) {
+  const int nch = C >> 3;
+  const T* xr = x + row * C;
+  const T* gr = dy + row * C;
+  float xv[NCH][8], gv[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int ch = lane + 64 * u;
+    if (ch < nch) {
+      vt_load8(xr + ch * 8, xv[u]);
+      vt_load8(gr + ch * 8, gv[u]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { xv[u][e] = 0.f; gv[u][e] = 0.f; }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += xv[u][e];
+  }
+  const float mean = warp_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u)
+    if (lane + 64 * u < nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q += (xv[u][e] - mean) * (xv[u][e] - mean);
+  const float istd = rsqrtf(warp_sum(q) / (float)C + eps);
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh = (xv[u][e] - mean) * istd;  // past C: gv = 0, so no contribution
+      const float g = gv[u][e] * gm[u][e];
+      a += g;
+      b += g * xh;
+      pg[u][e] += gv[u][e] * xh;
+      pb[u][e] += gv[u][e];
+      xv[u][e] = xh;
+      gv[u][e] = g;
+    }
+  a = warp_sum(a) / (float)C;
+  b = warp_sum(b) / (float)C;
+  T* o = dx + row * C;
+  const T* rr = dres ? dres + row * C : nullptr;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int ch = lane + 64 * u;
+    if (ch < nch) {
+      float res[8], out[8];
+      if (rr) vt_load8(rr + ch * 8, res);
+      else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) res[e] = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[e];
+      vt_store8(o + ch * 8, out);
+    }
+  }
+}
+
+// LayerNorm backward with 8-column chunks per lane; each block's 4 waves reduce
+// their dgamma / dbeta partials in LDS and add them with one atomic per column
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256) layernorm_bwd_v_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
+                                                              const T* __restrict__ dy, long long rows, int C, float eps,
+                                                              const T* dres, T* dx, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  __shared__ float red[2][3][64 * NCH * 8];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = C >> 3;
+  float pg[NCH][8], pb[NCH][8], gm[NCH][8];
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int ch = lane + 64 * u;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { pg[u][e] = 0.f; pb[u][e] = 0.f; gm[u][e] = 0.f; }
+    if (ch < nch) vt_load8(gamma + ch * 8, gm[u]);
+  }
+  for (long long row = blockIdx.x * 4LL + w; row < rows; row += gridDim.x * 4LL)
+    ln_bwd_row<T, NCH>(x, dy, dres, dx, row, C, eps, lane, gm, pg, pb);
+  if (w > 0) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[0][w - 1][(u * 64 + lane) * 8 + e] = pg[u][e];
+        red[1][w - 1][(u * 64 + lane) * 8 + e] = pb[u][e];
+      }
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) {
+      const int ch = lane + 64 * u;
+      if (ch < nch)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int i = (u * 64 + lane) * 8 + e;
+          atomicAdd(dgamma + ch * 8 + e, pg[u][e] + red[0][0][i] + red[0][1][i] + red[0][2][i]);
+          atomicAdd(dbeta + ch * 8 + e, pb[u][e] + red[1][0][i] + red[1][1][i] + red[1][2][i]);
+        }
+    }
+  }
+}
+
 // y = (x - mean) / sqrt(var + eps) * gamma + beta per row, in fp32 whatever
 // the storage dtype (models.py:382-388); one wave per row
 template <typename T>
@@ -46,7 +223,16 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const T* __restrict__ x,
 // QuickGELU (models.py:391-393): x * sigmoid(1.702 x)
 template <typename T>
 __global__ void quickgelu_kernel(const T* __restrict__ x, long long n, T* __restrict__ y) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+  const long long n8 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) ? 0 : n / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float v[8];
+    vt_load8(x + i * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-1.702f * v[e]));
+    vt_store8(y + i * 8, v);
+  }
+  for (long long i = n8 * 8 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
     const float v = to_f(x[i]);
     y[i] = from_f<T>(v / (1.f + __expf(-1.702f * v)));
   }
@@ -181,7 +367,23 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(const T* __restrict_
 template <typename T>
 __global__ void quickgelu_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy, long long n,
                                      T* __restrict__ dx) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+  const long long n8 =
+      ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(dx)) & 15)
+          ? 0
+          : n / 8;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    float v[8], g[8];
+    vt_load8(x + i * 8, v);
+    vt_load8(dy + i * 8, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sg = 1.f / (1.f + __expf(-1.702f * v[e]));
+      v[e] = g[e] * (sg + 1.702f * v[e] * sg * (1.f - sg));
+    }
+    vt_store8(dx + i * 8, v);
+  }
+  for (long long i = n8 * 8 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
     const float v = to_f(x[i]);
     const float sg = 1.f / (1.f + __expf(-1.702f * v));
     dx[i] = from_f<T>(to_f(dy[i]) * (sg + 1.702f * v * sg * (1.f - sg)));
@@ -375,15 +577,24 @@ extern "C" int artsbir_layernorm_fwd(int dtype, const void* x, const float* gamm
                                      int C, float eps, void* y, void* stream) {
   if (rows <= 0) return 0;
   const unsigned grid = (unsigned)((rows + 3) / 4);
-  VIT_DISPATCH(dtype, hipLaunchKernelGGL(layernorm_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)x, gamma, beta, rows, C, eps, (T*)y));
+  const bool vec = C % 8 == 0 && C <= 1024 && !((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
+                                                  reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) & 15);
+  if (vec && C <= 512)
+    VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_v_kernel<T, 1>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y));
+  else if (vec)
+    VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_v_kernel<T, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y));
+  else
+    VIT_DISPATCH(dtype, hipLaunchKernelGGL(layernorm_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y));
   ARTSBIR_CHECK_LAUNCH("layernorm_fwd");
   return 0;
 }
 
 extern "C" int artsbir_quickgelu(int dtype, const void* x, long long n, void* y, void* stream) {
   if (n <= 0) return 0;
-  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_kernel<T>, dim3(vit_grid(n)), dim3(256), 0, (hipStream_t)stream,
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_kernel<T>, dim3(vit_grid((n + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)x, n, (T*)y));
   ARTSBIR_CHECK_LAUNCH("quickgelu");
   return 0;
@@ -422,6 +633,21 @@ extern "C" int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamm
                                      void* stream) {
   if (rows <= 0) return 0;
   if (C < 1 || C > 1024) { set_error("layernorm_bwd: C=%d outside [1, 1024]", C); return -1; }
+  const bool vec = C % 8 == 0 && !((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
+                                    reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dres) |
+                                    reinterpret_cast<uintptr_t>(gamma)) & 15);
+  if (vec) {  // 8-column chunks per lane; 512 blocks: few atomics per column
+    long long gv = (rows + 3) / 4;
+    const unsigned gridv = (unsigned)(gv > 512 ? 512 : gv);
+#define LNBV(N) VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_bwd_v_kernel<T, N>), dim3(gridv), dim3(256), 0,   \
+                                                      (hipStream_t)stream, (const T*)x, gamma, (const T*)dy, rows, C, \
+                                                      eps, (const T*)dres, (T*)dx, dgamma, dbeta))
+    if (C <= 512) LNBV(1);
+    else LNBV(2);
+#undef LNBV
+    ARTSBIR_CHECK_LAUNCH("layernorm_bwd");
+    return 0;
+  }
   long long g = (rows + 3) / 4;
   const unsigned grid = (unsigned)(g > 2048 ? 2048 : g);
   const int cpl = (C + 63) / 64;
@@ -440,7 +666,7 @@ extern "C" int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamm
 
 extern "C" int artsbir_quickgelu_bwd(int dtype, const void* x, const void* dy, long long n, void* dx, void* stream) {
   if (n <= 0) return 0;
-  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_bwd_kernel<T>, dim3(vit_grid(n)), dim3(256), 0,
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_bwd_kernel<T>, dim3(vit_grid((n + 7) / 8)), dim3(256), 0,
                                        (hipStream_t)stream, (const T*)x, (const T*)dy, n, (T*)dx));
   ARTSBIR_CHECK_LAUNCH("quickgelu_bwd");
   return 0;

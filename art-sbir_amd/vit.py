@@ -249,9 +249,14 @@ class _BlockFunction(torch.autograd.Function):
         T = x2.dtype
         dev = x2.device
         (w_in, b_in, w_o, b_o, g1, be1, w_fc, b_fc, w_pr, b_pr, g2, be2) = _block_params(blk)
-        z = lambda p: torch.zeros(p.shape, dtype=torch.float32, device=dev)  # noqa: E731
-        dw_in, db_in, dw_o, db_o, dg1, dbe1 = z(w_in), z(b_in), z(w_o), z(b_o), z(g1), z(be1)
-        dw_fc, db_fc, dw_pr, db_pr, dg2, dbe2 = z(w_fc), z(b_fc), z(w_pr), z(b_pr), z(g2), z(be2)
+        # the twelve parameter gradients as views of one zero-filled buffer (one fill)
+        ps = (w_in, b_in, w_o, b_o, g1, be1, w_fc, b_fc, w_pr, b_pr, g2, be2)
+        flat = torch.zeros(sum(p.numel() for p in ps), dtype=torch.float32, device=dev)
+        views, o = [], 0
+        for p in ps:
+            views.append(flat[o:o + p.numel()].view(p.shape))
+            o += p.numel()
+        dw_in, db_in, dw_o, db_o, dg1, dbe1, dw_fc, db_fc, dw_pr, db_pr, dg2, dbe2 = views
         dy2 = dy.contiguous().view(M, E).to(T)
         # mlp: y = x1 + c_proj(gelu(c_fc(ln_2(x1))))
         _wgrad(dy2, a, dw_pr)

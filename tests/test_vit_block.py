@@ -123,7 +123,8 @@ def test_fp8_gemm_matches_dequantized_reference(dev):
     import _hip
     import vit
     g = torch.Generator(device=dev).manual_seed(3)
-    for M, N, K in [(200, 136, 256), (130, 2304, 768), (1, 1, 128)]:
+    # (600, 520, 384), (256, 768, 3072): the 256 x 256 LDS-DMA kernel with ragged tiles and a long K
+    for M, N, K in [(200, 136, 256), (130, 2304, 768), (1, 1, 128), (600, 520, 384), (256, 768, 3072)]:
         a = torch.randn(M, K, device=dev, generator=g)
         b = torch.randn(N, K, device=dev, generator=g) * 0.05
         bias = torch.randn(N, device=dev, generator=g)
@@ -147,7 +148,14 @@ def test_fp8_gemm_matches_dequantized_reference(dev):
         db = qb.view(torch.float8_e4m3fn).double().cpu() * sb.double().cpu()
         ref = da @ db.T + bias.double().cpu()
         err = (out.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
-        assert err < 5e-5, (M, N, K, err)  # f32 accumulation of up to 768 products
+        assert err < 5e-5, (M, N, K, err)  # f32 accumulation of up to 3072 products
+        # accumulate = 1 onto an f32 output (the residual stream)
+        init = torch.randn(M, N, device=dev, generator=g)
+        out2 = init.clone()
+        _hip.call("artsbir_gemm_nt_fp8", M, N, K, qa.data_ptr(), qb.data_ptr(), sa.data_ptr(), sb.data_ptr(),
+                  bias.data_ptr(), out2.data_ptr(), _hip.DT_F32, 1, _hip.stream())
+        err2 = (out2.double().cpu() - init.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+        assert err2 < 5e-5, (M, N, K, err2)
 
 
 def _vit_pair(seed, res=64, patch=16, width=128, layers=2, heads=2, out=64):
