@@ -1083,6 +1083,8 @@ static PwArgs to_pw(const WgradArgs& a) {
   p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
   p.Ho = a.Ho; p.Wo = a.Wo; p.dense = a.dense; p.ldx = a.ldx;
   p.Cout = a.Cout; p.K = a.K; p.M = a.M; p.m_per_split = 0; p.dw = a.dw;
+  static const int dbg = getenv("ARTSBIR_PW_DBG") ? atoi(getenv("ARTSBIR_PW_DBG")) : 0;
+  p.dbg = dbg;
   return p;
 }
 

@@ -55,6 +55,7 @@ struct PwArgs {
   long long M;
   long long m_per_split;  // set by the launcher
   float* dw;              // f32 [Cout][K], accumulated
+  int dbg;                // profiling (ARTSBIR_PW_DBG): bit 0 skips the dW atomics
 };
 // candidate c (0 .. pwgrad_num_cfgs()-1) of the pipelined wgrad kernel;
 // false, launching nothing, if it does not apply to the shape

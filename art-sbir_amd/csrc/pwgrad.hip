@@ -295,6 +295,15 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
     compute(kt % NSTAGE);
   }
 
+  if (a.dbg & 1) {  // profiling: everything but the dW atomics (the sum keeps the MFMAs alive)
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (sum == 1.2345e-30f) atomicAdd(a.dw, sum);
+    return;
+  }
   // acc[i][j][r]: co = co0 + wco*WTCO + 16 i + 4 g + r, k = k0 + wkk*WTK + 16 j + t
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -565,10 +574,14 @@ static void pw_launch_c(int c, const PwArgs& a, long long blocks, hipStream_t st
 }
 
 // split-K levels: (target workgroups, minimum K-steps per workgroup).  Fewer,
-// longer splits trade CU fill for fewer f32 atomics into dW (large outputs).
-static const int kSplitTarget[] = {1536, 512, 256};
-static const int kSplitMinSteps[] = {8, 24, 64};
-constexpr int kNumLevels = 3;
+// longer splits trade CU fill for fewer f32 atomics into dW (the device-scope
+// atomics of the split flushes run memory-side and cost ~30 % of a dense
+// wgrad at 1536 workgroups).  The split count rounds DOWN to the target, so a
+// 256 / 512 target fills whole rounds of the 256 CUs (one workgroup per CU)
+// instead of leaving a tail round of a few workgroups.
+static const int kSplitTarget[] = {1536, 768, 512, 256};
+static const int kSplitMinSteps[] = {8, 16, 24, 64};
+constexpr int kNumLevels = 4;
 
 // candidates: kNumPw tile configurations x kNumLevels split levels, then the
 // halo-tiled small-channel kernel
@@ -588,7 +601,7 @@ bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
   if (g.bkk > 128 && a.K <= g.bkk / 2) return false;
   const long long ntiles = (long long)((a.Cout + g.bco - 1) / g.bco) * ((a.K + g.bkk - 1) / g.bkk);
   const long long ksteps = (a.M + 63) / 64;
-  long long splits = (kSplitTarget[level] + ntiles - 1) / ntiles;
+  long long splits = kSplitTarget[level] >= ntiles ? kSplitTarget[level] / ntiles : 1;
   const long long max_splits = (ksteps + kSplitMinSteps[level] - 1) / kSplitMinSteps[level];
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
