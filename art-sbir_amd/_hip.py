@@ -92,6 +92,8 @@ SIGNATURES = {
     "artsbir_gemm_tn": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _c_ll, _vp, _vp],
     "artsbir_conv2d_dgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp],
     "artsbir_conv2d_fwd_seg": [_P, _vp, _vp, _vp, _c_int, _vp, _vp],
+    "artsbir_conv2d_fwd_act": [_P, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
+    "artsbir_bn_fold": [_vp, _c_int, _c_ll, _vp, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp],
     "artsbir_conv2d_dgrad_bnb": [_P, _vp, _vp, _vp, _vp, _c_int, _PB, _c_int, _c_ll, _vp],
     "artsbir_pack_input": [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_pack_weight": [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_ll, _vp, _vp],

@@ -956,6 +956,32 @@ extern "C" int artsbir_bn_bwd_finalize(const float* slots, int C, double count, 
   return 0;
 }
 
+// BatchNorm2d in eval mode folded into the preceding convolution:
+// scale = gamma / sqrt(var + eps); w_out[co][k] = w[co][k] * scale, bias_out[co]
+// = beta - mean * scale (models.py:198-236 at inference: conv -> bn -> relu)
+__global__ void bn_fold_kernel(const float* __restrict__ w, int Co, long long K, const float* __restrict__ gamma,
+                               const float* __restrict__ beta, const float* __restrict__ mean,
+                               const float* __restrict__ var, float eps, float* __restrict__ w_out,
+                               float* __restrict__ bias_out) {
+  const long long n = (long long)Co * K;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / K);
+    const float sc = gamma[co] / sqrtf(var[co] + eps);
+    w_out[i] = w[i] * sc;
+    if (i - (long long)co * K == 0) bias_out[co] = beta[co] - mean[co] * sc;
+  }
+}
+
+extern "C" int artsbir_bn_fold(const float* w, int Co, long long K, const float* gamma, const float* beta,
+                               const float* mean, const float* var, float eps, float* w_out, float* bias_out,
+                               void* stream) {
+  if (Co <= 0 || K <= 0) { set_error("bn_fold: bad shape"); return -1; }
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(grid_for((long long)Co * K)), dim3(256), 0, (hipStream_t)stream, w, Co, K,
+                     gamma, beta, mean, var, eps, w_out, bias_out);
+  ARTSBIR_CHECK_LAUNCH("bn_fold");
+  return 0;
+}
+
 extern "C" int artsbir_colsum(int dtype, const void* x, long long rows, long long ld, long long C, float* out,
                               void* stream) {
   if (C % 8 || ld % 8) { set_error("colsum: C and ld must be multiples of 8"); return -1; }

@@ -128,6 +128,7 @@ struct ConvArgs {
   float* stats;     // [NSLOT][2][Cout] (x nseg)
   const void* res;  // epilogue residual (T): mode 1 same index, mode 2 2x2 average-unpool
   int res_mode;
+  int relu;         // ReLU on the stored output (after bias and residual)
   // host-side only (the launcher splits / fuses; kernels ignore them)
   int nseg;                 // BN segments (separate reference forward calls) of equal size
   const void* bnb_desc;     // artsbir_bn_bwd_desc of a fused BN-backward reduction (dgrad)
@@ -364,6 +365,10 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(ConvArgs a) {
       const T* rp = reinterpret_cast<const T*>(a.res) + ri * a.ldy + gn;
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] += e < nv ? scale * to_f(rp[e]) : 0.f;
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     }
     if (a.out_f32) {
       float* yp = reinterpret_cast<float*>(a.y) + gm * a.ldy + gn;
@@ -831,12 +836,13 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     return -1;
   }
   const artsbir_bn_bwd_desc* bd = reinterpret_cast<const artsbir_bn_bwd_desc*>(a.bnb_desc);
-  if (sizeof(T) == 2 && !a.out_f32 && !a.accumulate && !a.bias && !a.in_scale) {
+  if (sizeof(T) == 2 && !a.out_f32 && !a.accumulate && !a.in_scale && !((a.bias || a.relu) && a.stats)) {
     PgArgs p{};
     p.x = a.x; p.x_elems = a.x_elems; p.sN = a.sN; p.sH = a.sH; p.sW = a.sW;
     p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
     p.Ho = a.Ho; p.Wo = a.Wo; p.w = a.w; p.Cout = a.Cout; p.K = a.K; p.M = a.M;
     p.y = a.y; p.ldy = a.ldy; p.stats = a.stats; p.res = a.res; p.res_mode = a.res_mode;
+    p.bias = a.bias; p.relu = a.relu;
     {
       static const int dbg = getenv("ARTSBIR_PG_DBG") ? atoi(getenv("ARTSBIR_PG_DBG")) : 0;
       p.dbg = dbg;
@@ -861,7 +867,8 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
       choice = atoi(force);
     } else {
       const ConvKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.Ho, a.Wo, a.res_mode,
-                        a.stats ? 1 : 0, a.nseg, bd ? p.bnb * 4 + p.bnb_nt : 0};
+                        (a.stats ? 1 : 0) | (a.bias ? 2 : 0) | (a.relu ? 4 : 0), a.nseg,
+                        bd ? p.bnb * 4 + p.bnb_nt : 0};
       std::lock_guard<std::mutex> lk(g_tune_mu);
       auto it = g_conv_choice.find(key);
       if (it != g_conv_choice.end()) {
@@ -909,7 +916,7 @@ extern "C" int artsbir_conv2d_fwd(const artsbir_conv_desc* d, const void* x, con
   a.M = (long long)d->N * Ho * Wo;
   a.y = y; a.ldy = ldy > 0 ? ldy : d->Cout;
   a.out_f32 = out_f32; a.accumulate = accumulate; a.bias = bias; a.stats = stats;
-  a.res = nullptr; a.res_mode = 0;
+  a.res = nullptr; a.res_mode = 0; a.relu = 0;
   a.nseg = 1; a.bnb_desc = nullptr; a.bnb_pstride = 0;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
@@ -935,8 +942,37 @@ extern "C" int artsbir_conv2d_fwd_seg(const artsbir_conv_desc* d, const void* x,
   a.M = (long long)d->N * Ho * Wo;
   a.y = y; a.ldy = d->Cout;
   a.out_f32 = 0; a.accumulate = 0; a.bias = nullptr; a.stats = stats;
-  a.res = nullptr; a.res_mode = 0;
+  a.res = nullptr; a.res_mode = 0; a.relu = 0;
   a.nseg = nseg; a.bnb_desc = nullptr; a.bnb_pstride = 0;
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
+}
+
+// eval-mode Conv2d + BatchNorm2d (folded into w and bias by artsbir_bn_fold) +
+// optional residual + optional ReLU in one launch (models.py:198-236 at inference)
+extern "C" int artsbir_conv2d_fwd_act(const artsbir_conv_desc* d, const void* x, const void* w, void* y,
+                                      const float* bias, const void* res, int res_mode, int relu, void* stream) {
+  if (check_conv(d)) return -1;
+  if (res_mode != 0 && res_mode != 1) { set_error("conv2d_fwd_act: res_mode %d (0 or 1)", res_mode); return -1; }
+  if (res_mode && !res) { set_error("conv2d_fwd_act: residual missing"); return -1; }
+  ConvArgs a;
+  int Ho, Wo;
+  fill_geom(d, Ho, Wo);
+  a.x = x;
+  a.sW = d->C;
+  a.sH = (long long)d->W * d->C;
+  a.sN = (long long)d->H * d->W * d->C;
+  a.x_elems = (long long)d->N * a.sN;
+  a.H = d->H; a.W = d->W; a.C = d->C;
+  a.R = d->R; a.S = d->S; a.stride = d->stride; a.pad = d->pad;
+  a.Ho = Ho; a.Wo = Wo;
+  a.in_scale = nullptr; a.in_shift = nullptr; a.in_relu = 0;
+  a.w = w; a.Cout = d->Cout; a.K = d->R * d->S * d->C;
+  a.M = (long long)d->N * Ho * Wo;
+  a.y = y; a.ldy = d->Cout;
+  a.out_f32 = 0; a.accumulate = 0; a.bias = bias; a.stats = nullptr;
+  a.res = res; a.res_mode = res_mode; a.relu = relu ? 1 : 0;
+  a.nseg = 1; a.bnb_desc = nullptr; a.bnb_pstride = 0;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
 }
@@ -998,7 +1034,7 @@ static int dgrad_common(const artsbir_conv_desc* d, const void* dy, const void* 
   a.M = (long long)d->N * d->H * d->W;
   a.y = dx; a.ldy = d->C;
   a.out_f32 = 0; a.accumulate = 0; a.bias = nullptr; a.stats = nullptr;
-  a.res = res; a.res_mode = res_mode;
+  a.res = res; a.res_mode = res_mode; a.relu = 0;
   a.nseg = nseg; a.bnb_desc = bnb; a.bnb_pstride = pstride;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
@@ -1021,7 +1057,7 @@ extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void*
   p.w = b; p.Cout = N; p.K = K; p.M = M;
   p.y = c; p.ldy = ldc > 0 ? ldc : N;
   p.out_f32 = out_f32; p.accumulate = accumulate; p.bias = bias; p.stats = stats;
-  p.res = nullptr; p.res_mode = 0;
+  p.res = nullptr; p.res_mode = 0; p.relu = 0;
   p.nseg = 1; p.bnb_desc = nullptr; p.bnb_pstride = 0;
   hipStream_t st = (hipStream_t)stream;
   return dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);

@@ -22,6 +22,8 @@ struct PgArgs {
   long long seg_stride;   // floats between the statistics of consecutive segments
   const void* res;        // optional residual (res_mode 1: same index, 2: 2x2 average-unpool)
   int res_mode;
+  const float* bias;      // optional per-output-channel bias (added after the residual, before the ReLU)
+  int relu;               // 1: ReLU on the stored output (eval-mode conv + folded BN + ReLU)
   int dbg;                // experiment bits (ARTSBIR_PG_DBG), 0 in production
   // fused BatchNorm-backward reduction (data gradient only, no stats): the
   // output d is the gradient at a BN(+ReLU) output; g = d * mask is stored and

@@ -459,6 +459,16 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += rsc[u] * to_f(rv[u].v[e]);
           }
+          if constexpr (!BNB) {
+            if (a.bias) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += a.bias[ch0 + e];
+            }
+            if (a.relu) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+          }
           if constexpr (BNB) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -645,6 +655,16 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
         if (RESK || (BK == 0 && res)) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rsc * to_f(rv[u].v[e]);
+        }
+        if constexpr (BK == 0) {
+          if (a.bias) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += a.bias[chc + e];
+          }
+          if (a.relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
         }
         if constexpr (BNB) {
 #pragma unroll
@@ -1609,6 +1629,16 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
         if (pv[j]) {
+          if constexpr (!BNB) {  // eval-mode conv + folded BN (+ ReLU): bias and activation here
+            if (a.bias) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += a.bias[ch0 + e];
+            }
+            if (a.relu) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
+          }
           if constexpr (BNB) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -1803,8 +1833,11 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
 
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
-  if (c == 20) return sconv_launch(a, st);
-  if (c == 21) return hconv_launch(a, st);
+  const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
+  if (act && (a.stats || a.bnb)) return false;
+  if (c == 20) return !act && sconv_launch(a, st);
+  if (c == 21) return hconv_launch(a, st);  // bias / ReLU epilogue supported
+  if (act && c >= 11 && c <= 13) return false;
   bool multi;
   if (!pg_supported(a, multi)) return false;
   if (c >= 11 && c <= 13) return pg_pf_launch(c, a, multi, st);
@@ -1849,7 +1882,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
 
 // static choice (no tuning): streaming kernel for many tiles, else best-scored tile
 int pgemm_default_cfg(const PgArgs& a) {
-  if (sconv_ok(a)) return 20;
+  if (sconv_ok(a) && !a.bias && !a.relu) return 20;
   bool multi;
   if (!pg_supported(a, multi)) return -1;
   const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;

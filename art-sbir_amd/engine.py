@@ -50,6 +50,11 @@ OVERLAP_WGRAD = os.environ.get("ARTSBIR_OVERLAP_WGRAD", "1") != "0"
 # ARTSBIR_MASK_BITS=0 makes the fused backward re-read the block output for its
 # ReLU mask instead of the bit mask written by the forward
 MASK_BITS = os.environ.get("ARTSBIR_MASK_BITS", "1") != "0"
+# inference (eval BatchNorm, no autograd): every BatchNorm folded into its conv
+# (artsbir_bn_fold) and applied with the ReLU / residual add in the conv's
+# epilogue (artsbir_conv2d_fwd_act): no separate BN / activation passes.
+# ARTSBIR_FUSED_EVAL=0 runs inference through the training-path kernels.
+FUSED_EVAL = os.environ.get("ARTSBIR_FUSED_EVAL", "1") != "0"
 # ARTSBIR_DETERMINISTIC=1 (parity runs): forward BatchNorm statistics
 # by a fixed-order f64 reduction of the stored conv output (artsbir_bn_stats_det)
 # instead of the epilogue's f32 atomics, so a forward is bit-identical from run
@@ -182,6 +187,8 @@ class Engine:
         # as the backward proceeds, so the data-parallel all-reduce overlaps it
         self.grad_hook = None
         self._side_keep = []  # tensors the weight-gradient stream still reads (released at the join)
+        self._eval = None      # folded conv weights + biases of the eval forward
+        self._eval_key = None
 
     # ------------------------------------------------------------------ utils
     @property
@@ -321,6 +328,94 @@ class Engine:
              tag=f"act_pool {B}x{H}x{W}x{C} pool{pool}")
         return out
 
+    # ------------------------------------------------ inference (folded BN)
+    def _eval_params_key(self):
+        bns = [mod for mod in self.model.modules() if isinstance(mod, torch.nn.BatchNorm2d)]
+        return (self._params_key(), tuple((b.running_mean.data_ptr(), b.running_mean._version,
+                                           b.running_var._version, b.weight._version, b.bias._version) for b in bns))
+
+    def _fold(self, conv, bn, ci_pad=None):
+        """conv weight with the eval BatchNorm folded in, packed for the forward, and its bias"""
+        w = conv.weight.detach().float().contiguous()
+        co, ci, r, s = w.shape
+        wf = torch.empty_like(w)
+        bias = torch.empty(co, dtype=torch.float32, device=w.device)
+        call("artsbir_bn_fold", ptr(w), co, ci * r * s, ptr(bn.weight.detach()), ptr(bn.bias.detach()),
+             ptr(bn.running_mean), ptr(bn.running_var), float(bn.eps), ptr(wf), ptr(bias), _s())
+        ci_pad = ci_pad or ci
+        fw = self._empty(co, r, s, ci_pad, device=w.device)
+        call("artsbir_pack_weight", self.dt, ptr(wf), co, ci, r, s, ci_pad, 0, 0, ptr(fw), _s())
+        return fw, bias
+
+    def _eval_packed(self):
+        key = self._eval_params_key()
+        if self._eval_key != key:
+            m = self.model
+            ev = {}
+            blocks = []
+            for blk in m.blocks():
+                d = {"conv1": self._fold(blk.conv1, blk.bn1), "conv2": self._fold(blk.conv2, blk.bn2),
+                     "conv3": self._fold(blk.conv3, blk.bn3)}
+                if blk.downsample is not None:
+                    d["down"] = self._fold(blk.downsample[1], blk.downsample[2])
+                blocks.append(d)
+            ev["blocks"] = blocks
+            self._eval, self._eval_key = ev, key
+        return self._eval
+
+    def _conv_act(self, x, fb, conv, stride, pad, relu, res=None):
+        fw, bias = fb
+        cout, _, R, S = conv.weight.shape
+        B, H, W, C = x.shape
+        Ho = (H + 2 * pad - R) // stride + 1
+        Wo = (W + 2 * pad - S) // stride + 1
+        y = self._empty(B, Ho, Wo, cout, device=x.device)
+        d = self._desc(B, H, W, C, cout, R, S, stride, pad)
+        es = y.element_size()
+        nbytes = float(es * (B * H * W * C + cout * R * S * C + B * Ho * Wo * cout * (2 if res is not None else 1)))
+        call("artsbir_conv2d_fwd_act", d, ptr(x), ptr(fw), ptr(y), ptr(bias), ptr(res) if res is not None else None,
+             1 if res is not None else 0, relu, _s(), kernel="auto", flops=2.0 * B * Ho * Wo * cout * R * S * C,
+             nbytes=nbytes, tag=f"fwd_act {B}x{H}x{W}x{C}->{cout} {R}x{S}/{stride}")
+        return y
+
+    def _forward_eval(self, xs):
+        """inference forward (models.py:344-360 with eval BatchNorm): conv + folded
+        BN + ReLU (+ residual) per launch, AvgPool2d as a pooling pass"""
+        m = self.model
+        ev = self._eval_packed()
+        pk = self.packed()
+        G = len(xs)
+        Bs, cin, R, R2 = xs[0].shape
+        B = G * Bs
+        dev = xs[0].device
+        x0 = self._empty(B, R, R2, 8, device=dev)
+        for i, xi in enumerate(xs):
+            xi = xi.contiguous().float()
+            call("artsbir_pack_input", self.dt, ptr(xi), Bs, cin, R, R2, _at(x0, i * Bs), _s())
+        # the stem's few-channel convs stay on their direct kernels (sconv / hconv,
+        # no bias epilogue) with the eval BN applied by act_pool: faster than the
+        # GEMM kernel with a fused epilogue at 8 / 32 input channels
+        self._G = 1
+        (fw1, _), (fw2, _), (fw3, _) = pk["stem"]
+        y1, b1 = self._conv_bn(Act(x0), m.conv1, m.bn1, fw1, 2, 1, False, None)
+        y2, b2 = self._conv_bn(Act(self._act_pool(y1, b1, 1, 0)), m.conv2, m.bn2, fw2, 1, 1, False, None)
+        y3, b3 = self._conv_bn(Act(self._act_pool(y2, b2, 1, 0)), m.conv3, m.bn3, fw3, 1, 1, False, None)
+        h = self._act_pool(y3, b3, 1, 2)
+        for blk, bp in zip(m.blocks(), ev["blocks"]):
+            s = blk.stride
+            a1 = self._conv_act(h, bp["conv1"], blk.conv1, 1, 0, 1)
+            a2 = self._conv_act(a1, bp["conv2"], blk.conv2, 1, 1, 1)
+            if s > 1:
+                a2 = self._act_pool(a2, None, 0, s)
+            if blk.downsample is not None:
+                din = self._act_pool(h, None, 0, s) if s > 1 else h
+                idn = self._conv_act(din, bp["down"], blk.downsample[1], 1, 0, 0)
+            else:
+                idn = h
+            h = self._conv_act(a2, bp["conv3"], blk.conv3, 1, 0, 1, res=idn)
+        out, _ = self._attnpool_fwd(m.attnpool, pk, h)
+        return out
+
     # ---------------------------------------------------------------- forward
     def forward(self, x, train: bool, save: bool):
         """x: [B,3,R,R] or a list of G such batches (G separate reference forward
@@ -334,6 +429,8 @@ class Engine:
         G = len(xs)
         self._G = G
         _hip.lib().artsbir_set_deterministic(1 if DETERMINISTIC else 0)
+        if not train and not save and FUSED_EVAL and type(self) is Engine:
+            return self._forward_eval(xs), None
         m = self.model
         pk = self.packed()
         Bs, cin, R, R2 = xs[0].shape

@@ -92,6 +92,13 @@ int artsbir_conv2d_dgrad(const artsbir_conv_desc* d, const void* dy, const void*
 int artsbir_conv2d_fwd_seg(const artsbir_conv_desc* d, const void* x, const void* w, void* y, int nseg,
                            float* stats, void* stream);
 
+/* y = act(conv(x) + bias[n] (+ res[m][n])), act = ReLU if relu (res_mode 0 / 1).
+ * Eval-mode Conv2d + BatchNorm2d + ReLU (+ the Bottleneck's residual add) of
+ * models.py:198-236 in one launch, the BatchNorm folded into w and bias by
+ * artsbir_bn_fold (inference: no batch statistics, nothing else to apply). */
+int artsbir_conv2d_fwd_act(const artsbir_conv_desc* d, const void* x, const void* w, void* y, const float* bias,
+                           const void* res, int res_mode, int relu, void* stream);
+
 /* conv2d_dgrad whose output is the gradient at the output of a BatchNorm2d(+ReLU)
  * (models.py:199-210, 234-235): the BN-backward reduction is fused into it.  dx
  * receives g = dx_raw * relu-mask (bnb->kind 1: mask_bn(y[0]) > 0;
@@ -199,6 +206,11 @@ int artsbir_bn_bwd_finalize_seg(const float* slots, int nseg, long long seg_stri
                                 const float* gamma, const float* istd, long long istd_stride, float* dgamma,
                                 float* dbeta, float* coef, void* stream);
 int artsbir_bn_bwd_apply(const artsbir_bn_bwd_desc* d, void* stream);
+/* BatchNorm2d (eval) folded into the preceding conv (models.py:198-236):
+ * w_out[co][k] = w[co][k] * gamma/sqrt(var+eps), bias_out[co] = beta - mean*gamma/sqrt(var+eps);
+ * w f32 [Co][K] in the reference layout (K = Ci*R*S). */
+int artsbir_bn_fold(const float* w, int Co, long long K, const float* gamma, const float* beta, const float* mean,
+                    const float* var, float eps, float* w_out, float* bias_out, void* stream);
 /* out[c] += sum_r x[r*ld + c]  (bias / positional-embedding gradients). */
 int artsbir_colsum(int dtype, const void* x, long long rows, long long ld, long long C, float* out, void* stream);
 

@@ -156,3 +156,41 @@ def test_triplet_step_against_golden_fixture(dev):
     with torch.no_grad():
         e = mine(elements[0].to(dev)).cpu().numpy()
     np.testing.assert_allclose(e, gold["emb_eval"], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-4), (torch.bfloat16, 3e-2)])
+def test_fused_eval_matches_unfused(dtype, tol, dev):
+    """inference with every BatchNorm folded into its conv and applied with the
+    ReLU / residual add in the conv epilogue (engine._forward_eval) = the
+    training-path kernels with eval BatchNorm (separate BN / activation passes),
+    on non-trivial running statistics; the f32 path also against the oracle"""
+    import engine
+    cfg = SMALL
+    ref, mine = _pair(cfg, dev, dtype=dtype)
+    g = torch.Generator().manual_seed(5)
+    with torch.no_grad():  # non-trivial BN affine and running statistics
+        for mod_r, mod_m in zip(ref.modules(), mine.modules()):
+            if isinstance(mod_m, torch.nn.BatchNorm2d):
+                C = mod_m.num_features
+                vals = [1 + 0.2 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g),
+                        0.2 * torch.randn(C, generator=g), 0.5 + torch.rand(C, generator=g)]
+                for mod in (mod_r, mod_m):
+                    for t, v in zip((mod.weight, mod.bias, mod.running_mean, mod.running_var), vals):
+                        t.copy_(v.to(t.device))
+    ref.eval(); mine.eval()
+    s, _, _ = oenc.synthetic_triplet(6, cfg["res"])
+    old = engine.FUSED_EVAL
+    try:
+        with torch.no_grad():
+            engine.FUSED_EVAL = True
+            e_fused = mine(s.to(dev)).float().cpu()
+            engine.FUSED_EVAL = False
+            e_plain = mine(s.to(dev)).float().cpu()
+    finally:
+        engine.FUSED_EVAL = old
+    rel = ((e_fused - e_plain).norm() / e_plain.norm()).item()
+    assert rel < tol, rel
+    if dtype == torch.float32:
+        with torch.no_grad():
+            e_ref = ref(s)
+        assert torch.allclose(e_fused, e_ref, atol=1e-3, rtol=1e-3), _rel(e_fused, e_ref)
