@@ -283,8 +283,9 @@ def main():
                     help="three separate encoder calls per step instead of forward_branches")
     ap.add_argument("--no-embed", action="store_true", help="skip the embed-only (eval-BN) leg")
     ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step")
-    ap.add_argument("--c5", action="store_true",
-                    help="add the C5 leg: ViT-B/16 768-d triplet training step, fp8 projections, 512 triplets")
+    ap.add_argument("--c5", action="store_true", default=True,
+                    help="the C5 leg: ViT-B/16 768-d triplet training step, fp8 projections, 512 triplets (default)")
+    ap.add_argument("--no-c5", dest="c5", action="store_false", help="skip the C5 leg")
     ap.add_argument("--c5-batch", type=int, default=512, help="C5 triplets per GPU per step")
     ap.add_argument("--no-loss-check", action="store_true", help="skip the f32 step-0 loss check")
     ap.add_argument("--tune-cache", default=None,

@@ -195,3 +195,63 @@ def test_gemm_tn_strided(M, N, K, ldd, ldx, cfg, dev):
         assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
     finally:
         os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+
+
+@pytest.mark.parametrize("cfg", ["auto", "0", "1", "2", "3", "4", "10", "21"])
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("mode", ["bias", "bias_relu", "bias_res_relu"])
+def test_conv_fwd_act(case, cfg, mode, dev, cfg_env):
+    """artsbir_conv2d_fwd_act (eval conv + folded BN + ReLU + residual) on every
+    kernel that takes the bias / ReLU epilogue, vs torch fp32 on bf16 operands;
+    shapes a candidate does not take fall back to the auto choice"""
+    N, H, W, C, Co, R, S, st, pd = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+    w = (torch.randn(Co, C, R, S, generator=g) * 0.1).bfloat16().float()
+    bias = torch.randn(Co, generator=g)
+    ref = F.conv2d(x, w, stride=st, padding=pd) + bias[None, :, None, None]
+    res = None
+    if mode == "bias_res_relu":
+        res = torch.randn(ref.shape, generator=g).bfloat16().float()
+        ref = ref + res
+    if mode != "bias":
+        ref = ref.clamp_min(0)
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    d = _hip.conv_desc(torch.bfloat16, N, H, W, C, Co, R, S, st, pd)
+    xd = _nhwc(x).to(dev, torch.bfloat16)
+    wp = torch.empty(Co, R, S, C, dtype=torch.bfloat16, device=dev)
+    wd, biasd = w.to(dev), bias.to(dev)  # alive through the calls
+    _hip.call("artsbir_pack_weight", _hip.DT_BF16, wd.data_ptr(), Co, C, R, S, C, 0, 0, wp.data_ptr(),
+              _hip.stream())
+    y = torch.empty(N, Ho, Wo, Co, dtype=torch.bfloat16, device=dev)
+    resd = _nhwc(res).to(dev, torch.bfloat16) if res is not None else None
+    _set(cfg)
+    try:
+        _hip.call("artsbir_conv2d_fwd_act", d, xd.data_ptr(), wp.data_ptr(), y.data_ptr(), biasd.data_ptr(),
+                  resd.data_ptr() if resd is not None else None, 1 if resd is not None else 0,
+                  0 if mode == "bias" else 1, _hip.stream())
+    except _hip.HipError:
+        os.environ.pop("ARTSBIR_PGEMM_CFG", None)  # candidate not applicable to this shape / epilogue
+        _hip.call("artsbir_conv2d_fwd_act", d, xd.data_ptr(), wp.data_ptr(), y.data_ptr(), biasd.data_ptr(),
+                  resd.data_ptr() if resd is not None else None, 1 if resd is not None else 0,
+                  0 if mode == "bias" else 1, _hip.stream())
+    torch.cuda.synchronize()
+    out = y.float().cpu().permute(0, 3, 1, 2)
+    assert torch.allclose(out, ref, atol=3e-2, rtol=1e-2), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("M,N,K", [(600, 512, 256), (300, 1024, 2048), (57, 96, 64)])
+def test_gemm_nt_bf16_bias(M, N, K, dev):
+    """biased dense GEMM with a bf16 output (the attention-pool k|v projection) on
+    the pipelined kernel, vs torch fp32"""
+    g = torch.Generator().manual_seed(12)
+    a = torch.randn(M, K, generator=g).bfloat16().float()
+    b = (torch.randn(N, K, generator=g) * 0.05).bfloat16().float()
+    bias = torch.randn(N, generator=g)
+    ref = a @ b.T + bias
+    c = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    ad, bd, biasd = a.to(dev, torch.bfloat16), b.to(dev, torch.bfloat16), bias.to(dev)  # alive through the call
+    _hip.call("artsbir_gemm_nt", _hip.DT_BF16, M, N, K, ad.data_ptr(), K, bd.data_ptr(), c.data_ptr(), N, 0, 0,
+              biasd.data_ptr(), None, _hip.stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(c.float().cpu(), ref, atol=3e-2, rtol=1e-2), (c.float().cpu() - ref).abs().max()
