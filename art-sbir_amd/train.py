@@ -11,7 +11,8 @@ Differences, all opt-in or documented:
   * get_loss dispatches on the output TYPE, not ``len(output) > 3`` (the
     reference misfires for a plain model at batch size <= 3);
   * the reference evaluates its test loss on the stale last TRAIN batch
-    (train.py:80,89); here the test batches are used unless ``--stale_eval``;
+    (train.py:80,89); that is reproduced by default (drop-in), ``--fresh_eval``
+    evaluates on the test batches instead;
   * data: the Sketchy/Kaggle files are not available offline — ``-d Synthetic``
     (default) generates the triplets (data_preparation.SyntheticTripletDataset);
   * one process per GPU when launched by torch.distributed.run: minibatches
@@ -55,7 +56,7 @@ def get_loss(loss_fn, model, elements):
 
 
 def triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
-                  stale_eval=False):
+                  stale_eval=True):
     # the training loop runs on a high-priority stream, so the dispatcher serves
     # the data-gradient / BatchNorm chain ahead of the weight gradients that the
     # engine overlaps on its side stream
@@ -68,7 +69,7 @@ def triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, opt
 
 
 def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, optimizer, with_classification,
-                   stale_eval=False):
+                   stale_eval=True):
     start_time = timer()
     reducer = ddp.attach_overlapped_reducer(model)
     train_losses, test_losses, itrain_losses, itest_losses = [], [], [], []
@@ -165,7 +166,10 @@ def parse_args(argv=None):
     p.add_argument('--resolution', type=int, default=224)
     p.add_argument('--width', type=int, default=64)
     p.add_argument('--synthetic_n', type=int, default=256, help="triplets in the synthetic dataset")
-    p.add_argument('--stale_eval', action='store_true', help="reproduce the reference's stale-batch test loss")
+    p.add_argument('--stale_eval', dest='stale_eval', action='store_true', default=True,
+                   help="the reference's test loss on the stale last train batch (train.py:80,89; default)")
+    p.add_argument('--fresh_eval', dest='stale_eval', action='store_false',
+                   help="test loss over the test batches instead of the stale train batch")
     p.add_argument('--no_save', action='store_true')
     return p.parse_args(argv)
 
