@@ -110,6 +110,9 @@ SIGNATURES = {
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_mha_fwd_lse": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_layernorm_bwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_layernorm_bwd_sums": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp],
+    "artsbir_quickgelu_bwd_sum": [_c_int, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
     "artsbir_quickgelu_bwd": [_c_int, _vp, _vp, _c_ll, _vp, _vp],
     "artsbir_mha_bwd": [_c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_vit_patchify": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp],

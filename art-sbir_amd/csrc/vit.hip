@@ -88,10 +88,11 @@ __global__ void __launch_bounds__(256) layernorm_v_kernel(const T* __restrict__ 
 
 // LayerNorm backward with 8-column chunks per lane; each block's 4 waves reduce
 // their dgamma / dbeta partials in LDS and add them with one atomic per column
-template <typename T, int NCH>
+template <typename T, int NCH, bool SUMS>
 __device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __restrict__ dy, const T* dres, T* dx,
                                            long long row, int C, float eps, int lane, const float (&gm)[NCH][8],
-                                           float (&pg)[NCH][8], float (&pb)[NCH][8]) {
+                                           float (&pg)[NCH][8], float (&pb)[NCH][8], float (&pr)[NCH][8],
+                                           float (&po)[NCH][8]) {
   const int nch = C >> 3;
   const T* xr = x + row * C;
   const T* gr = dy + row * C;
@@ -148,37 +149,50 @@ __device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __r
 #pragma unroll
       for (int e = 0; e < 8; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[e];
       vt_store8(o + ch * 8, out);
+      if constexpr (SUMS) {  // column sums of the residual gradient and of dx (bias gradients)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { pr[u][e] += res[e]; po[u][e] += out[e]; }
+      }
     }
   }
 }
 
 // LayerNorm backward with 8-column chunks per lane; each block's 4 waves reduce
-// their dgamma / dbeta partials in LDS and add them with one atomic per column
-template <typename T, int NCH>
+// their dgamma / dbeta partials in LDS and add them with one atomic per column.
+// SUMS: also the column sums of dres and of dx (the bias gradients of the
+// projections around the LayerNorm, instead of two colsum passes)
+template <typename T, int NCH, bool SUMS>
 __global__ void __launch_bounds__(256) layernorm_bwd_v_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
                                                               const T* __restrict__ dy, long long rows, int C, float eps,
                                                               const T* dres, T* dx, float* __restrict__ dgamma,
-                                                              float* __restrict__ dbeta) {
-  __shared__ float red[2][3][64 * NCH * 8];
+                                                              float* __restrict__ dbeta, float* __restrict__ dres_sum,
+                                                              float* __restrict__ dx_sum) {
+  constexpr int NR = SUMS ? 4 : 2;
+  __shared__ float red[NR][3][64 * NCH * 8];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nch = C >> 3;
-  float pg[NCH][8], pb[NCH][8], gm[NCH][8];
+  float pg[NCH][8], pb[NCH][8], gm[NCH][8], pr[NCH][8], po[NCH][8];
 #pragma unroll
   for (int u = 0; u < NCH; ++u) {
     const int ch = lane + 64 * u;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { pg[u][e] = 0.f; pb[u][e] = 0.f; gm[u][e] = 0.f; }
+    for (int e = 0; e < 8; ++e) { pg[u][e] = 0.f; pb[u][e] = 0.f; gm[u][e] = 0.f; pr[u][e] = 0.f; po[u][e] = 0.f; }
     if (ch < nch) vt_load8(gamma + ch * 8, gm[u]);
   }
   for (long long row = blockIdx.x * 4LL + w; row < rows; row += gridDim.x * 4LL)
-    ln_bwd_row<T, NCH>(x, dy, dres, dx, row, C, eps, lane, gm, pg, pb);
+    ln_bwd_row<T, NCH, SUMS>(x, dy, dres, dx, row, C, eps, lane, gm, pg, pb, pr, po);
   if (w > 0) {
 #pragma unroll
     for (int u = 0; u < NCH; ++u)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        red[0][w - 1][(u * 64 + lane) * 8 + e] = pg[u][e];
-        red[1][w - 1][(u * 64 + lane) * 8 + e] = pb[u][e];
+        const int i = (u * 64 + lane) * 8 + e;
+        red[0][w - 1][i] = pg[u][e];
+        red[1][w - 1][i] = pb[u][e];
+        if constexpr (SUMS) {
+          red[NR - 2][w - 1][i] = pr[u][e];
+          red[NR - 1][w - 1][i] = po[u][e];
+        }
       }
   }
   __syncthreads();
@@ -192,6 +206,12 @@ __global__ void __launch_bounds__(256) layernorm_bwd_v_kernel(const T* __restric
           const int i = (u * 64 + lane) * 8 + e;
           atomicAdd(dgamma + ch * 8 + e, pg[u][e] + red[0][0][i] + red[0][1][i] + red[0][2][i]);
           atomicAdd(dbeta + ch * 8 + e, pb[u][e] + red[1][0][i] + red[1][1][i] + red[1][2][i]);
+          if constexpr (SUMS) {
+            if (dres_sum)
+              atomicAdd(dres_sum + ch * 8 + e, pr[u][e] + red[NR - 2][0][i] + red[NR - 2][1][i] + red[NR - 2][2][i]);
+            if (dx_sum)
+              atomicAdd(dx_sum + ch * 8 + e, po[u][e] + red[NR - 1][0][i] + red[NR - 1][1][i] + red[NR - 1][2][i]);
+          }
         }
     }
   }
@@ -388,6 +408,55 @@ __global__ void quickgelu_bwd_kernel(const T* __restrict__ x, const T* __restric
     const float sg = 1.f / (1.f + __expf(-1.702f * v));
     dx[i] = from_f<T>(to_f(dy[i]) * (sg + 1.702f * v * sg * (1.f - sg)));
   }
+}
+
+// QuickGELU backward over rows of C columns with the column sums of dx (the
+// bias gradient of the projection that produced x): a thread owns 8 columns
+// and walks rows; one atomic per column per block at the end
+template <typename T>
+__global__ void __launch_bounds__(128) quickgelu_bwd_sum_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                                long long rows, int C, T* __restrict__ dx,
+                                                                float* __restrict__ dsum) {
+  const int c8 = blockIdx.x * 128 + threadIdx.x;
+  if (c8 * 8 >= C) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  constexpr int U = 4;  // rows in flight per thread
+  const long long step = gridDim.y;
+  long long r = blockIdx.y;
+  for (; r + (U - 1) * step < rows; r += U * step) {
+    float v[U][8], g[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = (r + u * step) * C + c8 * 8;
+      vt_load8(x + o, v[u]);
+      vt_load8(dy + o, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sg = 1.f / (1.f + __expf(-1.702f * v[u][e]));
+        v[u][e] = g[u][e] * (sg + 1.702f * v[u][e] * sg * (1.f - sg));
+        acc[e] += v[u][e];
+      }
+      vt_store8(dx + (r + u * step) * C + c8 * 8, v[u]);
+    }
+  }
+  for (; r < rows; r += step) {
+    const long long o = r * C + c8 * 8;
+    float v[8], g[8];
+    vt_load8(x + o, v);
+    vt_load8(dy + o, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sg = 1.f / (1.f + __expf(-1.702f * v[e]));
+      v[e] = g[e] * (sg + 1.702f * v[e] * sg * (1.f - sg));
+      acc[e] += v[e];
+    }
+    vt_store8(dx + o, v);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) atomicAdd(dsum + c8 * 8 + e, acc[e]);
 }
 
 // attention backward, query side, one wave per (query i, batch n, head h):
@@ -628,22 +697,31 @@ extern "C" int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int
   return 0;
 }
 
-extern "C" int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamma, const void* dy, long long rows,
-                                     int C, float eps, const void* dres, void* dx, float* dgamma, float* dbeta,
-                                     void* stream) {
+static int layernorm_bwd_impl(int dtype, const void* x, const float* gamma, const void* dy, long long rows, int C,
+                              float eps, const void* dres, void* dx, float* dgamma, float* dbeta, float* dres_sum,
+                              float* dx_sum, void* stream) {
   if (rows <= 0) return 0;
   if (C < 1 || C > 1024) { set_error("layernorm_bwd: C=%d outside [1, 1024]", C); return -1; }
+  const bool sums = dres_sum || dx_sum;
+  if (dres_sum && !dres) { set_error("layernorm_bwd: dres_sum without dres"); return -1; }
   const bool vec = C % 8 == 0 && !((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
                                     reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dres) |
                                     reinterpret_cast<uintptr_t>(gamma)) & 15);
+  if (!vec && sums) { set_error("layernorm_bwd: column sums need C %% 8 == 0 and 16-B aligned rows"); return -1; }
   if (vec) {  // 8-column chunks per lane; 512 blocks: few atomics per column
     long long gv = (rows + 3) / 4;
     const unsigned gridv = (unsigned)(gv > 512 ? 512 : gv);
-#define LNBV(N) VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_bwd_v_kernel<T, N>), dim3(gridv), dim3(256), 0,   \
-                                                      (hipStream_t)stream, (const T*)x, gamma, (const T*)dy, rows, C, \
-                                                      eps, (const T*)dres, (T*)dx, dgamma, dbeta))
-    if (C <= 512) LNBV(1);
-    else LNBV(2);
+#define LNBV(N, S) VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_bwd_v_kernel<T, N, S>), dim3(gridv), dim3(256), 0, \
+                                                         (hipStream_t)stream, (const T*)x, gamma, (const T*)dy, rows,  \
+                                                         C, eps, (const T*)dres, (T*)dx, dgamma, dbeta, dres_sum,      \
+                                                         dx_sum))
+    if (C <= 512) {
+      if (sums) LNBV(1, true);
+      else LNBV(1, false);
+    } else {
+      if (sums) LNBV(2, true);
+      else LNBV(2, false);
+    }
 #undef LNBV
     ARTSBIR_CHECK_LAUNCH("layernorm_bwd");
     return 0;
@@ -664,11 +742,41 @@ extern "C" int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamm
   return 0;
 }
 
+extern "C" int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamma, const void* dy, long long rows,
+                                     int C, float eps, const void* dres, void* dx, float* dgamma, float* dbeta,
+                                     void* stream) {
+  return layernorm_bwd_impl(dtype, x, gamma, dy, rows, C, eps, dres, dx, dgamma, dbeta, nullptr, nullptr, stream);
+}
+
+extern "C" int artsbir_layernorm_bwd_sums(int dtype, const void* x, const float* gamma, const void* dy,
+                                          long long rows, int C, float eps, const void* dres, void* dx, float* dgamma,
+                                          float* dbeta, float* dres_sum, float* dx_sum, void* stream) {
+  return layernorm_bwd_impl(dtype, x, gamma, dy, rows, C, eps, dres, dx, dgamma, dbeta, dres_sum, dx_sum, stream);
+}
+
 extern "C" int artsbir_quickgelu_bwd(int dtype, const void* x, const void* dy, long long n, void* dx, void* stream) {
   if (n <= 0) return 0;
   VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_bwd_kernel<T>, dim3(vit_grid((n + 7) / 8)), dim3(256), 0,
                                        (hipStream_t)stream, (const T*)x, (const T*)dy, n, (T*)dx));
   ARTSBIR_CHECK_LAUNCH("quickgelu_bwd");
+  return 0;
+}
+
+extern "C" int artsbir_quickgelu_bwd_sum(int dtype, const void* x, const void* dy, long long rows, int C, void* dx,
+                                         float* dsum, void* stream) {
+  if (rows <= 0) return 0;
+  if (C % 8 || !dsum || ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
+                           reinterpret_cast<uintptr_t>(dx)) & 15)) {
+    set_error("quickgelu_bwd_sum: C %% 8 == 0, 16-B aligned rows and a sum buffer required");
+    return -1;
+  }
+  const unsigned gx = (unsigned)((C / 8 + 127) / 128);
+  long long gy = 1024 / gx;
+  if (gy > rows) gy = rows;
+  if (gy < 1) gy = 1;
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_bwd_sum_kernel<T>, dim3(gx, (unsigned)gy), dim3(128), 0,
+                                       (hipStream_t)stream, (const T*)x, (const T*)dy, rows, C, (T*)dx, dsum));
+  ARTSBIR_CHECK_LAUNCH("quickgelu_bwd_sum");
   return 0;
 }
 

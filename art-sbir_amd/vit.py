@@ -103,11 +103,20 @@ def _ln(x2: torch.Tensor, w, b, eps) -> torch.Tensor:
     return y
 
 
-def _ln_bwd(x2, w, dy2, eps, dres, dw, db) -> torch.Tensor:
+def _ln_bwd(x2, w, dy2, eps, dres, dw, db, dres_sum=None, dx_sum=None) -> torch.Tensor:
+    """LayerNorm backward (+ residual gradient); with dres_sum / dx_sum the column
+    sums of dres and dx (bias gradients of the projections around it) in the same pass"""
     dx = torch.empty_like(x2)
-    call("artsbir_layernorm_bwd", _dt(x2), x2.data_ptr(), w.detach().float().contiguous().data_ptr(),
-         dy2.data_ptr(), x2.shape[0], x2.shape[1], float(eps), dres.data_ptr() if dres is not None else None,
-         dx.data_ptr(), dw.data_ptr(), db.data_ptr(), _st())
+    wg = w.detach().float().contiguous()
+    if dres_sum is None and dx_sum is None:
+        call("artsbir_layernorm_bwd", _dt(x2), x2.data_ptr(), wg.data_ptr(), dy2.data_ptr(), x2.shape[0],
+             x2.shape[1], float(eps), dres.data_ptr() if dres is not None else None, dx.data_ptr(), dw.data_ptr(),
+             db.data_ptr(), _st())
+    else:
+        call("artsbir_layernorm_bwd_sums", _dt(x2), x2.data_ptr(), wg.data_ptr(), dy2.data_ptr(), x2.shape[0],
+             x2.shape[1], float(eps), dres.data_ptr() if dres is not None else None, dx.data_ptr(), dw.data_ptr(),
+             db.data_ptr(), dres_sum.data_ptr() if dres_sum is not None else None,
+             dx_sum.data_ptr() if dx_sum is not None else None, _st())
     return dx
 
 
@@ -260,17 +269,18 @@ class _BlockFunction(torch.autograd.Function):
         dy2 = dy.contiguous().view(M, E).to(T)
         # mlp: y = x1 + c_proj(gelu(c_fc(ln_2(x1))))
         _wgrad(dy2, a, dw_pr)
-        _colsum(dy2, db_pr)
         da = _gemm(dy2, _t(w_pr, T), M, 4 * E, E)
         df = torch.empty_like(f)
-        call("artsbir_quickgelu_bwd", _dt(f), f.data_ptr(), da.data_ptr(), f.numel(), df.data_ptr(), _st())
+        # QuickGELU backward with the c_fc bias gradient (column sums of df) in the same pass
+        call("artsbir_quickgelu_bwd_sum", _dt(f), f.data_ptr(), da.data_ptr(), M, 4 * E, df.data_ptr(),
+             db_fc.data_ptr(), _st())
         _wgrad(df, h2, dw_fc)
-        _colsum(df, db_fc)
         dh2 = _gemm(df, _t(w_fc, T), M, E, 4 * E)
-        dx1 = _ln_bwd(x1t, g2, dh2, blk.ln_2.eps, dy2, dg2, dbe2)
+        # LayerNorm-2 backward + the residual gradient dy2; its pass also sums the
+        # c_proj bias gradient (columns of dy2) and the out_proj one (columns of dx1)
+        dx1 = _ln_bwd(x1t, g2, dh2, blk.ln_2.eps, dy2, dg2, dbe2, dres_sum=db_pr, dx_sum=db_o)
         # attention: x1 = x + out_proj(mha(in_proj(ln_1(x))))
         _wgrad(dx1, att, dw_o)
-        _colsum(dx1, db_o)
         datt = _gemm(dx1, _t(w_o, T), M, E, E)
         dqkv = torch.empty_like(qkv)
         dsc = torch.empty(M * heads, dtype=torch.float32, device=dev)

@@ -246,8 +246,18 @@ int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int heads, con
  * ACCUMULATED (f32), C <= 1024. */
 int artsbir_layernorm_bwd(int dtype, const void* x, const float* gamma, const void* dy, long long rows, int C,
                           float eps, const void* dres, void* dx, float* dgamma, float* dbeta, void* stream);
+/* the same plus the column sums of dres and of dx added into dres_sum / dx_sum
+ * (either nullable): the bias gradients of the projections before and after
+ * the LayerNorm (models.py:396-417 c_proj / out_proj) in the same pass. */
+int artsbir_layernorm_bwd_sums(int dtype, const void* x, const float* gamma, const void* dy, long long rows, int C,
+                               float eps, const void* dres, void* dx, float* dgamma, float* dbeta, float* dres_sum,
+                               float* dx_sum, void* stream);
 /* QuickGELU backward: dx = dy * (s + 1.702 x s (1 - s)), s = sigmoid(1.702 x). */
 int artsbir_quickgelu_bwd(int dtype, const void* x, const void* dy, long long n, void* dx, void* stream);
+/* QuickGELU backward over [rows][C] with dsum[c] += sum_r dx[r][c] (the c_fc
+ * bias gradient in the same pass). */
+int artsbir_quickgelu_bwd_sum(int dtype, const void* x, const void* dy, long long rows, int C, void* dx, float* dsum,
+                              void* stream);
 /* Attention backward: dqkv [L*N][3E] (dq | dk | dv, overwritten) from qkv, the
  * forward output out, its gradient dout and lse (artsbir_mha_fwd_lse);
  * dscratch: f32 [L*N*heads] (the per-row dout . out). */
