@@ -96,18 +96,23 @@ __device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __r
   const int nch = C >> 3;
   const T* xr = x + row * C;
   const T* gr = dy + row * C;
-  float xv[NCH][8], gv[NCH][8];
+  const T* rr = dres ? dres + row * C : nullptr;
+  float xv[NCH][8], gv[NCH][8], res[NCH][8];
   float s = 0.f;
 #pragma unroll
-  for (int u = 0; u < NCH; ++u) {
+  for (int u = 0; u < NCH; ++u) {  // all three operands of the row requested together
     const int ch = lane + 64 * u;
     if (ch < nch) {
       vt_load8(xr + ch * 8, xv[u]);
       vt_load8(gr + ch * 8, gv[u]);
+      if (rr) vt_load8(rr + ch * 8, res[u]);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { xv[u][e] = 0.f; gv[u][e] = 0.f; }
     }
+    if (!rr || ch >= nch)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) res[u][e] = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) s += xv[u][e];
   }
@@ -136,22 +141,17 @@ __device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __r
   a = warp_sum(a) / (float)C;
   b = warp_sum(b) / (float)C;
   T* o = dx + row * C;
-  const T* rr = dres ? dres + row * C : nullptr;
 #pragma unroll
   for (int u = 0; u < NCH; ++u) {
     const int ch = lane + 64 * u;
     if (ch < nch) {
-      float res[8], out[8];
-      if (rr) vt_load8(rr + ch * 8, res);
-      else
+      float out[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) res[e] = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[e];
+      for (int e = 0; e < 8; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[u][e];
       vt_store8(o + ch * 8, out);
       if constexpr (SUMS) {  // column sums of the residual gradient and of dx (bias gradients)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { pr[u][e] += res[e]; po[u][e] += out[e]; }
+        for (int e = 0; e < 8; ++e) { pr[u][e] += res[u][e]; po[u][e] += out[e]; }
       }
     }
   }
