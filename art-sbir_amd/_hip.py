@@ -110,6 +110,10 @@ SIGNATURES = {
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_mha_fwd_lse": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_layernorm_bwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_layernorm_fwd_pmax": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp, _vp],
+    "artsbir_quickgelu_pmax": [_c_int, _vp, _c_ll, _vp, _vp, _vp],
+    "artsbir_mha_fwd_lse_pmax": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "artsbir_quantize_fp8_pmax": [_c_int, _vp, _c_ll, _vp, _c_int, _vp, _vp, _vp],
     "artsbir_layernorm_bwd_sums": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp,
                                    _vp],
     "artsbir_quickgelu_bwd_sum": [_c_int, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
@@ -118,6 +122,8 @@ SIGNATURES = {
     "artsbir_vit_patchify": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_quantize_fp8": [_c_int, _vp, _c_ll, _vp, _vp, _vp],
     "artsbir_gemm_nt_fp8": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
+    "artsbir_gemm_nt_fp8_ex": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _c_int,
+                               _vp],
     "artsbir_vit_tokens": [_c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_vit_tokens_bwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_bn_finalize_seg": [_vp, _c_int, _c_ll, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float,

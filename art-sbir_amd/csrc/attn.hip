@@ -127,7 +127,7 @@ __device__ __forceinline__ void at_store_t(bf16* dst, const f32x16& c0, const f3
 template <bool MASK>
 __global__ void __launch_bounds__(512) attn_fwd_kernel(const bf16* __restrict__ qkv, int L, int N, int heads,
                                                        const float* __restrict__ mask, bf16* __restrict__ out,
-                                                       float* __restrict__ lse) {
+                                                       float* __restrict__ lse, unsigned* __restrict__ pmax) {
   __shared__ __attribute__((aligned(16))) char smem[2 * AT_IMG];
   char* kimg = smem;
   char* vimg = smem + AT_IMG;
@@ -184,9 +184,27 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(const bf16* __restrict__ 
     o1 = at_mfma(at_trfrag(vimg, 32 * kb, 32, lane), pf0, o1);
     o1 = at_mfma(at_trfrag(vimg, 32 * kb + 16, 32, lane), pf1, o1);
   }
+  float am = 0.f;
   if (q < L) {
     at_store_t(out + ((long long)q * N + n) * E + h * 64, o0, o1, 1.f / l, hh);
     if (lse && hh == 0) lse[((long long)q * N + n) * heads + h] = m + __logf(l);
+    if (pmax) {
+      const float il = 1.f / l;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) am = fmaxf(am, fmaxf(fabsf((float)(bf16)(o0[i] * il)), fabsf((float)(bf16)(o1[i] * il))));
+    }
+  }
+  if (pmax) {  // fused fp8 amax of the output (see vit.hip vt_block_amax)
+    __shared__ float red_amax[8];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+    if (lane == 0) red_amax[w] = am;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float b = 0.f;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) b = fmaxf(b, red_amax[i]);
+      atomicMax(pmax + (blockIdx.x & 4095), __float_as_uint(b));
+    }
   }
 }
 
@@ -330,16 +348,17 @@ __global__ void __launch_bounds__(512) attn_bwd_kv_kernel(const bf16* __restrict
 
 // launchers (vit.hip's entry points route bf16 here): false if not applicable
 bool attn_fwd_mfma(const bf16* qkv, int L, int N, int heads, const float* mask, bf16* out, float* lse,
-                   hipStream_t st) {
+                   unsigned* pmax, hipStream_t st) {
   if (L < 1 || L > 32 * AT_MAXB || N < 1 || heads < 1) return false;
   const long long grid = (long long)N * heads;
   if (grid > 0x7fffffffLL) return false;
   const int nthr = ((L + 31) / 32) * 64;
   if (mask)
-    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, L, N, heads, mask, out, lse);
+    hipLaunchKernelGGL(attn_fwd_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, L, N, heads, mask, out, lse,
+                       pmax);
   else
     hipLaunchKernelGGL(attn_fwd_kernel<false>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, L, N, heads, mask, out,
-                       lse);
+                       lse, pmax);
   return true;
 }
 

@@ -134,7 +134,8 @@ __global__ void __launch_bounds__(256) gemm_fp8_kernel(int M, int N, int K, cons
                                                        const unsigned char* __restrict__ B,
                                                        const float* __restrict__ sa, const float* __restrict__ sb,
                                                        const float* __restrict__ bias, T* __restrict__ C,
-                                                       int accumulate) {
+                                                       int accumulate, const bf16* __restrict__ res,
+                                                       bf16* __restrict__ out2, int skip_c) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][128 * 128];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tiles_n = (N + 127) / 128;
@@ -210,7 +211,9 @@ __global__ void __launch_bounds__(256) gemm_fp8_kernel(int M, int N, int K, cons
         float v = acc[i][j][r] * s + bn;
         T* p = C + (long long)m * N + n;
         if (accumulate) v += to_f(*p);
-        *p = from_f<T>(v);
+        if (res) v += (float)res[(long long)m * N + n];
+        if (!skip_c) *p = from_f<T>(v);
+        if (out2) out2[(long long)m * N + n] = (bf16)v;
       }
     }
 }
@@ -258,7 +261,8 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
                                                           const unsigned char* __restrict__ B,
                                                           const float* __restrict__ sa, const float* __restrict__ sb,
                                                           const float* __restrict__ bias, T* __restrict__ C,
-                                                          int accumulate) {
+                                                          int accumulate, const bf16* __restrict__ res,
+                                                          bf16* __restrict__ out2, int skip_c) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][256 * 128];  // [stage][A | B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -348,6 +352,8 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
       float v[4] = {v4.x * s + bn[0], v4.y * s + bn[1], v4.z * s + bn[2], v4.w * s + bn[3]};
       if (m < M) {
         T* p = C + (long long)m * N + n;
+        const long long ro = (long long)m * N + n;
+        typedef __attribute__((ext_vector_type(4))) bf16 bf16x4;
         if (n + 3 < N && (N & 3) == 0) {
           if (accumulate) {
             if constexpr (sizeof(T) == 4) {
@@ -358,18 +364,37 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
               for (int e = 0; e < 4; ++e) v[e] += to_f(p[e]);
             }
           }
-          if constexpr (sizeof(T) == 4) {
-            *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-          } else {
-            __attribute__((ext_vector_type(4))) bf16 o;
+          if (res) {  // bf16 residual input (the block's x)
+            const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + ro);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+          }
+          if (!skip_c) {
+            if constexpr (sizeof(T) == 4) {
+              *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+              bf16x4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+              *reinterpret_cast<bf16x4*>(p) = o;
+            }
+          }
+          if (out2) {  // a bf16 copy of the result (the next LayerNorm's input / the block output)
+            bf16x4 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-            *reinterpret_cast<decltype(o)*>(p) = o;
+            *reinterpret_cast<bf16x4*>(out2 + ro) = o;
           }
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            if (n + e < N) p[e] = from_f<T>(accumulate ? v[e] + to_f(p[e]) : v[e]);
+            if (n + e < N) {
+              float w = v[e];
+              if (accumulate) w += to_f(p[e]);
+              if (res) w += (float)res[ro + e];
+              if (!skip_c) p[e] = from_f<T>(w);
+              if (out2) out2[ro + e] = (bf16)w;
+            }
         }
       }
     }
@@ -397,12 +422,60 @@ extern "C" int artsbir_quantize_fp8(int dtype, const void* x, long long n, unsig
   return 0;
 }
 
+// the quantiser of a tensor whose producer already folded max |x| into 4096
+// partials (artsbir_layernorm_fwd_pmax, artsbir_quickgelu_pmax,
+// artsbir_mha_fwd_lse_pmax): reduce them, then the quantisation pass only
+__global__ void __launch_bounds__(1024) fp8_pmax_reduce_kernel(const unsigned* __restrict__ pmax, int n,
+                                                              unsigned* __restrict__ amax_bits) {
+  unsigned m = 0u;
+  for (int i = threadIdx.x; i < n; i += 1024) m = max(m, pmax[i]);
+  __shared__ unsigned red[16];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned b = 0u;
+    for (int i = 0; i < 16; ++i) b = max(b, red[i]);
+    *amax_bits = b;
+  }
+}
+
+extern "C" int artsbir_quantize_fp8_pmax(int dtype, const void* x, long long n, const unsigned* pmax, int npmax,
+                                         unsigned char* q, float* scale, void* stream) {
+  if (n <= 0 || !x || !q || !scale || !pmax || npmax <= 0) { set_error("quantize_fp8_pmax: bad arguments"); return -1; }
+  hipStream_t st = (hipStream_t)stream;
+  unsigned* bits = reinterpret_cast<unsigned*>(scale);
+  hipLaunchKernelGGL(fp8_pmax_reduce_kernel, dim3(1), dim3(1024), 0, st, pmax, npmax, bits);
+  long long g = (n + 2047) / 2048;
+  const unsigned grid = (unsigned)(g > 2048 ? 2048 : g < 1 ? 1 : g);
+  FP8_DISPATCH(dtype, hipLaunchKernelGGL(fp8_quant_kernel<T>, dim3(grid), dim3(256), 0, st, (const T*)x, n, bits, q));
+  hipLaunchKernelGGL(fp8_scale_kernel, dim3(1), dim3(1), 0, st, bits);
+  ARTSBIR_CHECK_LAUNCH("quantize_fp8_pmax");
+  return 0;
+}
+
+extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* a, const unsigned char* b,
+                                      const float* sa, const float* sb, const float* bias, void* c, int out_dtype,
+                                      int accumulate, const void* res, void* out2, int skip_c, void* stream);
+
 extern "C" int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, const unsigned char* b,
                                    const float* sa, const float* sb, const float* bias, void* c, int out_dtype,
                                    int accumulate, void* stream) {
+  return artsbir_gemm_nt_fp8_ex(M, N, K, a, b, sa, sb, bias, c, out_dtype, accumulate, nullptr, nullptr, 0, stream);
+}
+
+// the same with a fused residual input (bf16 res[M][N] added), a second bf16
+// output out2 (a rounded copy of the result) and skip_c (C only read, for
+// accumulate, not written): the block's residual adds and casts of
+// models.py:412-417 in the projection epilogues
+extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* a, const unsigned char* b,
+                                      const float* sa, const float* sb, const float* bias, void* c, int out_dtype,
+                                      int accumulate, const void* res, void* out2, int skip_c, void* stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 128 != 0 || K <= 0) { set_error("gemm_nt_fp8: K=%d must be a positive multiple of 128", K); return -1; }
-  if (!a || !b || !sa || !sb || !c) { set_error("gemm_nt_fp8: bad arguments"); return -1; }
+  if (!a || !b || !sa || !sb || (!c && (!skip_c || accumulate))) { set_error("gemm_nt_fp8: bad arguments"); return -1; }
+  if (skip_c && !out2) { set_error("gemm_nt_fp8: skip_c without a second output"); return -1; }
   const long long tiles = (long long)((M + 127) / 128) * ((N + 127) / 128);
   if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8: too many tiles"); return -1; }
   hipStream_t st = (hipStream_t)stream;
@@ -414,10 +487,12 @@ extern "C" int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, 
       return -1;
     }
     FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_v2_kernel<T>, dim3((unsigned)t2), dim3(512), 0, st, M, N, K,
-                                             a, b, sa, sb, bias, (T*)c, accumulate));
+                                             a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res, (bf16*)out2,
+                                             skip_c));
   } else {
     FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K,
-                                             a, b, sa, sb, bias, (T*)c, accumulate));
+                                             a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res, (bf16*)out2,
+                                             skip_c));
   }
   ARTSBIR_CHECK_LAUNCH("gemm_nt_fp8");
   return 0;

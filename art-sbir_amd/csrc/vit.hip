@@ -41,14 +41,36 @@ __device__ __forceinline__ void vt_store8(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
 }
 
+// fp8 amax of a producer's output, fused: each block folds max |y| of what it
+// wrote into pmax[blockIdx.x % ARTSBIR_PMAX] (zeroed by the caller; unsigned
+// order of non-negative floats = float order), so the quantiser reduces 4096
+// partials instead of re-reading the tensor (artsbir_quantize_fp8_pmax)
+#define ARTSBIR_PMAX 4096
+__device__ __forceinline__ void vt_block_amax(float m, unsigned* pmax) {
+  __shared__ float red_amax[16];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) red_amax[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float b = 0.f;
+    for (int i = 0; i < nw; ++i) b = fmaxf(b, red_amax[i]);
+    atomicMax(pmax + (blockIdx.x & (ARTSBIR_PMAX - 1)), __float_as_uint(b));
+  }
+}
+
 // LayerNorm forward with 8-column chunks per lane (C % 8 == 0; chunk lane + 64 u)
 template <typename T, int NCH>
 __global__ void __launch_bounds__(256) layernorm_v_kernel(const T* __restrict__ x, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, long long rows, int C,
-                                                          float eps, T* __restrict__ y) {
+                                                          float eps, T* __restrict__ y, unsigned* __restrict__ pmax) {
   const int lane = threadIdx.x & 63;
   const long long row = blockIdx.x * 4LL + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  if (row >= rows) {
+    if (pmax) vt_block_amax(0.f, pmax);  // every wave reaches the block's barrier
+    return;
+  }
   const int nch = C >> 3;
   const T* xr = x + row * C;
   float v[NCH][8];
@@ -72,6 +94,7 @@ __global__ void __launch_bounds__(256) layernorm_v_kernel(const T* __restrict__ 
       for (int e = 0; e < 8; ++e) q += (v[u][e] - mean) * (v[u][e] - mean);
   const float istd = rsqrtf(warp_sum(q) / (float)C + eps);
   T* yr = y + row * C;
+  float am = 0.f;
 #pragma unroll
   for (int u = 0; u < NCH; ++u) {
     const int ch = lane + 64 * u;
@@ -82,8 +105,11 @@ __global__ void __launch_bounds__(256) layernorm_v_kernel(const T* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 8; ++e) o[e] = (v[u][e] - mean) * istd * g[e] + b[e];
       vt_store8(yr + ch * 8, o);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf((float)(T)o[e]));  // the stored (rounded) value
     }
   }
+  if (pmax) vt_block_amax(am, pmax);
 }
 
 // LayerNorm backward with 8-column chunks per lane; each block's 4 waves reduce
@@ -242,20 +268,28 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const T* __restrict__ x,
 
 // QuickGELU (models.py:391-393): x * sigmoid(1.702 x)
 template <typename T>
-__global__ void quickgelu_kernel(const T* __restrict__ x, long long n, T* __restrict__ y) {
+__global__ void quickgelu_kernel(const T* __restrict__ x, long long n, T* __restrict__ y,
+                                 unsigned* __restrict__ pmax) {
   const long long n8 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) ? 0 : n / 8;
+  float am = 0.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
     float v[8];
     vt_load8(x + i * 8, v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = v[e] / (1.f + __expf(-1.702f * v[e]));
+    for (int e = 0; e < 8; ++e) {
+      v[e] = v[e] / (1.f + __expf(-1.702f * v[e]));
+      am = fmaxf(am, fabsf((float)(T)v[e]));
+    }
     vt_store8(y + i * 8, v);
   }
   for (long long i = n8 * 8 + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
     const float v = to_f(x[i]);
-    y[i] = from_f<T>(v / (1.f + __expf(-1.702f * v)));
+    const T o = from_f<T>(v / (1.f + __expf(-1.702f * v)));
+    y[i] = o;
+    am = fmaxf(am, fabsf(to_f(o)));
   }
+  if (pmax) vt_block_amax(am, pmax);
 }
 
 // softmax(q k^T / sqrt(64) + mask) v for one (query position, batch, head)
@@ -629,7 +663,7 @@ __global__ void vit_tokens_bwd_kernel(const T* __restrict__ dtok, int B, int P, 
 
 // MFMA attention for the bf16 mode (attn.hip)
 bool attn_fwd_mfma(const bf16* qkv, int L, int N, int heads, const float* mask, bf16* out, float* lse,
-                   hipStream_t st);
+                   unsigned* pmax, hipStream_t st);
 bool attn_bwd_mfma(const bf16* qkv, const bf16* o, const bf16* dout, const float* lse, int L, int N, int heads,
                    const float* mask, bf16* dqkv, float* dscratch, hipStream_t st);
 
@@ -642,31 +676,49 @@ static inline unsigned vit_grid(long long n) {
 
 using namespace artsbir;
 
-extern "C" int artsbir_layernorm_fwd(int dtype, const void* x, const float* gamma, const float* beta, long long rows,
-                                     int C, float eps, void* y, void* stream) {
+static int layernorm_fwd_impl(int dtype, const void* x, const float* gamma, const float* beta, long long rows, int C,
+                              float eps, void* y, unsigned* pmax, void* stream) {
   if (rows <= 0) return 0;
   const unsigned grid = (unsigned)((rows + 3) / 4);
   const bool vec = C % 8 == 0 && C <= 1024 && !((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y) |
                                                   reinterpret_cast<uintptr_t>(gamma) | reinterpret_cast<uintptr_t>(beta)) & 15);
   if (vec && C <= 512)
     VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_v_kernel<T, 1>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y));
+                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y, pmax));
   else if (vec)
     VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_v_kernel<T, 2>), dim3(grid), dim3(256), 0, (hipStream_t)stream,
-                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y));
-  else
+                                         (const T*)x, gamma, beta, rows, C, eps, (T*)y, pmax));
+  else if (pmax) {
+    set_error("layernorm_fwd: the fused amax needs C %% 8 == 0 (<= 1024) and 16-B aligned rows");
+    return -1;
+  } else
     VIT_DISPATCH(dtype, hipLaunchKernelGGL(layernorm_kernel<T>, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                                          (const T*)x, gamma, beta, rows, C, eps, (T*)y));
   ARTSBIR_CHECK_LAUNCH("layernorm_fwd");
   return 0;
 }
 
-extern "C" int artsbir_quickgelu(int dtype, const void* x, long long n, void* y, void* stream) {
+extern "C" int artsbir_layernorm_fwd(int dtype, const void* x, const float* gamma, const float* beta, long long rows,
+                                     int C, float eps, void* y, void* stream) {
+  return layernorm_fwd_impl(dtype, x, gamma, beta, rows, C, eps, y, nullptr, stream);
+}
+
+extern "C" int artsbir_layernorm_fwd_pmax(int dtype, const void* x, const float* gamma, const float* beta,
+                                          long long rows, int C, float eps, void* y, unsigned* pmax, void* stream) {
+  if (!pmax) { set_error("layernorm_fwd_pmax: pmax missing"); return -1; }
+  return layernorm_fwd_impl(dtype, x, gamma, beta, rows, C, eps, y, pmax, stream);
+}
+
+extern "C" int artsbir_quickgelu_pmax(int dtype, const void* x, long long n, void* y, unsigned* pmax, void* stream) {
   if (n <= 0) return 0;
-  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_kernel<T>, dim3(vit_grid((n + 7) / 8)), dim3(256), 0, (hipStream_t)stream,
-                                       (const T*)x, n, (T*)y));
+  VIT_DISPATCH(dtype, hipLaunchKernelGGL(quickgelu_kernel<T>, dim3(vit_grid((n + 7) / 8)), dim3(256), 0,
+                                       (hipStream_t)stream, (const T*)x, n, (T*)y, pmax));
   ARTSBIR_CHECK_LAUNCH("quickgelu");
   return 0;
+}
+
+extern "C" int artsbir_quickgelu(int dtype, const void* x, long long n, void* y, void* stream) {
+  return artsbir_quickgelu_pmax(dtype, x, n, y, nullptr, stream);
 }
 
 extern "C" int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int heads, const float* mask,
@@ -677,12 +729,26 @@ extern "C" int artsbir_mha_fwd(int dtype, const void* qkv, int L, int N, int hea
   return artsbir_mha_fwd_lse(dtype, qkv, L, N, heads, mask, out, nullptr, stream);
 }
 
+static int mha_fwd_impl(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out, float* lse,
+                        unsigned* pmax, void* stream);
+
 extern "C" int artsbir_mha_fwd_lse(int dtype, const void* qkv, int L, int N, int heads, const float* mask,
                                    void* out, float* lse, void* stream) {
+  return mha_fwd_impl(dtype, qkv, L, N, heads, mask, out, lse, nullptr, stream);
+}
+
+extern "C" int artsbir_mha_fwd_lse_pmax(int dtype, const void* qkv, int L, int N, int heads, const float* mask,
+                                        void* out, float* lse, unsigned* pmax, void* stream) {
+  if (dtype != ARTSBIR_DT_BF16 || !pmax) { set_error("mha_fwd_lse_pmax: bf16 and a pmax buffer"); return -1; }
+  return mha_fwd_impl(dtype, qkv, L, N, heads, mask, out, lse, pmax, stream);
+}
+
+static int mha_fwd_impl(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out, float* lse,
+                        unsigned* pmax, void* stream) {
   if (L < 1 || L > 256) { set_error("mha_fwd: sequence length %d outside [1, 256]", L); return -1; }
   if (heads < 1 || N < 1) { set_error("mha_fwd: bad batch %d / heads %d", N, heads); return -1; }
   if (dtype == ARTSBIR_DT_BF16) {  // MFMA path (attn.hip)
-    if (!attn_fwd_mfma((const bf16*)qkv, L, N, heads, mask, (bf16*)out, lse, (hipStream_t)stream)) {
+    if (!attn_fwd_mfma((const bf16*)qkv, L, N, heads, mask, (bf16*)out, lse, pmax, (hipStream_t)stream)) {
       set_error("mha_fwd: batch %d x heads %d too large", N, heads);
       return -1;
     }

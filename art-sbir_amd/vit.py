@@ -96,10 +96,23 @@ def _colsum(x: torch.Tensor, out: torch.Tensor):
     call("artsbir_colsum", _dt(x), x.data_ptr(), x.shape[0], x.shape[1], x.shape[1], out.data_ptr(), _st())
 
 
-def _ln(x2: torch.Tensor, w, b, eps) -> torch.Tensor:
+PMAX = 4096  # partial maxima a fused-amax producer folds into (csrc/vit.hip vt_block_amax)
+
+
+def _pmax(dev) -> torch.Tensor:
+    return torch.zeros(PMAX, dtype=torch.int32, device=dev)
+
+
+def _ln(x2: torch.Tensor, w, b, eps, pmax=None) -> torch.Tensor:
+    """LayerNorm forward; with pmax (fp8 mode) its max |y| is folded into pmax on the way"""
     y = torch.empty_like(x2)
-    call("artsbir_layernorm_fwd", _dt(x2), x2.data_ptr(), w.detach().float().contiguous().data_ptr(),
-         b.detach().float().contiguous().data_ptr(), x2.shape[0], x2.shape[1], float(eps), y.data_ptr(), _st())
+    wg, bg = w.detach().float().contiguous(), b.detach().float().contiguous()
+    if pmax is None:
+        call("artsbir_layernorm_fwd", _dt(x2), x2.data_ptr(), wg.data_ptr(), bg.data_ptr(), x2.shape[0], x2.shape[1],
+             float(eps), y.data_ptr(), _st())
+    else:
+        call("artsbir_layernorm_fwd_pmax", _dt(x2), x2.data_ptr(), wg.data_ptr(), bg.data_ptr(), x2.shape[0],
+             x2.shape[1], float(eps), y.data_ptr(), pmax.data_ptr(), _st())
     return y
 
 
@@ -124,26 +137,35 @@ def _ln_bwd(x2, w, dy2, eps, dres, dw, db, dres_sum=None, dx_sum=None) -> torch.
 FP8_MAX = 448.0  # e4m3fn
 
 
-def _fp8(x: torch.Tensor):
-    """per-tensor e4m3 quantisation on the device: (uint8 codes, f32 scale tensor [1])"""
+def _fp8(x: torch.Tensor, pmax=None):
+    """per-tensor e4m3 quantisation on the device: (uint8 codes, f32 scale tensor [1]);
+    pmax: the partial maxima x's producer folded (no amax pass over x)"""
     q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
     sc = torch.empty(1, dtype=torch.float32, device=x.device)
-    call("artsbir_quantize_fp8", _dt(x), x.data_ptr(), x.numel(), q.data_ptr(), sc.data_ptr(), _st())
+    if pmax is None:
+        call("artsbir_quantize_fp8", _dt(x), x.data_ptr(), x.numel(), q.data_ptr(), sc.data_ptr(), _st())
+    else:
+        call("artsbir_quantize_fp8_pmax", _dt(x), x.data_ptr(), x.numel(), pmax.data_ptr(), pmax.numel(),
+             q.data_ptr(), sc.data_ptr(), _st())
     return q, sc
 
 
-def _gemm_fp8(a: torch.Tensor, w: torch.Tensor, bias, out=None, out_dtype=torch.bfloat16):
-    """C = A @ W^T (+ bias) with both operands quantised to e4m3 per tensor"""
+def _gemm_fp8(a: torch.Tensor, w: torch.Tensor, bias, out=None, out_dtype=torch.bfloat16, a_pmax=None,
+              accumulate=None, res=None, out2=None, skip_c=False):
+    """C = A @ W^T (+ bias) (+ C if accumulate) (+ res) with both operands quantised
+    to e4m3 per tensor; out2: a bf16 copy of the result; skip_c: C not written"""
     M, K = a.shape
     N = w.shape[0]
-    qa, sa = _fp8(a)
+    qa, sa = _fp8(a, a_pmax)
     qw, sw = _fp8(_as(w, torch.bfloat16))
-    acc = out is not None
+    acc = (out is not None) if accumulate is None else accumulate
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype, device=a.device)
-    call("artsbir_gemm_nt_fp8", M, N, K, qa.data_ptr(), qw.data_ptr(), sa.data_ptr(), sw.data_ptr(),
-         bias.detach().float().contiguous().data_ptr() if bias is not None else None, out.data_ptr(),
-         _hip.dtype_code(out.dtype), 1 if acc else 0, _st())
+    b = bias.detach().float().contiguous() if bias is not None else None
+    call("artsbir_gemm_nt_fp8_ex", M, N, K, qa.data_ptr(), qw.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+         b.data_ptr() if b is not None else None, out.data_ptr(), _hip.dtype_code(out.dtype), 1 if acc else 0,
+         res.data_ptr() if res is not None else None, out2.data_ptr() if out2 is not None else None,
+         1 if skip_c else 0, _st())
     return out
 
 
@@ -219,32 +241,46 @@ class _BlockFunction(torch.autograd.Function):
         M = L * N
         x2 = x.contiguous().view(M, E)
         eps1, eps2 = blk.ln_1.eps, blk.ln_2.eps
-        h = _ln(x2, g1, be1, eps1)
+        # fp8: every quantised activation's producer folds its amax on the way (pm*)
+        pm = [_pmax(x.device) for _ in range(4)] if fp8 else [None] * 4
+        h = _ln(x2, g1, be1, eps1, pm[0])
         bi = b_in.detach().float().contiguous()
-        qkv = _gemm_fp8(h, w_in, b_in, out_dtype=T) if fp8 else _gemm(h, _as(w_in, T), M, 3 * E, E, bias=bi)
+        qkv = (_gemm_fp8(h, w_in, b_in, out_dtype=T, a_pmax=pm[0]) if fp8
+               else _gemm(h, _as(w_in, T), M, 3 * E, E, bias=bi))
         att = torch.empty(M, E, dtype=T, device=x.device)
         lse = torch.empty(M * heads, dtype=torch.float32, device=x.device)
         mask = blk._mask(x)
-        call("artsbir_mha_fwd_lse", _dt(x), qkv.data_ptr(), L, N, heads,
-             mask.data_ptr() if mask is not None else None, att.data_ptr(), lse.data_ptr(), _st())
-        x1 = x2.float().clone() if T == torch.float32 else _cast(x2, torch.float32)  # the f32 residual stream
         if fp8:
-            _gemm_fp8(att, w_o, b_o, out=x1)
+            call("artsbir_mha_fwd_lse_pmax", _dt(x), qkv.data_ptr(), L, N, heads,
+                 mask.data_ptr() if mask is not None else None, att.data_ptr(), lse.data_ptr(), pm[1].data_ptr(),
+                 _st())
         else:
+            call("artsbir_mha_fwd_lse", _dt(x), qkv.data_ptr(), L, N, heads,
+                 mask.data_ptr() if mask is not None else None, att.data_ptr(), lse.data_ptr(), _st())
+        if fp8:  # x1 = x + out_proj(att) (f32 residual stream) and its bf16 copy, in the GEMM epilogue
+            x1 = torch.empty(M, E, dtype=torch.float32, device=x.device)
+            x1t = torch.empty(M, E, dtype=T, device=x.device)
+            _gemm_fp8(att, w_o, b_o, out=x1, a_pmax=pm[1], accumulate=False, res=x2, out2=x1t)
+        else:
+            x1 = x2.float().clone() if T == torch.float32 else _cast(x2, torch.float32)  # the f32 residual stream
             _gemm(att, _as(w_o, T), M, E, E, bias=b_o.detach().float().contiguous(), out=x1)
-        x1t = x1.clone() if T == torch.float32 else _cast(x1, T)  # LN2's input (x1 goes on accumulating)
-        h2 = _ln(x1t, g2, be2, eps2)
+            x1t = x1.clone() if T == torch.float32 else _cast(x1, T)  # LN2's input (x1 goes on accumulating)
+        h2 = _ln(x1t, g2, be2, eps2, pm[2])
         if fp8:
-            f = _gemm_fp8(h2, w_fc, b_fc, out_dtype=T)
+            f = _gemm_fp8(h2, w_fc, b_fc, out_dtype=T, a_pmax=pm[2])
         else:
             f = _gemm(h2, _as(w_fc, T), M, 4 * E, E, bias=b_fc.detach().float().contiguous())
         a = torch.empty_like(f)
-        call("artsbir_quickgelu", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), _st())
         if fp8:
-            _gemm_fp8(a, w_pr, b_pr, out=x1)
+            call("artsbir_quickgelu_pmax", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), pm[3].data_ptr(), _st())
+        else:
+            call("artsbir_quickgelu", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), _st())
+        if fp8:  # y = x1 + c_proj(a), written once in bf16 by the GEMM epilogue
+            y = torch.empty(M, E, dtype=T, device=x.device)
+            _gemm_fp8(a, w_pr, b_pr, out=x1, a_pmax=pm[3], accumulate=True, out2=y, skip_c=True)
         else:
             _gemm(a, _as(w_pr, T), M, E, 4 * E, bias=b_pr.detach().float().contiguous(), out=x1)
-        y = x1 if T == torch.float32 else _cast(x1, T)
+            y = x1 if T == torch.float32 else _cast(x1, T)
         ctx.save_for_backward(x2, h, qkv, att, lse, x1t, h2, f, a)
         ctx.blk, ctx.mask, ctx.dims = blk, mask, (L, N, E, heads)
         return y.view(L, N, E)

@@ -227,6 +227,14 @@ int artsbir_attnpool_bwd(int dtype, const float* q, const void* kv, const float*
  * y[r] = (x[r] - mean) / sqrt(var + eps) * gamma + beta, rows of C. */
 int artsbir_layernorm_fwd(int dtype, const void* x, const float* gamma, const float* beta, long long rows, int C,
                           float eps, void* y, void* stream);
+/* fp8 producers: the same outputs, plus max |y| of the stored values folded
+ * into pmax[4096] (unsigned bits, zeroed by the caller) for
+ * artsbir_quantize_fp8_pmax (the amax pass over the tensor is skipped). */
+int artsbir_layernorm_fwd_pmax(int dtype, const void* x, const float* gamma, const float* beta, long long rows, int C,
+                               float eps, void* y, unsigned* pmax, void* stream);
+int artsbir_quickgelu_pmax(int dtype, const void* x, long long n, void* y, unsigned* pmax, void* stream);
+int artsbir_mha_fwd_lse_pmax(int dtype, const void* qkv, int L, int N, int heads, const float* mask, void* out,
+                             float* lse, unsigned* pmax, void* stream);
 /* QuickGELU (models.py:391-393): y = x * sigmoid(1.702 x), n elements. */
 int artsbir_quickgelu(int dtype, const void* x, long long n, void* y, void* stream);
 /* Self-attention core of nn.MultiheadAttention (models.py:399,409-411), seq-first:
@@ -268,11 +276,22 @@ int artsbir_mha_bwd(int dtype, const void* qkv, const void* out, const void* dou
  * q = e4m3fn(x / s) with s = amax|x| / 448 (1 when x is all zero) written to
  * scale[0] (device f32); n elements of x (dtype f32 / bf16). */
 int artsbir_quantize_fp8(int dtype, const void* x, long long n, unsigned char* q, float* scale, void* stream);
+/* the same for a tensor whose producer folded max |x| into the npmax partials
+ * pmax (an *_pmax entry point above): no amax pass over x. */
+int artsbir_quantize_fp8_pmax(int dtype, const void* x, long long n, const unsigned* pmax, int npmax,
+                              unsigned char* q, float* scale, void* stream);
 /* C[M][N] = sa[0] * sb[0] * sum_k A[m][k] B[n][k] (+ bias[n]) (+ C when accumulate;
  * then out_dtype must be f32) on e4m3fn operands (block-scaled MFMA, unit
  * block scales); K % 128 == 0; sa, sb, bias device f32. */
 int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, const unsigned char* b, const float* sa,
                         const float* sb, const float* bias, void* c, int out_dtype, int accumulate, void* stream);
+/* the same plus a bf16 residual input res[M][N] added in the epilogue, a bf16
+ * copy of the result into out2[M][N] and skip_c (c is read for accumulate but
+ * not written): the ViT block's residual adds and casts (models.py:412-417)
+ * fused into the projections.  res / out2 nullable. */
+int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* a, const unsigned char* b, const float* sa,
+                           const float* sb, const float* bias, void* c, int out_dtype, int accumulate, const void* res,
+                           void* out2, int skip_c, void* stream);
 
 /* ---- ViT-B/16 embedding (CLIP VisionTransformer: conv1 patch16, class
  * token, positional embedding) ------------------------------------------ */

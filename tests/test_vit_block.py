@@ -303,3 +303,76 @@ def test_mfma_attention_bf16(L, N, heads, masked, dev):
             assert dq[:, sl].abs().max().item() < 1e-3, part
         else:
             assert rel(dq[:, sl], ref) < 2e-2, (part, rel(dq[:, sl], ref))
+
+
+@pytest.mark.gpu
+def test_fused_amax_producers_quantise_identically(dev):
+    """the fp8 producers with the fused amax (LayerNorm, QuickGELU, attention) give
+    exactly the codes and scale of the separate amax pass over their outputs"""
+    import _hip
+    import vit
+    g = torch.Generator(device=dev).manual_seed(17)
+    st = _hip.stream()
+    rows, C = 1000, 768
+    x = torch.randn(rows, C, device=dev, generator=g).bfloat16()
+    w = 1 + 0.1 * torch.randn(C, device=dev, generator=g)
+    b = 0.1 * torch.randn(C, device=dev, generator=g)
+    pm = vit._pmax(dev)
+    y = vit._ln(x, w, b, 1e-5, pm)
+    for t, p in ((y, pm),):
+        q0, s0 = vit._fp8(t)
+        q1, s1 = vit._fp8(t, p)
+        assert torch.equal(q0, q1) and torch.equal(s0, s1)
+    f = torch.randn(rows, 3072, device=dev, generator=g).bfloat16() * 3
+    a = torch.empty_like(f)
+    pm = vit._pmax(dev)
+    _hip.call("artsbir_quickgelu_pmax", _hip.DT_BF16, f.data_ptr(), f.numel(), a.data_ptr(), pm.data_ptr(), st)
+    q0, s0 = vit._fp8(a)
+    q1, s1 = vit._fp8(a, pm)
+    assert torch.equal(q0, q1) and torch.equal(s0, s1)
+    L, N, heads = 197, 6, 12
+    E = 64 * heads
+    qkv = torch.randn(L * N, 3 * E, device=dev, generator=g).bfloat16()
+    out = torch.empty(L * N, E, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(L * N * heads, device=dev)
+    pm = vit._pmax(dev)
+    _hip.call("artsbir_mha_fwd_lse_pmax", _hip.DT_BF16, qkv.data_ptr(), L, N, heads, None, out.data_ptr(),
+              lse.data_ptr(), pm.data_ptr(), st)
+    q0, s0 = vit._fp8(out)
+    q1, s1 = vit._fp8(out, pm)
+    assert torch.equal(q0, q1) and torch.equal(s0, s1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(600, 520, 384), (68, 256, 256)])
+def test_fp8_gemm_residual_and_second_output(M, N, K, dev):
+    """artsbir_gemm_nt_fp8_ex: bf16 residual input, bf16 copy of the result,
+    C read but not written (skip_c) — the ViT block's fused residual adds"""
+    import _hip
+    import vit
+    g = torch.Generator(device=dev).manual_seed(21)
+    a = torch.randn(M, K, device=dev, generator=g)
+    b = torch.randn(N, K, device=dev, generator=g) * 0.05
+    bias = torch.randn(N, device=dev, generator=g)
+    qa, sa = vit._fp8(a)
+    qb, sb = vit._fp8(b)
+    da = qa.view(torch.float8_e4m3fn).double().cpu() * sa.double().cpu()
+    db = qb.view(torch.float8_e4m3fn).double().cpu() * sb.double().cpu()
+    ref = da @ db.T + bias.double().cpu()
+    res = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    c = torch.empty(M, N, device=dev)
+    out2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    _hip.call("artsbir_gemm_nt_fp8_ex", M, N, K, qa.data_ptr(), qb.data_ptr(), sa.data_ptr(), sb.data_ptr(),
+              bias.data_ptr(), c.data_ptr(), _hip.DT_F32, 0, res.data_ptr(), out2.data_ptr(), 0, _hip.stream())
+    want = ref + res.double().cpu()
+    scale = want.abs().max().item()
+    assert (c.double().cpu() - want).abs().max().item() / scale < 5e-5
+    assert torch.equal(out2.cpu(), c.cpu().bfloat16())
+    # accumulate onto C, skip writing it, only the bf16 copy
+    c0 = c.clone()
+    out3 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    _hip.call("artsbir_gemm_nt_fp8_ex", M, N, K, qa.data_ptr(), qb.data_ptr(), sa.data_ptr(), sb.data_ptr(),
+              bias.data_ptr(), c.data_ptr(), _hip.DT_F32, 1, None, out3.data_ptr(), 1, _hip.stream())
+    assert torch.equal(c, c0)
+    want3 = c0.double().cpu() + ref
+    assert (out3.double().cpu() - want3).abs().max().item() / want3.abs().max().item() < 1e-2
