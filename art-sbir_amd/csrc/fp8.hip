@@ -256,7 +256,67 @@ __device__ __forceinline__ i32x8 f8_frag(const char* img, int row, int kq) {
   return i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
 }
 
+typedef __attribute__((ext_vector_type(4))) unsigned f8_u32x4;
+
+// the epilogue of four adjacent outputs of row m (offset ro, column n):
+// (+ C if accumulate) (+ res) -> C unless skip_c, and a bf16 copy to out2
 template <typename T>
+__device__ __forceinline__ void f8_store_row4(T* __restrict__ C, const bf16* __restrict__ res,
+                                              bf16* __restrict__ out2, long long ro, int n, int N, float v[4],
+                                              int accumulate, int skip_c) {
+  T* p = C + ro;
+  typedef __attribute__((ext_vector_type(4))) bf16 bf16x4;
+  if (n + 3 < N && (N & 3) == 0) {
+    if (accumulate) {
+      if constexpr (sizeof(T) == 4) {
+        const float4 o = *reinterpret_cast<const float4*>(p);
+        v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += to_f(p[e]);
+      }
+    }
+    if (res) {  // bf16 residual input (the block's x)
+      const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + ro);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+    }
+    if (!skip_c) {
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        bf16x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+        *reinterpret_cast<bf16x4*>(p) = o;
+      }
+    }
+    if (out2) {  // a bf16 copy of the result (the next LayerNorm's input / the block output)
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+      *reinterpret_cast<bf16x4*>(out2 + ro) = o;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (n + e < N) {
+        float w = v[e];
+        if (accumulate) w += to_f(p[e]);
+        if (res) w += (float)res[ro + e];
+        if (!skip_c) p[e] = from_f<T>(w);
+        if (out2) out2[ro + e] = (bf16)w;
+      }
+  }
+}
+
+// RD: the epilogue operands read from memory.  0: none; 1: C (accumulate) or
+// res, one of the two, prefetched a pass ahead into registers; 2: any
+// combination, read in place.  One counter (vmcnt) tracks a wave's loads and
+// stores alike, so a load issued after a store waits for that store too: RD 1
+// issues pass p + 1's loads before pass p's stores, and no load waits behind
+// the output traffic.
+template <typename T, int RD>
 __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
                                                           const unsigned char* __restrict__ B,
                                                           const float* __restrict__ sa, const float* __restrict__ sb,
@@ -301,12 +361,12 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's pieces of stage kt landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // and its reads of stage kt-1 retired
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // and its reads of the other stage retired
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-    const char* ai = smem[buf][0];
-    const char* bi = smem[buf][1];
+    const char* ai = &smem[buf][0][0];
+    const char* bi = &smem[buf][1][0];
     i32x8 bfr[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(bi, wn + 16 * j + fr, kq);
@@ -327,12 +387,36 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   float* eb = reinterpret_cast<float*>(&smem[0][0][0]) + wid * 32 * EP;
   const float s = sa[0] * sb[0];
   const int ec = (lane & 15) * 4, er = lane >> 4;  // this lane's 4 columns, row phase
+  const int n = n0 + wn + ec;
+  const bool vec = n + 3 < N && (N & 3) == 0;
   float bn[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int n = n0 + wn + ec + e;
-    bn[e] = (bias && n < N) ? bias[n] : 0.f;
-  }
+  for (int e = 0; e < 4; ++e) bn[e] = (bias && n + e < N) ? bias[n + e] : 0.f;
+  // RD 1: row rr of pass p's operand (C as f32x4 / bf16x4, or res as bf16x4)
+  f8_u32x4 pre[2][8];
+  const bool rd_c = accumulate != 0;
+  auto prefetch = [&](int pass, f8_u32x4* dst) {
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) {
+      const int m = m0 + wm + 32 * pass + 4 * rr + er;
+      const long long ro = (long long)m * N + n;
+      dst[rr] = f8_u32x4{0u, 0u, 0u, 0u};
+      if (m < M && vec) {
+        if (rd_c) {
+          if constexpr (sizeof(T) == 4) {
+            dst[rr] = *reinterpret_cast<const f8_u32x4*>(C + ro);
+          } else {
+            const uint2 t = *reinterpret_cast<const uint2*>(C + ro);
+            dst[rr].x = t.x; dst[rr].y = t.y;
+          }
+        } else {
+          const uint2 t = *reinterpret_cast<const uint2*>(res + ro);
+          dst[rr].x = t.x; dst[rr].y = t.y;
+        }
+      }
+    }
+  };
+  if constexpr (RD == 1) prefetch(0, pre[0]);
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
 #pragma unroll
@@ -343,59 +427,30 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
         for (int r = 0; r < 4; ++r) eb[(16 * ii + 4 * kq + r) * EP + 16 * j + fr] = acc[2 * pass + ii][j][r];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
+    if constexpr (RD == 1) {
+      if (pass + 1 < 4) prefetch(pass + 1, pre[(pass + 1) & 1]);
+      asm volatile("" ::: "memory");  // those loads go out ahead of this pass's stores
+    }
+#pragma unroll
     for (int rr = 0; rr < 8; ++rr) {
       const int lr = 4 * rr + er;
       const int m = m0 + wm + 32 * pass + lr;
-      const int n = n0 + wn + ec;
       const float4 v4 = *reinterpret_cast<const float4*>(eb + lr * EP + ec);
       float v[4] = {v4.x * s + bn[0], v4.y * s + bn[1], v4.z * s + bn[2], v4.w * s + bn[3]};
-      if (m < M) {
-        T* p = C + (long long)m * N + n;
-        const long long ro = (long long)m * N + n;
-        typedef __attribute__((ext_vector_type(4))) bf16 bf16x4;
-        if (n + 3 < N && (N & 3) == 0) {
-          if (accumulate) {
-            if constexpr (sizeof(T) == 4) {
-              const float4 o = *reinterpret_cast<const float4*>(p);
-              v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] += to_f(p[e]);
-            }
-          }
-          if (res) {  // bf16 residual input (the block's x)
-            const bf16x4 r4 = *reinterpret_cast<const bf16x4*>(res + ro);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
-          }
-          if (!skip_c) {
-            if constexpr (sizeof(T) == 4) {
-              *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
-            } else {
-              bf16x4 o;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-              *reinterpret_cast<bf16x4*>(p) = o;
-            }
-          }
-          if (out2) {  // a bf16 copy of the result (the next LayerNorm's input / the block output)
-            bf16x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-            *reinterpret_cast<bf16x4*>(out2 + ro) = o;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (n + e < N) {
-              float w = v[e];
-              if (accumulate) w += to_f(p[e]);
-              if (res) w += (float)res[ro + e];
-              if (!skip_c) p[e] = from_f<T>(w);
-              if (out2) out2[ro + e] = (bf16)w;
-            }
+      if (m >= M) continue;
+      const long long ro = (long long)m * N + n;
+      if (RD == 1 && vec) {
+        const f8_u32x4 t = pre[pass & 1][rr];
+        if (rd_c && sizeof(T) == 4) {
+          v[0] += __uint_as_float(t.x); v[1] += __uint_as_float(t.y);
+          v[2] += __uint_as_float(t.z); v[3] += __uint_as_float(t.w);
+        } else {  // four bf16
+          v[0] += __uint_as_float(t.x << 16); v[1] += __uint_as_float(t.x & 0xffff0000u);
+          v[2] += __uint_as_float(t.y << 16); v[3] += __uint_as_float(t.y & 0xffff0000u);
         }
+        f8_store_row4<T>(C, nullptr, out2, ro, n, N, v, 0, skip_c);
+      } else {
+        f8_store_row4<T>(C, res, out2, ro, n, N, v, accumulate, skip_c);
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -486,9 +541,24 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
       set_error("gemm_nt_fp8: operand larger than 2 GiB");
       return -1;
     }
-    FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_v2_kernel<T>, dim3((unsigned)t2), dim3(512), 0, st, M, N, K,
-                                             a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res, (bf16*)out2,
-                                             skip_c));
+    static const int nostore = [] { const char* e = getenv("ARTSBIR_FP8_NOSTORE"); return e ? atoi(e) : 0; }();
+    if (nostore) {  // timing experiment only: the main loop without the epilogue's memory traffic
+      accumulate = 0; res = nullptr; out2 = nullptr; skip_c = 1;
+    }
+    const int nrd = (accumulate ? 1 : 0) + (res ? 1 : 0);
+    if (nrd == 0) {
+      FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0>), dim3((unsigned)t2), dim3(512), 0, st, M,
+                                               N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                               (bf16*)out2, skip_c));
+    } else if (nrd == 1) {
+      FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1>), dim3((unsigned)t2), dim3(512), 0, st, M,
+                                               N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                               (bf16*)out2, skip_c));
+    } else {
+      FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2>), dim3((unsigned)t2), dim3(512), 0, st, M,
+                                               N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                               (bf16*)out2, skip_c));
+    }
   } else {
     FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K,
                                              a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res, (bf16*)out2,
