@@ -89,6 +89,7 @@ SIGNATURES = {
     "artsbir_conv2d_fwd": [_P, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_conv2d_wgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp, _vp],
     "artsbir_gemm_nt": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_gemm_nt_gate": [_c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _vp, _c_ll, _vp, _vp, _vp],
     "artsbir_gemm_tn": [_c_int, _c_ll, _c_int, _c_int, _vp, _c_ll, _vp, _c_ll, _vp, _vp],
     "artsbir_conv2d_dgrad": [_P, _vp, _vp, _vp, _vp, _c_int, _vp],
     "artsbir_conv2d_fwd_seg": [_P, _vp, _vp, _vp, _c_int, _vp, _vp],

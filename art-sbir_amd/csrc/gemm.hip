@@ -774,7 +774,7 @@ static int run_old(const ConvArgs& a, hipStream_t st) {
 }
 
 static bool run_candidate(int c, const ConvArgs& a, const PgArgs& p, hipStream_t st) {
-  if (c == -2) return run_old<bf16>(a, st) == 0;
+  if (c == -2) return a.res_mode != 3 && run_old<bf16>(a, st) == 0;
   return pgemm_launch_cfg(p, c, st);
 }
 
@@ -863,8 +863,9 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     }
     int choice;
     const char* force = getenv("ARTSBIR_PGEMM_CFG");
-    if (force) {
-      choice = atoi(force);
+    static const char* force_bnb = getenv("ARTSBIR_BNB_CFG");  // experiment: the fused BN-backward dgrads only
+    if (force || (bd && force_bnb)) {
+      choice = atoi(force ? force : force_bnb);
     } else {
       const ConvKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.Ho, a.Wo, a.res_mode,
                         (a.stats ? 1 : 0) | (a.bias ? 2 : 0) | (a.relu ? 4 : 0), a.nseg,
@@ -886,11 +887,12 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
         g_conv_choice[key] = choice;
       }
     }
-    if (choice != -2 && pgemm_launch_cfg(p, choice, st)) {
+    if ((choice != -2 && pgemm_launch_cfg(p, choice, st)) || (bd && force_bnb && pgemm_launch_cfg(p, 0, st))) {
       ARTSBIR_CHECK_LAUNCH("pgemm");
       return 0;
     }
   }
+  if (a.res_mode == 3) { set_error("gemm_nt_gate: no kernel for this shape"); return -1; }
   return run_old<T>(a, st);
 }
 
@@ -1061,6 +1063,30 @@ extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void*
   p.nseg = 1; p.bnb_desc = nullptr; p.bnb_pstride = 0;
   hipStream_t st = (hipStream_t)stream;
   return dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
+}
+
+// C[M][N] = (A[M][K] B[N][K]^T) * quickgelu'(X[M][N]) in bf16, with the column
+// sums of C added into stats ([ARTSBIR_NSLOT][2][N] f32 slots, sum and sum of
+// squares): the ViT MLP backward's c_proj data gradient, QuickGELU backward
+// and c_fc bias gradient (models.py:391-393, 412-417) in one pass
+extern "C" int artsbir_gemm_nt_gate(long long M, int N, int K, const void* a, long long lda, const void* b, void* c,
+                                    long long ldc, const void* x, float* stats, void* stream) {
+  if (K % 8 != 0 || lda % 8 != 0 || N % 8 != 0) { set_error("gemm_nt_gate: K, lda and N must be multiples of 8"); return -1; }
+  if (!a || !b || !c || !x) { set_error("gemm_nt_gate: null operand"); return -1; }
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 0x7fffffffLL) { set_error("gemm_nt_gate: M too large"); return -1; }
+  ConvArgs p;
+  p.x = a; p.sN = lda; p.sH = 0; p.sW = 0;
+  p.x_elems = (M - 1) * lda + K;
+  p.H = 1; p.W = 1; p.C = K;
+  p.R = 1; p.S = 1; p.stride = 1; p.pad = 0; p.Ho = 1; p.Wo = 1;
+  p.in_scale = nullptr; p.in_shift = nullptr; p.in_relu = 0;
+  p.w = b; p.Cout = N; p.K = K; p.M = M;
+  p.y = c; p.ldy = ldc > 0 ? ldc : N;
+  p.out_f32 = 0; p.accumulate = 0; p.bias = nullptr; p.stats = stats;
+  p.res = x; p.res_mode = 3; p.relu = 0;
+  p.nseg = 1; p.bnb_desc = nullptr; p.bnb_pstride = 0;
+  return launch_conv<bf16>(p, (hipStream_t)stream);
 }
 
 template <typename T, int BM, int BN>

@@ -514,6 +514,12 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
   }
 }
 
+// d/dx [x sigmoid(1.702 x)] (models.py:391-393), as vit.hip's quickgelu_bwd
+__device__ __forceinline__ float pg_quickgelu_grad(float x) {
+  const float sg = 1.f / (1.f + __expf(-1.702f * x));
+  return sg + 1.702f * x * sg * (1.f - sg);
+}
+
 // ---- epilogue operands prefetched into registers (PF variants): every lane
 // issues the global loads of its own epilogue operands (residual, y_0, mask
 // bits, y_1 — the same addresses pg_epilogue_k reads) BEFORE the main loop, so
@@ -652,7 +658,10 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j0 + u][r]; v[4 + r] = acc[2 * p + 1][j0 + u][r]; }
-        if (RESK || (BK == 0 && res)) {
+        if (BK == 0 && a.res_mode == 3) {  // gate: the QuickGELU backward at the pre-activation in the res slot
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] *= pg_quickgelu_grad(to_f(rv[u].v[e]));
+        } else if (RESK || (BK == 0 && res)) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rsc * to_f(rv[u].v[e]);
         }
@@ -1835,6 +1844,8 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
   if (act && (a.stats || a.bnb)) return false;
+  // res_mode 3 (gated data gradient, pg_epilogue_k only): the plain pgemm_kernel tiles
+  if (a.res_mode == 3 && (c < 0 || c > 4 || a.bnb || a.R * a.S != 1)) return false;
   if (c == 20) return !act && sconv_launch(a, st);
   if (c == 21) return hconv_launch(a, st);  // bias / ReLU epilogue supported
   if (act && c >= 11 && c <= 13) return false;
@@ -1882,11 +1893,11 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
 
 // static choice (no tuning): streaming kernel for many tiles, else best-scored tile
 int pgemm_default_cfg(const PgArgs& a) {
-  if (sconv_ok(a) && !a.bias && !a.relu) return 20;
+  if (sconv_ok(a) && !a.bias && !a.relu && a.res_mode != 3) return 20;
   bool multi;
   if (!pg_supported(a, multi)) return -1;
   const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
-  if (((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch) >= 4 * 256) return 10;
+  if (((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch) >= 4 * 256 && a.res_mode != 3) return 10;
   int best = -1;
   float best_score = -1.f;
   for (int c = 0; c < 5; ++c) {

@@ -305,11 +305,19 @@ class _BlockFunction(torch.autograd.Function):
         dy2 = dy.contiguous().view(M, E).to(T)
         # mlp: y = x1 + c_proj(gelu(c_fc(ln_2(x1))))
         _wgrad(dy2, a, dw_pr)
-        da = _gemm(dy2, _t(w_pr, T), M, 4 * E, E)
         df = torch.empty_like(f)
-        # QuickGELU backward with the c_fc bias gradient (column sums of df) in the same pass
-        call("artsbir_quickgelu_bwd_sum", _dt(f), f.data_ptr(), da.data_ptr(), M, 4 * E, df.data_ptr(),
-             db_fc.data_ptr(), _st())
+        if T == torch.bfloat16:
+            # c_proj input gradient gated by QuickGELU's derivative in the GEMM epilogue,
+            # the c_fc bias gradient as its column sums (per-slot partials, then summed)
+            slots = torch.zeros(_hip.NSLOT, 2, 4 * E, dtype=torch.float32, device=dev)
+            call("artsbir_gemm_nt_gate", M, 4 * E, E, dy2.data_ptr(), E, _t(w_pr, T).data_ptr(), df.data_ptr(),
+                 4 * E, f.data_ptr(), slots.data_ptr(), _st())
+            call("artsbir_colsum", _hip.DT_F32, slots.data_ptr(), _hip.NSLOT, 8 * E, 4 * E, db_fc.data_ptr(), _st())
+        else:
+            da = _gemm(dy2, _t(w_pr, T), M, 4 * E, E)
+            # QuickGELU backward with the c_fc bias gradient (column sums of df) in the same pass
+            call("artsbir_quickgelu_bwd_sum", _dt(f), f.data_ptr(), da.data_ptr(), M, 4 * E, df.data_ptr(),
+                 db_fc.data_ptr(), _st())
         _wgrad(df, h2, dw_fc)
         dh2 = _gemm(df, _t(w_fc, T), M, E, 4 * E)
         # LayerNorm-2 backward + the residual gradient dy2; its pass also sums the

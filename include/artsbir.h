@@ -74,6 +74,13 @@ int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void* a, long lo
                     const void* b, void* c, long long ldc, int out_f32, int accumulate,
                     const float* bias, float* stats, void* stream);
 
+/* bf16 c[m][n] = (sum_k a[m][k] * b[n][k]) * quickgelu'(x[m][n]); stats[ARTSBIR_NSLOT][2][n]
+ * += column sums of c and of c^2 (f32 atomics).  Replaces, in the ViT MLP backward
+ * (models.py:391-393, 412-417), the c_proj input gradient, QuickGELU.backward and
+ * the c_fc bias gradient: one GEMM pass instead of a GEMM and an elementwise pass. */
+int artsbir_gemm_nt_gate(long long M, int N, int K, const void* a, long long lda, const void* b, void* c,
+                         long long ldc, const void* x, float* stats, void* stream);
+
 /* dw[n][k] += sum_m dy[m][n] * x[m][k]  (f32 atomics) — nn.Linear weight gradient. */
 int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void* dy, long long ldd,
                     const void* x, long long ldx, float* dw, void* stream);

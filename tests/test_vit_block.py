@@ -376,3 +376,27 @@ def test_fp8_gemm_residual_and_second_output(M, N, K, dev):
     assert torch.equal(c, c0)
     want3 = c0.double().cpu() + ref
     assert (out3.double().cpu() - want3).abs().max().item() / want3.abs().max().item() < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(300, 512, 768), (1000, 3072, 768), (4096, 256, 128)])
+def test_gemm_nt_gate_matches_gemm_then_quickgelu_bwd(M, N, K, dev):
+    """artsbir_gemm_nt_gate = (a @ b^T) * quickgelu'(x) (the c_proj input gradient
+    through QuickGELU.backward, models.py:391-393) in bf16, with its column sums
+    (the c_fc bias gradient) in the statistics slots; ragged M"""
+    import _hip
+    g = torch.Generator(device=dev).manual_seed(31)
+    a = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    b = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
+    x = (torch.randn(M, N, device=dev, generator=g) * 2).bfloat16()
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    slots = torch.zeros(_hip.NSLOT, 2, N, device=dev)
+    _hip.call("artsbir_gemm_nt_gate", M, N, K, a.data_ptr(), K, b.data_ptr(), out.data_ptr(), N, x.data_ptr(),
+              slots.data_ptr(), _hip.stream())
+    xd = x.double().cpu()
+    sg = torch.sigmoid(1.702 * xd)
+    ref = (a.double().cpu() @ b.double().cpu().T) * (sg + 1.702 * xd * sg * (1 - sg))
+    err = (out.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-2, err  # bf16 output rounding
+    colsum = slots[:, 0].sum(0).double().cpu()
+    assert ((colsum - ref.sum(0)).norm() / ref.sum(0).norm()).item() < 1e-4
