@@ -400,3 +400,20 @@ def test_gemm_nt_gate_matches_gemm_then_quickgelu_bwd(M, N, K, dev):
     assert err < 1e-2, err  # bf16 output rounding
     colsum = slots[:, 0].sum(0).double().cpu()
     assert ((colsum - ref.sum(0)).norm() / ref.sum(0).norm()).item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_fp8_quantiser_exhaustive_over_bf16(dev):
+    """artsbir_quantize_fp8 on every finite bf16 value below a bound (the bound sets
+    the tensor's amax, hence the scale) = torch's e4m3fn cast of x / (amax / 448),
+    code for code: the fma-corrected reciprocal division and the branch-free
+    rounding of fp8.hip against IEEE division and torch's RNE"""
+    import vit
+    allb = (torch.arange(65536, dtype=torch.int32).to(torch.int16)).view(torch.bfloat16)
+    allb = allb[torch.isfinite(allb)]
+    for bound in [3.0e38, 448.0, 1.0, 0.3, 7.5e-3, 1.0e-20, 6.0e4]:
+        x = allb[allb.float().abs() <= bound].contiguous()
+        q, s = vit._fp8(x.to(dev))
+        amax = x.float().abs().max()
+        want = (x.float() / (amax / 448.0)).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q.cpu(), want), (bound, int((q.cpu() != want).sum()))
