@@ -123,6 +123,7 @@ SIGNATURES = {
     "artsbir_vit_patchify": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_quantize_fp8": [_c_int, _vp, _c_ll, _vp, _vp, _vp],
     "artsbir_gemm_nt_fp8": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
+    "artsbir_gemm_nt_fp8_gelu": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "artsbir_gemm_nt_fp8_ex": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp, _vp, _c_int,
                                _vp],
     "artsbir_vit_tokens": [_c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],

@@ -134,13 +134,24 @@ __global__ void fp8_scale_kernel(unsigned* amax_bits) {  // amax -> the scale s,
 
 __device__ __forceinline__ int fp8_slot(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
+// QuickGELU (models.py:391-393) as vit.hip's quickgelu_kernel computes it
+__device__ __forceinline__ float f8_quickgelu(float x) { return x / (1.f + __expf(-1.702f * x)); }
+
+// a wave's max |x| into the producer partials pmax[blockIdx & 4095] (the
+// fused-amax convention of vit.hip: 4096 slots, reduced by the quantiser)
+__device__ __forceinline__ void f8_amax_flush(float m, unsigned* pmax) {
+  m = fp8_wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(pmax + (blockIdx.x & 4095), __float_as_uint(m));
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) gemm_fp8_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
                                                        const unsigned char* __restrict__ B,
                                                        const float* __restrict__ sa, const float* __restrict__ sb,
                                                        const float* __restrict__ bias, T* __restrict__ C,
                                                        int accumulate, const bf16* __restrict__ res,
-                                                       bf16* __restrict__ out2, int skip_c) {
+                                                       bf16* __restrict__ out2, int skip_c,
+                                                       unsigned* __restrict__ pmax) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][128 * 128];  // [buf][A|B]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tiles_n = (N + 127) / 128;
@@ -202,6 +213,7 @@ __global__ void __launch_bounds__(256) gemm_fp8_kernel(int M, int N, int K, cons
     __syncthreads();
   }
   const float s = sa[0] * sb[0];
+  float am = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -215,12 +227,21 @@ __global__ void __launch_bounds__(256) gemm_fp8_kernel(int M, int N, int K, cons
         if (m >= M) continue;
         float v = acc[i][j][r] * s + bn;
         T* p = C + (long long)m * N + n;
+        if (pmax) {  // c_fc + QuickGELU: C = f, out2 = quickgelu(f), max |out2| into pmax
+          const bf16 f = (bf16)v;
+          *p = from_f<T>(v);
+          const bf16 g = (bf16)f8_quickgelu((float)f);
+          out2[(long long)m * N + n] = g;
+          am = fmaxf(am, fabsf((float)g));
+          continue;
+        }
         if (accumulate) v += to_f(*p);
         if (res) v += (float)res[(long long)m * N + n];
         if (!skip_c) *p = from_f<T>(v);
         if (out2) out2[(long long)m * N + n] = (bf16)v;
       }
     }
+  if (pmax) f8_amax_flush(am, pmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -315,6 +336,36 @@ __device__ __forceinline__ void f8_store_row4(T* __restrict__ C, const bf16* __r
   }
 }
 
+// c_fc + QuickGELU epilogue of four adjacent outputs: C = f (bf16), out2 =
+// quickgelu(f) computed from the stored bf16 f (as the unfused quickgelu_kernel
+// reads it), am = running max |out2|
+template <typename T>
+__device__ __forceinline__ void f8_gelu_row4(T* __restrict__ C, bf16* __restrict__ out2, long long ro, int n, int N,
+                                             const float v[4], float& am) {
+  typedef __attribute__((ext_vector_type(4))) bf16 bf16x4;
+  if (sizeof(T) == 2 && n + 3 < N && (N & 3) == 0) {
+    bf16x4 fo, go;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      fo[e] = (bf16)v[e];
+      go[e] = (bf16)f8_quickgelu((float)fo[e]);
+      am = fmaxf(am, fabsf((float)go[e]));
+    }
+    *reinterpret_cast<bf16x4*>(C + ro) = fo;
+    *reinterpret_cast<bf16x4*>(out2 + ro) = go;
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (n + e >= N) continue;
+    const bf16 f = (bf16)v[e];
+    const bf16 g = (bf16)f8_quickgelu((float)f);
+    C[ro + e] = from_f<T>((float)f);
+    out2[ro + e] = g;
+    am = fmaxf(am, fabsf((float)g));
+  }
+}
+
 // RD: the epilogue operands read from memory.  0: none; 1: C (accumulate) or
 // res, one of the two, prefetched a pass ahead into registers; 2: any
 // combination, read in place.  One counter (vmcnt) tracks a wave's loads and
@@ -327,7 +378,8 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
                                                           const float* __restrict__ sa, const float* __restrict__ sb,
                                                           const float* __restrict__ bias, T* __restrict__ C,
                                                           int accumulate, const bf16* __restrict__ res,
-                                                          bf16* __restrict__ out2, int skip_c) {
+                                                          bf16* __restrict__ out2, int skip_c,
+                                                          unsigned* __restrict__ pmax) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][256 * 128];  // [stage][A | B]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -421,6 +473,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
       }
     }
   };
+  float am = 0.f;
   if constexpr (RD == 1) prefetch(0, pre[0]);
 #pragma unroll
   for (int pass = 0; pass < 4; ++pass) {
@@ -444,7 +497,9 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
       float v[4] = {v4.x * s + bn[0], v4.y * s + bn[1], v4.z * s + bn[2], v4.w * s + bn[3]};
       if (m >= M) continue;
       const long long ro = (long long)m * N + n;
-      if (RD == 1 && vec) {
+      if (RD == 0 && pmax) {  // c_fc + QuickGELU (T = bf16): C = f, out2 = quickgelu(f)
+        f8_gelu_row4<T>(C, out2, ro, n, N, v, am);
+      } else if (RD == 1 && vec) {
         const f8_u32x4 t = pre[pass & 1][rr];
         if (rd_c && sizeof(T) == 4) {
           v[0] += __uint_as_float(t.x); v[1] += __uint_as_float(t.y);
@@ -461,6 +516,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
   }
+  if (RD == 0 && pmax) f8_amax_flush(am, pmax);
 }
 
 }  // namespace artsbir
@@ -554,21 +610,50 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
     if (nrd == 0) {
       FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0>), dim3((unsigned)t2), dim3(512), 0, st, M,
                                                N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                               (bf16*)out2, skip_c));
+                                               (bf16*)out2, skip_c, nullptr));
     } else if (nrd == 1) {
       FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1>), dim3((unsigned)t2), dim3(512), 0, st, M,
                                                N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                               (bf16*)out2, skip_c));
+                                               (bf16*)out2, skip_c, nullptr));
     } else {
       FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2>), dim3((unsigned)t2), dim3(512), 0, st, M,
                                                N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                               (bf16*)out2, skip_c));
+                                               (bf16*)out2, skip_c, nullptr));
     }
   } else {
     FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K,
                                              a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res, (bf16*)out2,
-                                             skip_c));
+                                             skip_c, nullptr));
   }
   ARTSBIR_CHECK_LAUNCH("gemm_nt_fp8");
+  return 0;
+}
+
+// c_fc + QuickGELU of the ViT MLP (models.py:391-393, 412-417) in one fp8 GEMM:
+// c = f = A B^T + bias (bf16, kept for the backward), out2 = quickgelu(f) (bf16,
+// the c_proj input) and max |out2| folded into pmax[4096] for its quantiser
+// (artsbir_quantize_fp8_pmax) — no separate activation pass over f
+extern "C" int artsbir_gemm_nt_fp8_gelu(int M, int N, int K, const unsigned char* a, const unsigned char* b,
+                                        const float* sa, const float* sb, const float* bias, void* c, void* out2,
+                                        unsigned* pmax, void* stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 128 != 0 || K <= 0) { set_error("gemm_nt_fp8_gelu: K=%d must be a positive multiple of 128", K); return -1; }
+  if (!a || !b || !sa || !sb || !c || !out2 || !pmax) { set_error("gemm_nt_fp8_gelu: bad arguments"); return -1; }
+  const long long tiles = (long long)((M + 127) / 128) * ((N + 127) / 128);
+  if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8_gelu: too many tiles"); return -1; }
+  hipStream_t st = (hipStream_t)stream;
+  if (M >= 256 && N >= 256) {
+    const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    if ((long long)M * K > 0x7fffffffLL || (long long)N * K > 0x7fffffffLL) {
+      set_error("gemm_nt_fp8_gelu: operand larger than 2 GiB");
+      return -1;
+    }
+    hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa, sb,
+                       bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
+  } else {
+    hipLaunchKernelGGL(gemm_fp8_kernel<bf16>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K, a, b, sa, sb, bias,
+                       (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
+  }
+  ARTSBIR_CHECK_LAUNCH("gemm_nt_fp8_gelu");
   return 0;
 }

@@ -169,6 +169,21 @@ def _gemm_fp8(a: torch.Tensor, w: torch.Tensor, bias, out=None, out_dtype=torch.
     return out
 
 
+def _gemm_fp8_gelu(a: torch.Tensor, w: torch.Tensor, bias, a_pmax, g_pmax):
+    """f = A @ W^T + bias and g = quickgelu(f), both bf16, from one fp8 GEMM whose
+    epilogue also folds max |g| into g_pmax (g's quantiser then skips the amax pass)"""
+    M, K = a.shape
+    N = w.shape[0]
+    qa, sa = _fp8(a, a_pmax)
+    qw, sw = _fp8(_as(w, torch.bfloat16))
+    f = torch.empty(M, N, dtype=torch.bfloat16, device=a.device)
+    g = torch.empty_like(f)
+    b = bias.detach().float().contiguous() if bias is not None else None
+    call("artsbir_gemm_nt_fp8_gelu", M, N, K, qa.data_ptr(), qw.data_ptr(), sa.data_ptr(), sw.data_ptr(),
+         b.data_ptr() if b is not None else None, f.data_ptr(), g.data_ptr(), g_pmax.data_ptr(), _st())
+    return f, g
+
+
 # ------------------------------------------------------------------ modules
 class _LNFunction(torch.autograd.Function):
     @staticmethod
@@ -266,15 +281,19 @@ class _BlockFunction(torch.autograd.Function):
             _gemm(att, _as(w_o, T), M, E, E, bias=b_o.detach().float().contiguous(), out=x1)
             x1t = x1.clone() if T == torch.float32 else _cast(x1, T)  # LN2's input (x1 goes on accumulating)
         h2 = _ln(x1t, g2, be2, eps2, pm[2])
-        if fp8:
-            f = _gemm_fp8(h2, w_fc, b_fc, out_dtype=T, a_pmax=pm[2])
+        if fp8 and T == torch.bfloat16:  # c_fc and QuickGELU in one GEMM epilogue
+            f, a = _gemm_fp8_gelu(h2, w_fc, b_fc, pm[2], pm[3])
         else:
-            f = _gemm(h2, _as(w_fc, T), M, 4 * E, E, bias=b_fc.detach().float().contiguous())
-        a = torch.empty_like(f)
-        if fp8:
-            call("artsbir_quickgelu_pmax", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), pm[3].data_ptr(), _st())
-        else:
-            call("artsbir_quickgelu", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), _st())
+            if fp8:
+                f = _gemm_fp8(h2, w_fc, b_fc, out_dtype=T, a_pmax=pm[2])
+            else:
+                f = _gemm(h2, _as(w_fc, T), M, 4 * E, E, bias=b_fc.detach().float().contiguous())
+            a = torch.empty_like(f)
+            if fp8:
+                call("artsbir_quickgelu_pmax", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), pm[3].data_ptr(),
+                     _st())
+            else:
+                call("artsbir_quickgelu", _dt(f), f.data_ptr(), f.numel(), a.data_ptr(), _st())
         if fp8:  # y = x1 + c_proj(a), written once in bf16 by the GEMM epilogue
             y = torch.empty(M, E, dtype=T, device=x.device)
             _gemm_fp8(a, w_pr, b_pr, out=x1, a_pmax=pm[3], accumulate=True, out2=y, skip_c=True)

@@ -300,6 +300,14 @@ int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* a, const un
                            const float* sb, const float* bias, void* c, int out_dtype, int accumulate, const void* res,
                            void* out2, int skip_c, void* stream);
 
+/* c = f = a b^T * sa sb + bias (bf16), out2 = quickgelu(f) (bf16, from the stored f),
+ * max |out2| folded into pmax[4096] (atomicMax on the f32 bits) for
+ * artsbir_quantize_fp8_pmax.  Replaces c_fc + QuickGELU of the ViT MLP
+ * (models.py:391-393, 412-417) in the fp8 forward: one pass instead of two. */
+int artsbir_gemm_nt_fp8_gelu(int M, int N, int K, const unsigned char* a, const unsigned char* b,
+                             const float* sa, const float* sb, const float* bias, void* c, void* out2,
+                             unsigned* pmax, void* stream);
+
 /* ---- ViT-B/16 embedding (CLIP VisionTransformer: conv1 patch16, class
  * token, positional embedding) ------------------------------------------ */
 /* img f32 [B][3][R][R] -> rows [B*P][3*patch*patch] in conv-weight order (the

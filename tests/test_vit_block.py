@@ -417,3 +417,29 @@ def test_fp8_quantiser_exhaustive_over_bf16(dev):
         amax = x.float().abs().max()
         want = (x.float() / (amax / 448.0)).to(torch.float8_e4m3fn).view(torch.uint8)
         assert torch.equal(q.cpu(), want), (bound, int((q.cpu() != want).sum()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(600, 520, 384), (68, 256, 256), (1000, 3072, 768)])
+def test_fp8_gemm_gelu_matches_gemm_then_quickgelu(M, N, K, dev):
+    """artsbir_gemm_nt_fp8_gelu = artsbir_gemm_nt_fp8_ex (bf16 f) followed by
+    artsbir_quickgelu_pmax on f, bit for bit: f, quickgelu(f) and the quantiser's
+    scale from the folded maxima"""
+    import vit
+    g = torch.Generator(device=dev).manual_seed(41)
+    a = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    w = torch.randn(N, K, device=dev, generator=g) * 0.05
+    bias = torch.randn(N, device=dev, generator=g)
+    f_ref = vit._gemm_fp8(a, w, bias, out_dtype=torch.bfloat16)
+    g_ref = torch.empty_like(f_ref)
+    pm_ref = vit._pmax(dev)
+    vit.call("artsbir_quickgelu_pmax", vit._dt(f_ref), f_ref.data_ptr(), f_ref.numel(), g_ref.data_ptr(),
+             pm_ref.data_ptr(), vit._st())
+    pm = vit._pmax(dev)
+    f, gg = vit._gemm_fp8_gelu(a, w, bias, None, pm)
+    assert torch.equal(f, f_ref)
+    assert torch.equal(gg, g_ref)
+    assert pm.max().item() == pm_ref.max().item()
+    q1, s1 = vit._fp8(gg, pm)
+    q2, s2 = vit._fp8(g_ref)
+    assert torch.equal(q1, q2) and torch.equal(s1, s2)
