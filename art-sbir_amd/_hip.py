@@ -139,6 +139,7 @@ SIGNATURES = {
     "artsbir_colsum": [_c_int, _vp, _c_ll, _c_ll, _c_ll, _vp, _vp],
     "artsbir_tokens_fwd": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_tokens_bwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp],
+    "artsbir_tokens_bwd_ex": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_attnpool_fwd": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_attnpool_bwd": [_c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp],
     "artsbir_triplet_fwd": [_vp, _vp, _vp, _c_int, _c_int, _c_float, _c_float, _vp, _vp, _vp],

@@ -753,6 +753,29 @@ __global__ void tokens_bwd_kernel(const float* __restrict__ dtok, int B, int P, 
   }
 }
 
+// the same from a compute-dtype dtok whose token-0 row lacks the query
+// projection's share d0 [B][C] f32 (added here): dh[b][p] = dtok[b][1+p] +
+// (dtok[b][0] + d0[b]) / P
+template <typename T>
+__global__ void tokens_bwd_ex_kernel(const T* __restrict__ dtok, const float* __restrict__ d0, int B, int P, int C,
+                                     T* __restrict__ dh) {
+  const int CG = C / 8;
+  const long long n = (long long)B * P * CG;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int cg = (int)(i % CG);
+    const long long bp = i / CG;
+    const long long b = bp / P;
+    const int p = (int)(bp % P);
+    float t0[8], e0[8], d[8];
+    load8<T>(dtok + (b * (P + 1)) * C + cg * 8, t0);
+    loadf8(d0 + b * C + cg * 8, e0);
+    load8<T>(dtok + (b * (P + 1) + p + 1) * C + cg * 8, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] += (t0[e] + e0[e]) / P;
+    store8<T>(dh + bp * C + cg * 8, d);
+  }
+}
+
 }  // namespace artsbir
 
 using namespace artsbir;
@@ -1049,5 +1072,15 @@ extern "C" int artsbir_tokens_bwd(int dtype, const float* dtok, int B, int P, in
   DISPATCH_T(dtype, hipLaunchKernelGGL(tokens_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                        dtok, B, P, C, (T*)dh));
   ARTSBIR_CHECK_LAUNCH("tokens_bwd");
+  return 0;
+}
+
+extern "C" int artsbir_tokens_bwd_ex(int dtype, const void* dtok, const float* d0, int B, int P, int C, void* dh,
+                                     void* stream) {
+  if (C % 8) { set_error("tokens_bwd_ex: C %% 8 != 0"); return -1; }
+  long long n = (long long)B * P * (C / 8);
+  DISPATCH_T(dtype, hipLaunchKernelGGL(tokens_bwd_ex_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                                       (const T*)dtok, d0, B, P, C, (T*)dh));
+  ARTSBIR_CHECK_LAUNCH("tokens_bwd_ex");
   return 0;
 }

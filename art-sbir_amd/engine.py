@@ -605,13 +605,27 @@ class Engine:
         self._gemm_tn(B * Tk, 2 * C, C, dkv, 2 * C, tok, C, grads[ap.k_proj.weight])
         _, wkvT, _ = pk["kv"]
         _, wqT, _ = pk["q"]
-        dtok = torch.empty(B, Tk, C, dtype=torch.float32, device=dev)
-        self._gemm_nt(B * Tk, C, 2 * C, dkv, 2 * C, wkvT, dtok, C, 1, 0, None)
-        self._gemm_nt(B, C, C, dq, C, wqT, dtok, Tk * C, 1, 1, None)
-        call("artsbir_colsum", _hip.DT_F32, ptr(dtok), B, Tk * C, Tk * C, ptr(grads[ap.positional_embedding]), _s())
         Hs, Ws = c["hw"]
         dh = self._empty(B, Hs, Ws, C, device=dev)
-        call("artsbir_tokens_bwd", self.dt, ptr(dtok), B, P, C, ptr(dh), _s())
+        if self.dtype == torch.float32:
+            dtok = torch.empty(B, Tk, C, dtype=torch.float32, device=dev)
+            self._gemm_nt(B * Tk, C, 2 * C, dkv, 2 * C, wkvT, dtok, C, 1, 0, None)
+            self._gemm_nt(B, C, C, dq, C, wqT, dtok, Tk * C, 1, 1, None)
+            call("artsbir_colsum", _hip.DT_F32, ptr(dtok), B, Tk * C, Tk * C, ptr(grads[ap.positional_embedding]),
+                 _s())
+            call("artsbir_tokens_bwd", self.dt, ptr(dtok), B, P, C, ptr(dh), _s())
+        else:
+            # the token gradient of the key/value projections in the compute dtype
+            # (the MFMA conv GEMM); the query projection's share of the mean token
+            # (B rows) in f32 beside it, added where the two are consumed
+            dtok = self._empty(B, Tk, C, device=dev)
+            self._gemm_nt(B * Tk, C, 2 * C, dkv, 2 * C, wkvT, dtok, C, 0, 0, None)
+            d0 = torch.empty(B, C, dtype=torch.float32, device=dev)
+            self._gemm_nt(B, C, C, dq, C, wqT, d0, C, 1, 0, None)
+            pos = grads[ap.positional_embedding]
+            call("artsbir_colsum", self.dt, ptr(dtok), B, Tk * C, Tk * C, ptr(pos), _s())
+            call("artsbir_colsum", _hip.DT_F32, ptr(d0), B, C, C, ptr(pos), _s())
+            call("artsbir_tokens_bwd_ex", self.dt, ptr(dtok), ptr(d0), B, P, C, ptr(dh), _s())
         return dh
 
     def _seg_desc(self, kind, pool, targets, Bs, H, W, C):

@@ -224,6 +224,12 @@ int artsbir_colsum(int dtype, const void* x, long long rows, long long ld, long 
 /* ---- attention pool (models.py:249-272) --------------------------------- */
 int artsbir_tokens_fwd(int dtype, const void* h, const float* pos, int B, int P, int C, void* tok, void* stream);
 int artsbir_tokens_bwd(int dtype, const float* dtok, int B, int P, int C, void* dh, void* stream);
+
+/* the same with dtok in the compute dtype and the query projection's share of
+ * the mean token's gradient d0[B][C] (f32) given apart:
+ * dh[b][p] = dtok[b][1+p] + (dtok[b][0] + d0[b]) / P */
+int artsbir_tokens_bwd_ex(int dtype, const void* dtok, const float* d0, int B, int P, int C, void* dh,
+                          void* stream);
 int artsbir_attnpool_fwd(int dtype, const float* q, const void* kv, int B, int C, int heads, int T,
                          float* p, void* o, void* stream);
 int artsbir_attnpool_bwd(int dtype, const float* q, const void* kv, const float* p, const float* dout,
