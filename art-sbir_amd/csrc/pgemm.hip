@@ -575,7 +575,7 @@ __device__ __forceinline__ void epi_prefetch(const PgArgs& a, EpiRegs<MTC / 2, N
 // global memory in batches of EJB pixel tiles); y_0 and the mask bits of BK 3
 // are always staged, the BN constants always come from the LDS table.
 template <int BK, bool TWO, bool S_RES, bool S_Y1, bool S_MK, int BCH, int MTC, int NTP, int WTPX, int WTCH,
-          bool REG = false, int EJB = 2>
+          bool REG = false, int EJB = 2, bool GLB = false>
 __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
                                               int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg,
                                               const EpiRegs<MTC / 2, NTP>* er = nullptr) {
@@ -599,14 +599,24 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
     // BN constants (LDS table): xhat_t = (y - m_t) * xa_t; ACT mask (y - mm) * ms + mh > 0
     float xa0[8], m0[8], xa1[8], m1[8], mm[8], ms[8], mh[8];
-    if constexpr (BNB) {
+    if constexpr (BNB && GLB) {  // the same rows pg_prm_fill tabulates, straight from the (L2-resident) vectors
+      const long long po = wseg * a.bnb_pstride + chc;
+      loadf8v(a.bnb_istd[0] + po, xa0);
+      loadf8v(a.bnb_mean[0] + po, m0);
+      if constexpr (TWO) { loadf8v(a.bnb_istd[1] + po, xa1); loadf8v(a.bnb_mean[1] + po, m1); }
+      if constexpr (BK == 1) {
+        loadf8v(a.bnb_mbn + po, mm);
+        loadf8v(a.bnb_mbn + 2 * a.Cout + po, ms);
+        loadf8v(a.bnb_mbn + 3 * a.Cout + po, mh);
+      }
+    } else if constexpr (BNB) {
       const float* pp = sg.prm + (int)(wseg - sg.seg0) * PG_PRM_ROWS * BCH + (chc - bch);
       loadf8v(pp, xa0);
       loadf8v(pp + BCH, m0);
       if constexpr (TWO) { loadf8v(pp + 2 * BCH, xa1); loadf8v(pp + 3 * BCH, m1); }
       if constexpr (BK == 1) { loadf8v(pp + 4 * BCH, mm); loadf8v(pp + 5 * BCH, ms); loadf8v(pp + 6 * BCH, mh); }
     }
-    constexpr bool GLOBAL_OPS = !REG && ((RESK && !S_RES) || (TWO && !S_Y1) || (BK == 2 && !S_MK) || BK == 0);
+    constexpr bool GLOBAL_OPS = !REG && (GLB || (RESK && !S_RES) || (TWO && !S_Y1) || (BK == 2 && !S_MK) || BK == 0);
     constexpr int EJ = (GLOBAL_OPS && NTP >= EJB) ? EJB : 1;
 #pragma unroll
     for (int j0 = 0; j0 < NTP; j0 += EJ) {
@@ -641,11 +651,15 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
           }
         }
         if constexpr (BNB) {
-          y0v[u] = stg_read<BCH>(sg.y0, srow, schunk);
+          if constexpr (GLB) y0v[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + pc * a.ldy + chc);
+          else y0v[u] = stg_read<BCH>(sg.y0, srow, schunk);
           if constexpr (BK == 2)
             mkv[u] = S_MK ? stg_read<BCH>(sg.mk, srow, schunk)
                           : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + pc * a.ldy + chc);
-          if constexpr (BK == 3) mbits[u] = sg.bits[srow * (BCH / 8) + schunk];
+          if constexpr (BK == 3) {
+            if constexpr (GLB) mbits[u] = reinterpret_cast<const unsigned char*>(a.bnb_mask)[pc * (a.Cout >> 3) + (chc >> 3)];
+            else mbits[u] = sg.bits[srow * (BCH / 8) + schunk];
+          }
           if constexpr (TWO)
             y1v[u] = S_Y1 ? stg_read<BCH>(sg.y1, srow, schunk)
                           : ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + pc * a.ldy + chc);
@@ -1045,7 +1059,11 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
 // per tile) need to stream at HBM rate.
 // ---------------------------------------------------------------------------
 // FWDS: forward with BN statistics (carried across tiles, pg_epilogue_fwd)
-template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS>
+// BK > 0: the fused BN-backward epilogue specialised at compile time
+// (pg_epilogue_k, kinds as pgemm_kernel's, TWO targets), its operands and BN
+// constants read from global memory in batches of two pixel tiles while the
+// loader waves already stream the next tile's stages
+template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS, int BK = 0, bool TWO = false>
 __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int BPX = 256, NWC = 8, NWL = 4;
   static_assert(WPX * WCH == NWC, "compute waves");
@@ -1225,6 +1243,11 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
     const int slot = (int)(t % ARTSBIR_NSLOT);
     if constexpr (FWDS) {
       pg_epilogue_fwd<BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, ws, wslot);
+    } else if constexpr (BK != 0) {
+      const EpiStage sg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, a.seg_m > 0 ? bpx / a.seg_m : 0};
+      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 2, true>(a, acc, bpx, bch, wpx, wch,
+                                                                                          fr, fq, red, sg);
+      if (sums) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane, bpx, BPX);
     } else {
       pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH, 1>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
       // the flushing wave zeroes red before it reaches the next stage barrier,
@@ -1824,6 +1847,35 @@ static void pstream_launch(int bch, const PgArgs& a, int grid, int ntl, hipStrea
   else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, MULTI, BNB, FWDS>), dim3(grid), dim3(768), 0, st, a, ntl);
 }
 
+template <int BK, bool TWO>
+static void pstream_launch_k(int bch, const PgArgs& a, int grid, int ntl, hipStream_t st) {
+  constexpr bool ONLY64 = TWO || BK == 1;  // 128-channel blocks would spill there
+  if (ONLY64 || bch == 64)
+    hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false, true, false, BK, TWO>), dim3(grid), dim3(768), 0, st, a, ntl);
+  else if constexpr (!ONLY64)
+    hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, false, true, false, BK, TWO>), dim3(grid), dim3(768), 0, st, a,
+                       ntl);
+}
+
+// candidate 14: the persistent streaming kernel with the specialised fused
+// BN-backward epilogue (the kinds pg_launch_bnb takes, channel blocks 64 / 128)
+static bool pstream_bnb_launch(const PgArgs& a, bool multi, hipStream_t st) {
+  if (!a.bnb || multi || a.Cout < 64) return false;
+  if (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) return false;
+  if (a.bnb != 1 && !a.res_mode) return false;
+  const int bch = (a.Cout <= 64 || a.bnb == 1 || a.bnb_nt == 2) ? 64 : 128;  // see pstream_launch_k
+  const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);
+  if (nt > 0x7fffffffLL) return false;
+  const int grid = (int)(nt < 256 ? nt : 256), ntl = (int)nt;
+  set_last_kernel(bch == 64 ? "pstream_kernel<64,bnbk>" : "pstream_kernel<128,bnbk>");
+  if (a.bnb == 1) pstream_launch_k<1, false>(bch, a, grid, ntl, st);
+  else if (a.bnb == 3 && a.bnb_nt == 2) pstream_launch_k<3, true>(bch, a, grid, ntl, st);
+  else if (a.bnb == 3) pstream_launch_k<3, false>(bch, a, grid, ntl, st);
+  else if (a.bnb_nt == 2) pstream_launch_k<2, true>(bch, a, grid, ntl, st);
+  else pstream_launch_k<2, false>(bch, a, grid, ntl, st);
+  return true;
+}
+
 static bool pg_supported(const PgArgs& a, bool& multi) {
   if (a.Cout % 32 != 0 || a.M <= 0) return false;
   if (a.C % 64 == 0) multi = false;
@@ -1852,6 +1904,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   bool multi;
   if (!pg_supported(a, multi)) return false;
   if (c >= 11 && c <= 13) return pg_pf_launch(c, a, multi, st);
+  if (c == 14) return pstream_bnb_launch(a, multi, st);
   if (c == 10) {
     const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
     const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);

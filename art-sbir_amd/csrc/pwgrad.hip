@@ -520,8 +520,18 @@ static void hwgrad_tiles(const PwArgs& a, hipStream_t st) {
   else hwgrad_go<CT, OT, 8, NWC>(a, st);
 }
 
-static bool hwgrad_launch(const PwArgs& a, hipStream_t st) {
+// variant 0: the kernel below per channel class; variant 1 (64-channel tiled
+// shapes only): 4 compute waves of 9 (channel tile, tap) pairs each instead of
+// 8 waves of 4.5 (0.72 transposing LDS reads per MFMA instead of 0.9, no
+// repeated pairs; 144 accumulator registers per lane)
+static bool hwgrad_launch(const PwArgs& a, int variant, hipStream_t st) {
   if (!hwgrad_ok(a)) return false;
+  if (variant != 0) {
+    if (variant != 1 || a.C % 64 || a.Cout % 64) return false;
+    set_last_kernel("hwgrad_kernel<64,64,w4>");
+    hwgrad_tiles<64, 64, 4>(a, st);
+    return true;
+  }
   if (a.C == 32 && a.Cout == 32) {
     set_last_kernel("hwgrad_kernel<32,32>");
     hwgrad_tiles<32, 32, 4>(a, st);
@@ -584,13 +594,13 @@ static const int kSplitMinSteps[] = {8, 16, 24, 64};
 constexpr int kNumLevels = 4;
 
 // candidates: kNumPw tile configurations x kNumLevels split levels, then the
-// halo-tiled small-channel kernel
-int pwgrad_num_cfgs() { return kNumPw * kNumLevels + 1; }
+// halo-tiled kernel (two variants, see hwgrad_launch)
+int pwgrad_num_cfgs() { return kNumPw * kNumLevels + 2; }
 
 // candidate c = cfg + kNumPw * level of the pipelined wgrad; false (nothing
 // launched) if not applicable
 bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
-  if (cand == kNumPw * kNumLevels) return hwgrad_launch(a, st);
+  if (cand >= kNumPw * kNumLevels) return cand < pwgrad_num_cfgs() && hwgrad_launch(a, cand - kNumPw * kNumLevels, st);
   if (cand < 0 || cand >= kNumPw * kNumLevels) return false;
   const int c = cand % kNumPw, level = cand / kNumPw;
   if (a.Cout % 8 || a.K % 8 || a.M <= 0) return false;

@@ -19,6 +19,8 @@ SHAPES = [  # N, H, W, C (dx channels), Co (dy channels), R, kind, res_mode
     (1152, 14, 14, 1024, 256, 1, 3, 1),
     (1152, 28, 28, 512, 128, 1, 3, 1),
     (1152, 56, 56, 64, 256, 1, 1, 0),
+    (1152, 56, 56, 256, 64, 1, 3, 1),
+    (1152, 56, 56, 256, 128, 1, 3, 1),
 ]
 
 
@@ -64,6 +66,7 @@ def main():
         desc.istd[0] = prm[0, 1].data_ptr()
         desc.slots[0] = slots.data_ptr()
         fl = 2.0 * N * H * W * C * Co * R * R
+        nb = 2.0 * N * H * W * (Co + 2 * C + (C if rm else 0)) + (N * H * W * C / 8 if kind == 3 else 0)
         print(f"== dx {N}x{H}x{W}x{C} <- dy {Co} {R}x{R} kind{kind} res{rm}: {fl / 1e9:.0f} GFLOP", flush=True)
         for cfg in os.environ.get("CFGS", "0,1,2,3,10,21").split(","):
             os.environ["ARTSBIR_PGEMM_CFG"] = cfg
@@ -77,7 +80,7 @@ def main():
                 print(f"  cfg {cfg}: n/a ({str(e)[:60]})")
                 continue
             print(f"  cfg {cfg:>2} {kname:28s} plain {t_plain:8.1f} us ({fl / t_plain / 1e6:6.1f} TF)  "
-                  f"bnb {t_bnb:8.1f} us ({fl / t_bnb / 1e6:6.1f} TF)", flush=True)
+                  f"bnb {t_bnb:8.1f} us ({fl / t_bnb / 1e6:6.1f} TF, {nb / t_bnb / 1e3:6.0f} GB/s)", flush=True)
         os.environ.pop("ARTSBIR_PGEMM_CFG", None)
 
 

@@ -64,7 +64,7 @@ def sweep(label, fl, run, ncand):
 def main():
     dev = torch.device("cuda:0")
     st = _hip.stream()
-    ncand = 37  # pwgrad tile configs x split levels + the halo kernel (gemm.hip tune_wgrad)
+    ncand = 38  # pwgrad tile configs x split levels + the two halo kernel variants (gemm.hip tune_wgrad)
     which = os.environ.get("WHICH", "conv,dense")
     if "conv" in which:
         for (H, W, C, Co, R, s) in CONV:
