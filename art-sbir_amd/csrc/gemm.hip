@@ -1177,7 +1177,12 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   (void)hipDeviceSynchronize();  // quiet device (see tune_conv)
   int best = -1;
   float best_ms = 1e30f;
+  // ARTSBIR_WGRAD_MINLEVEL=L: only split levels >= L (fewer workgroups; the
+  // weight gradients share the chip with the data-gradient stream, which the
+  // standalone timing here cannot see)
+  static const int minlevel = getenv("ARTSBIR_WGRAD_MINLEVEL") ? atoi(getenv("ARTSBIR_WGRAD_MINLEVEL")) : 0;
   for (int c = -1; c < pwgrad_num_cfgs(); ++c) {
+    if (c >= 0 && pwgrad_level(c) >= 0 && pwgrad_level(c) < minlevel) continue;
     if (!run_wg_candidate(c, at, st)) continue;
     float ms = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {

@@ -63,6 +63,7 @@ struct PwArgs {
 // false, launching nothing, if it does not apply to the shape
 bool pwgrad_launch(PwArgs a, int c, hipStream_t st);
 int pwgrad_num_cfgs();
+int pwgrad_level(int c);
 
 // Launch candidate `cfg` (0..4: tile shapes of the pipelined kernel, 10: the
 // persistent streaming kernel).  Returns false, launching nothing, when the

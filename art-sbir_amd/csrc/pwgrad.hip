@@ -597,6 +597,9 @@ constexpr int kNumLevels = 4;
 // halo-tiled kernel (two variants, see hwgrad_launch)
 int pwgrad_num_cfgs() { return kNumPw * kNumLevels + 2; }
 
+// split level of candidate c of the pipelined wgrad (-1: the halo kernel)
+int pwgrad_level(int c) { return c >= 0 && c < kNumPw * kNumLevels ? c / kNumPw : -1; }
+
 // candidate c = cfg + kNumPw * level of the pipelined wgrad; false (nothing
 // launched) if not applicable
 bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {

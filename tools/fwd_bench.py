@@ -19,6 +19,9 @@ SHAPES = [  # N, H, W, C, Co, R, stride
     (1152, 7, 7, 512, 2048, 1, 1),
     (1152, 56, 56, 256, 64, 1, 1),
     (1152, 56, 56, 64, 64, 3, 1),
+    (1152, 28, 28, 128, 128, 3, 1),
+    (1152, 14, 14, 256, 256, 3, 1),
+    (1152, 7, 7, 512, 512, 3, 1),
 ]
 
 
@@ -39,7 +42,9 @@ def timeit(fn, reps=5):
 def main():
     dev = torch.device("cuda:0")
     st = _hip.stream()
-    for (N, H, W, C, Co, R, s) in SHAPES:
+    only = os.environ.get("ONLY")  # comma-separated indices into SHAPES
+    shapes = [SHAPES[int(i)] for i in only.split(",")] if only else SHAPES
+    for (N, H, W, C, Co, R, s) in shapes:
         x = torch.randn(N, H, W, C, device=dev).bfloat16()
         w = (torch.randn(Co, R, R, C, device=dev) * 0.05).bfloat16()
         Ho, Wo = H // s, W // s
