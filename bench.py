@@ -31,7 +31,7 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # MI355X dense (MI355X_MICROA
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s measured copy)
 # per-launch HBM bytes of each kernel from the committed rocprofv3 PMC passes
 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/summarize_pmc.py)
-PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r2_pmc_traffic.json"))
+PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r2b_pmc_traffic.json"))
 
 
 def pmc_traffic(kernel):
@@ -117,10 +117,11 @@ def cpu_baseline(batch=32, steps=3, layers=LAYERS, out_dim=OUT_DIM):
                       f"steps x {batch} triplets after 1 warm-up, torch CPU {torch.__version__}"}
 
 
-def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
+def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3, noise=0.5):
     """BASELINE metric, second half: gallery kNN QPS at 1M x 512.
-    Synthetic gallery G ~ N(0,1); query i = G[(i*7919) mod N] + 0.5 N(0,1), so each
-    query has one planted positive.  Timed: knn.knn (or knn_sharded over the
+    Synthetic gallery G ~ N(0,1); query i = G[(i*7919) mod N] + noise * N(0,1), so
+    each query has one planted positive (noise 0.5: the positive is the nearest;
+    noise 3.0: ranks spread, mAP@10 < 1).  Timed: knn.knn (or knn_sharded over the
     ranks: gallery rows split, one all_gather + all_reduce) producing the exact
     top-10 and the rank of the positive for all Q queries; inputs resident in HBM."""
     import knn
@@ -128,7 +129,7 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
     lo, hi = rank * N // world, (rank + 1) * N // world
     gal = torch.randn(N, D, device=dev, generator=g)  # same full gallery on every rank (seeded)
     pos = (torch.arange(Q, device=dev, dtype=torch.int64) * 7919) % N
-    qs = gal[pos] + 0.5 * torch.randn(Q, D, device=dev, generator=torch.Generator(device=dev).manual_seed(8))
+    qs = gal[pos] + noise * torch.randn(Q, D, device=dev, generator=torch.Generator(device=dev).manual_seed(8))
     shard = gal[lo:hi].contiguous()
     del gal
 
@@ -165,7 +166,8 @@ def retrieval_leg(dev, rank, world, N=1_000_000, D=512, Q=10_000, k=10, reps=3):
     map10 = float(torch.where(rk <= k, 1.0 / rk, torch.zeros_like(rk)).mean())
     return {"metric": "gallery kNN QPS @1M x 512 (exact top-10 + rank of positive)", "value": round(Q / el, 1),
             "unit": "queries/s", "ms": round(el * 1e3, 3), "N": N, "D": D, "Q": Q, "k": k, "n_gpus": world,
-            "scaling": "strong", "compute": "bf16 MFMA scan + exact f64 rerank", "map@10": round(map10, 6),
+            "scaling": "strong", "compute": "bf16 MFMA scan + exact f64 rerank", "noise": noise,
+            "map@10": round(map10, 6),
             "mrr": round(float((1.0 / rk).mean()), 6),
             "roofline": {"bound": "mfma", "kernel": scan_kernel, "achieved": round(scan_fl / scan_s / 1e12, 2),
                          "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
@@ -421,16 +423,21 @@ def main():
             # per kernel: algorithmic FLOPs and bytes (declared by the engine per
             # launch) over the HIP-event time of its launches; the dominant kernel
             # (most time) is priced against the roof its arithmetic intensity hits
+            # a[4]: each launch's own roofline time max(bytes / HBM peak, FLOPs /
+            # MFMA peak), summed: a kernel name pools MFMA-bound (3x3) and
+            # HBM-bound (1x1) shapes, whose pooled GB/s or TFLOP/s alone
+            # understates both; sum(roofline time) / sum(time) does not
+            peak_fl = MFMA_PEAK_TFLOPS[args.dtype]
             agg = {}
             for kname, fl, nb, e0, e1, *_ in prof:
-                a = agg.setdefault(kname, [0.0, 0.0, 0, 0.0])
+                a = agg.setdefault(kname, [0.0, 0.0, 0, 0.0, 0.0])
                 a[0] += fl
                 a[1] += e0.elapsed_time(e1) / 1e3
                 a[2] += 1
                 a[3] += nb
+                a[4] += max(nb / (HBM_PEAK_GBS * 1e9), fl / (peak_fl * 1e12))
             dom = max(agg, key=lambda k: agg[k][1])
-            fl, secs, cnt, nb = agg[dom]
-            peak_fl = MFMA_PEAK_TFLOPS[args.dtype]
+            fl, secs, cnt, nb, rt = agg[dom]
             ridge = peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
             if nb > 0 and fl / nb < ridge:
                 achieved = nb / secs / 1e9
@@ -444,9 +451,13 @@ def main():
                          "kernel": dom, "launches": cnt, "avg_launch_us": round(secs / cnt * 1e6, 2),
                          "avg_launch_flops": fl / cnt, "avg_launch_bytes": nb / cnt,
                          "intensity_flop_per_byte": round(fl / nb, 1) if nb else None,
+                         "frac_launch_roofline": round(rt / secs, 4),
+                         "step_launch_roofline": round(sum(v[4] for v in agg.values()) /
+                                                       sum(v[1] for v in agg.values()), 4),
                          "per_kernel": {k: {"launches": v[2], "avg_us": round(v[1] / v[2] * 1e6, 2),
                                             "tflops": round(v[0] / v[1] / 1e12, 1),
-                                            "gbs": round(v[3] / v[1] / 1e9, 1), "share_s": round(v[1], 4)}
+                                            "gbs": round(v[3] / v[1] / 1e9, 1), "share_s": round(v[1], 4),
+                                            "roof_frac": round(v[4] / v[1], 4)}
                                         for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}})
         step_flops = train_flops_per_triplet() * B
         line = {
@@ -471,6 +482,12 @@ def main():
     emb = None if args.no_embed else embed_leg(model, batch, args.dtype, world, args.steps)
     c5 = c5_leg(dev, rank, world, args.c5_batch, max(2, args.steps // 2)) if args.c5 else None
     ret = None if args.no_retrieval else retrieval_leg(dev, rank, world)
+    if ret is not None:
+        # the same workload with queries far from their positives (ranks spread,
+        # more list insertions and rank-band decisions in the scan)
+        hard = retrieval_leg(dev, rank, world, reps=2, noise=3.0)
+        ret["noise3"] = {k: hard[k] for k in ("value", "unit", "ms", "map@10", "mrr")}
+        ret["noise3"]["scan_frac"] = hard["roofline"]["frac"]
     if rank == 0:
         if emb is not None:
             line["embed"] = emb
