@@ -265,11 +265,11 @@ class Engine:
     # ------------------------------------------------------------- primitives
     def _gemm_nt(self, M, N, K, a, lda, b, c, ldc, out_f32, acc, bias):
         call("artsbir_gemm_nt", self.dt, M, N, K, ptr(a), lda, ptr(b), ptr(c), ldc, out_f32, acc, ptr(bias), None,
-             _s(), kernel="auto", flops=2.0 * M * N * K)
+             _s(), kernel="auto", flops=2.0 * M * N * K, tag=f"gemm_nt {M}x{N}x{K} f32{out_f32} acc{acc}")
 
     def _gemm_tn(self, M, N, K, dy, ldd, x, ldx, dw):
         call("artsbir_gemm_tn", self.dt, M, N, K, ptr(dy), ldd, ptr(x), ldx, ptr(dw), _s(),
-             kernel="auto", flops=2.0 * M * N * K)
+             kernel="auto", flops=2.0 * M * N * K, tag=f"gemm_tn {M}x{N}x{K}")
 
     def _conv(self, a: Act, fw, cout, R, S, stride, pad, stats_buf=None):
         B, H, W, C = a.shape
