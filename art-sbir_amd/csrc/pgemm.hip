@@ -822,20 +822,27 @@ __device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&a
 // BK (0 / 1 / 2 / 3, see pg_epilogue_k) and TWO select the fused epilogue.
 // PF: epilogue operands prefetched into registers before the main loop
 // (epi_prefetch) instead of staged through LDS after it
-template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false>
+// KS: k per stage.  64: LDS rows of 128 B (8 chunks, slot = chunk ^ (row & 7),
+// 8 rows per DMA instruction).  32: rows of 64 B (4 chunks, slot = chunk ^
+// ((row >> 2) & 3), 16 rows per DMA instruction) — half the bytes per stage, so
+// the same LDS holds twice the stages and more of them are in flight (C % 64
+// == 0 only)
+template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false, int KS = 64>
 __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   constexpr bool BNB = BK != 0;
   static_assert(!PF || BK != 2, "PF: the bf16 mask operand of kind 2 is not prefetched");
+  static_assert(KS == 64 || (KS == 32 && !MULTI), "32-k stages: uniform taps only");
+  constexpr int ROWB = 2 * KS, RPI = 1024 / ROWB, CPR = ROWB / 16;
   constexpr int NW = WPX * WCH;
-  constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
-  constexpr int IPX = BPX / (8 * NW);
-  constexpr int ICH_TOT = BCH / 8;
+  constexpr int PXB = BPX * ROWB, CHB = BCH * ROWB, STAGE = PXB + CHB;
+  constexpr int IPX = BPX / (RPI * NW);
+  constexpr int ICH_TOT = BCH / RPI;
   constexpr int ICH = (ICH_TOT + NW - 1) / NW;
   constexpr int WTPX = BPX / WPX, WTCH = BCH / WCH;
   constexpr int NTP = WTPX / 16, MTC = WTCH / 16;
   constexpr int LPS_HI = IPX + ICH;                            // loads per stage, waves with ICH weight loads
   constexpr int LPS_LO = IPX + ICH_TOT / NW;                   // ... waves with one fewer
-  static_assert(IPX >= 1 && IPX * 8 * NW == BPX, "pixel loader");
+  static_assert(IPX >= 1 && IPX * RPI * NW == BPX, "pixel loader");
   static_assert(MTC % 2 == 0 && WTCH % 32 == 0, "channel pairs");
   // stage ring | BN statistics accumulator | (BNB) BN constants | (BNB) mask bits
   constexpr int XTRA = BNB ? pg_prm_bytes<BCH>() + BPX * (BCH / 8) : 0;
@@ -864,13 +871,13 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
 
   // ---- loader decode: this lane fills slot (lane & 7) of row (lane >> 3)
   // of each 8-row wave instruction, with k-chunk csrc = slot ^ (row & 7)
-  const int lrow = lane >> 3, lslot = lane & 7;
-  const int csrc = lslot ^ lrow;
+  const int lrow = lane / CPR, lslot = lane % CPR;
+  const int csrc = KS == 64 ? (lslot ^ lrow) : (lslot ^ ((lrow >> 2) & 3));
   int rowoff[IPX];
   unsigned rmask[IPX];
 #pragma unroll
   for (int u = 0; u < IPX; ++u) {
-    const int row = (u * NW + wid) * 8 + lrow;
+    const int row = (u * NW + wid) * RPI + lrow;
     const long long gm = bpx + row;
     const bool valid = gm < a.M;
     const long long gmc = valid ? gm : bpx;
@@ -891,7 +898,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
 #pragma unroll
   for (int u = 0; u < ICH; ++u) {
     const int g = u * NW + wid;
-    const int ch = bch + pg_perm(g * 8 + lrow);
+    const int ch = bch + pg_perm(g * RPI + lrow);
     woff[u] = (g < ICH_TOT && ch < a.Cout) ? (unsigned)(ch * a.K * 2 + csrc * 16) : PG_OOB;
   }
   const bool lps_hi = (ICH - 1) * NW + wid < ICH_TOT;
@@ -906,7 +913,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
       rs = u_r * a.S + u_s;
       tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + u_ci + csrc * 8) * 2;
       kval = true;
-      u_ci += 64;
+      u_ci += KS;
       if (u_ci == a.C) {
         u_ci = 0;
         if (++u_s == a.S) { u_s = 0; ++u_r; }
@@ -925,11 +932,11 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
       const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
       glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
     }
-    const bool wk = kt * 64 + csrc * 8 < a.K;
+    const bool wk = kt * KS + csrc * 8 < a.K;
 #pragma unroll
     for (int u = 0; u < ICH; ++u) {
       if (u * NW + wid < ICH_TOT)
-        glds16(wr, chs + (u * NW + wid) * 1024, (wk && woff[u] != PG_OOB) ? woff[u] + kt * 128 : PG_OOB);
+        glds16(wr, chs + (u * NW + wid) * 1024, (wk && woff[u] != PG_OOB) ? woff[u] + kt * ROWB : PG_OOB);
     }
   };
 
@@ -944,13 +951,13 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     const char* pxs = smem + buf * STAGE;
     const char* chs = pxs + PXB;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int so = ((kk * 4 + fq) ^ (fr & 7)) << 4;
+    for (int kk = 0; kk < KS / 32; ++kk) {
+      const int so = (KS == 64 ? ((kk * 4 + fq) ^ (fr & 7)) : (fq ^ ((fr >> 2) & 3))) << 4;
       uint4 af[MTC], bv[NTP];
 #pragma unroll
-      for (int i = 0; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * 128 + so);
+      for (int i = 0; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * ROWB + so);
 #pragma unroll
-      for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * 128 + so);
+      for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * ROWB + so);
       PG_PRIO_ON();
 #pragma unroll
       for (int i = 0; i < MTC; ++i)
@@ -970,7 +977,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   }
   EpiRegs<MTC / 2, NTP> er;
   if constexpr (PF) epi_prefetch<BK, TWO, MTC, NTP, WTPX, WTCH>(a, er, bpx, bch, wpx, wch, fr, fq);
-  const int nk = (a.K + 63) / 64;
+  const int nk = (a.K + KS - 1) / KS;
 #pragma unroll
   for (int s = 0; s < NSTAGE - 1; ++s)
     if (s < nk) issue(s, s);
@@ -1773,7 +1780,9 @@ static const PgCfg kCfgs[] = {
     {256, 64, 3 * (256 + 64) * 128, 512, 0.85f},    // 2: 256 x 64, 3 stages
     {128, 128, 2 * 256 * 128, 256, 0.80f},          // 3: 128 x 128, 2 stages, 4 waves
     {256, 32, 4 * (256 + 32) * 128, 512, 0.70f},    // 4: 256 x 32, 4 stages
+    {256, 256, 4 * 512 * 64, 512, 0.0f},           // 5: 256 x 256, four 32-k stages (tuned only)
 };
+constexpr int kNumCfg = 6;
 
 template <bool MULTI, int BK, bool TWO>
 static void pg_launch_cfg(int c, const PgArgs& a, long long tiles, hipStream_t st) {
@@ -1783,7 +1792,11 @@ static void pg_launch_cfg(int c, const PgArgs& a, long long tiles, hipStream_t s
     case 1: hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
     case 2: hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
     case 3: hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 2, MULTI, BK, TWO>), g, dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((pgemm_kernel<256, 32, 8, 1, 4, MULTI, BK, TWO>), g, dim3(512), 0, st, a); break;
+    default:
+      if constexpr (!MULTI)
+        hipLaunchKernelGGL((pgemm_kernel<256, 256, 4, 2, 4, false, BK, TWO, false, 32>), g, dim3(512), 0, st, a);
+      break;
   }
 }
 
@@ -1897,7 +1910,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
   if (act && (a.stats || a.bnb)) return false;
   // res_mode 3 (gated data gradient, pg_epilogue_k only): the plain pgemm_kernel tiles
-  if (a.res_mode == 3 && (c < 0 || c > 4 || a.bnb || a.R * a.S != 1)) return false;
+  if (a.res_mode == 3 && (c < 0 || c >= kNumCfg || a.bnb || a.R * a.S != 1)) return false;
   if (c == 20) return !act && sconv_launch(a, st);
   if (c == 21) return hconv_launch(a, st);  // bias / ReLU epilogue supported
   if (act && c >= 11 && c <= 13) return false;
@@ -1926,14 +1939,16 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
     }
     return true;
   }
-  if (c < 0 || c > 4) return false;
+  if (c < 0 || c >= kNumCfg) return false;
+  if (c == 5 && multi) return false;
   const PgCfg& g = kCfgs[c];
   const long long tiles = ((a.M + g.bpx - 1) / g.bpx) * ((a.Cout + g.bch - 1) / g.bch);
   if (tiles > 0x7fffffffLL) return false;
-  static const char* names[2][5] = {{"pgemm_kernel<256,256>", "pgemm_kernel<256,128>", "pgemm_kernel<256,64>",
-                                      "pgemm_kernel<128,128>", "pgemm_kernel<256,32>"},
-                                     {"pgemm_kernel<256,256,bnb>", "pgemm_kernel<256,128,bnb>", "pgemm_kernel<256,64,bnb>",
-                                      "pgemm_kernel<128,128,bnb>", "pgemm_kernel<256,32,bnb>"}};
+  static const char* names[2][kNumCfg] = {
+      {"pgemm_kernel<256,256>", "pgemm_kernel<256,128>", "pgemm_kernel<256,64>", "pgemm_kernel<128,128>",
+       "pgemm_kernel<256,32>", "pgemm_kernel<256,256,k32>"},
+      {"pgemm_kernel<256,256,bnb>", "pgemm_kernel<256,128,bnb>", "pgemm_kernel<256,64,bnb>",
+       "pgemm_kernel<128,128,bnb>", "pgemm_kernel<256,32,bnb>", "pgemm_kernel<256,256,k32,bnb>"}};
   if (a.bnb) {
     if (!(multi ? pg_launch_bnb<true>(c, a, tiles, st) : pg_launch_bnb<false>(c, a, tiles, st))) return false;
   } else {
