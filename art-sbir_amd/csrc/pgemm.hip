@@ -100,6 +100,10 @@ __device__ __forceinline__ void vm_wait() {
 // wait until at most `ahead` stages of this wave's loads are outstanding
 template <int LPS, int NSTAGE>
 __device__ __forceinline__ void wait_stages(int ahead) {
+  if constexpr (NSTAGE >= 6) {
+    if (ahead >= 4) { vm_wait<4 * LPS>(); return; }
+    if (ahead >= 3) { vm_wait<3 * LPS>(); return; }
+  }
   if constexpr (NSTAGE >= 4) {
     if (ahead >= 2) { vm_wait<2 * LPS>(); return; }
   }
@@ -1070,13 +1074,18 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
 // (pg_epilogue_k, kinds as pgemm_kernel's, TWO targets), its operands and BN
 // constants read from global memory in batches of two pixel tiles while the
 // loader waves already stream the next tile's stages
-template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS, int BK = 0, bool TWO = false>
+// KS: k per stage as in pgemm_kernel (32: 64-B LDS rows, twice the stages in
+// the same LDS, uniform taps only)
+template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS, int BK = 0, bool TWO = false,
+          int KS = 64>
 __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int BPX = 256, NWC = 8, NWL = 4;
   static_assert(WPX * WCH == NWC, "compute waves");
-  constexpr int PXB = BPX * 128, CHB = BCH * 128, STAGE = PXB + CHB;
-  constexpr int LPX = BPX / (8 * NWL);
-  constexpr int LCH = BCH / (8 * NWL);
+  static_assert(KS == 64 || (KS == 32 && !MULTI), "32-k stages: uniform taps only");
+  constexpr int ROWB = 2 * KS, RPI = 1024 / ROWB, CPR = ROWB / 16;
+  constexpr int PXB = BPX * ROWB, CHB = BCH * ROWB, STAGE = PXB + CHB;
+  constexpr int LPX = BPX / (RPI * NWL);
+  constexpr int LCH = BCH / (RPI * NWL);
   constexpr int LPS = LPX + LCH;
   constexpr int WTPX = BPX / WPX, WTCH = BCH / WCH;
   constexpr int NTP = WTPX / 16, MTC = WTCH / 16;
@@ -1091,15 +1100,15 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   const int G = gridDim.x;
   const int bslot = (G % 8 == 0) ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   const int my_tiles = bslot < ntiles ? (ntiles - 1 - bslot) / G + 1 : 0;
-  const int nk = (a.K + 63) / 64;
+  const int nk = (a.K + KS - 1) / KS;
   const int total = my_tiles * nk;
   const int HoWo = a.Ho * a.Wo;
 
   if (wid >= NWC) {
     // ------------------------------------------------------------ loaders
     const int lw = wid - NWC;
-    const int lrow = lane >> 3, lslot = lane & 7;
-    const int csrc = lslot ^ lrow;
+    const int lrow = lane / CPR, lslot = lane % CPR;
+    const int csrc = KS == 64 ? (lslot ^ lrow) : (lslot ^ ((lrow >> 2) & 3));
     const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
     __amdgpu_buffer_rsrc_t xr = wr;
     int rowoff[LPX];
@@ -1114,7 +1123,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       xr = pg_rsrc(reinterpret_cast<const bf16*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * 2);
 #pragma unroll
       for (int u = 0; u < LPX; ++u) {
-        const int row = (u * NWL + lw) * 8 + lrow;
+        const int row = (u * NWL + lw) * RPI + lrow;
         const long long gm = bpx + row;
         const bool valid = gm < a.M;
         const long long gmc = valid ? gm : bpx;
@@ -1133,7 +1142,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       }
 #pragma unroll
       for (int u = 0; u < LCH; ++u) {
-        const int ch = bch + pg_perm((u * NWL + lw) * 8 + lrow);
+        const int ch = bch + pg_perm((u * NWL + lw) * RPI + lrow);
         woff[u] = ch < a.Cout ? (unsigned)(ch * a.K * 2 + csrc * 16) : PG_OOB;
       }
       u_ci = 0; u_s = 0; u_r = 0;
@@ -1149,7 +1158,7 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
         rs = u_r * a.S + u_s;
         tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + u_ci + csrc * 8) * 2;
         kval = true;
-        u_ci += 64;
+        u_ci += KS;
         if (u_ci == a.C) {
           u_ci = 0;
           if (++u_s == a.S) { u_s = 0; ++u_r; }
@@ -1168,10 +1177,10 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
         const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
         glds16(xr, pxs + (u * NWL + lw) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
       }
-      const bool wk = kt * 64 + csrc * 8 < a.K;
+      const bool wk = kt * KS + csrc * 8 < a.K;
 #pragma unroll
       for (int u = 0; u < LCH; ++u)
-        glds16(wr, chs + (u * NWL + lw) * 1024, (wk && woff[u] != PG_OOB) ? woff[u] + kt * 128 : PG_OOB);
+        glds16(wr, chs + (u * NWL + lw) * 1024, (wk && woff[u] != PG_OOB) ? woff[u] + kt * ROWB : PG_OOB);
     };
     for (int s = 0; s < NSTAGE - 1; ++s)
       if (s < total) issue(s);
@@ -1221,15 +1230,15 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       const char* pxs = smem + (s % NSTAGE) * STAGE;
       const char* chs = pxs + PXB;
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int so = ((kk * 4 + fq) ^ (fr & 7)) << 4;
+      for (int kk = 0; kk < KS / 32; ++kk) {
+        const int so = (KS == 64 ? ((kk * 4 + fq) ^ (fr & 7)) : (fq ^ ((fr >> 2) & 3))) << 4;
         uint4 af[MTC], bv[NTP];
 #pragma unroll
         for (int i = 0; i < MTC; ++i)
-          af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * 128 + so);
+          af[i] = *reinterpret_cast<const uint4*>(chs + (wch * WTCH + i * 16 + fr) * ROWB + so);
 #pragma unroll
         for (int j = 0; j < NTP; ++j)
-          bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * 128 + so);
+          bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * ROWB + so);
         PG_PRIO_ON();
 #pragma unroll
         for (int i = 0; i < MTC; ++i)
@@ -1870,6 +1879,32 @@ static void pstream_launch_k(int bch, const PgArgs& a, int grid, int ntl, hipStr
                        ntl);
 }
 
+// candidate 15: the persistent streaming kernel with 32-k stages (six in the
+// LDS the 64-k form holds three in; plain and forward-statistics epilogues,
+// C % 64 == 0, 64- / 128-channel blocks)
+static bool pstream_k32_launch(const PgArgs& a, bool multi, hipStream_t st) {
+  if (multi || a.bnb || a.Cout <= 32) return false;
+  const int bch = a.Cout <= 64 ? 64 : 128;
+  const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);
+  if (nt > 0x7fffffffLL) return false;
+  const int grid = (int)(nt < 256 ? nt : 256), ntl = (int)nt;
+  set_last_kernel(bch == 64 ? "pstream_kernel<64,k32>" : "pstream_kernel<128,k32>");
+  if (a.stats) {
+    if (bch == 64)
+      hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 6, false, false, true, 0, false, 32>), dim3(grid), dim3(768), 0, st, a,
+                         ntl);
+    else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 6, false, false, true, 0, false, 32>), dim3(grid), dim3(768), 0,
+                            st, a, ntl);
+  } else {
+    if (bch == 64)
+      hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 6, false, false, false, 0, false, 32>), dim3(grid), dim3(768), 0, st,
+                         a, ntl);
+    else hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 6, false, false, false, 0, false, 32>), dim3(grid), dim3(768), 0,
+                            st, a, ntl);
+  }
+  return true;
+}
+
 // candidate 14: the persistent streaming kernel with the specialised fused
 // BN-backward epilogue (the kinds pg_launch_bnb takes, channel blocks 64 / 128)
 static bool pstream_bnb_launch(const PgArgs& a, bool multi, hipStream_t st) {
@@ -1918,6 +1953,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (!pg_supported(a, multi)) return false;
   if (c >= 11 && c <= 13) return pg_pf_launch(c, a, multi, st);
   if (c == 14) return pstream_bnb_launch(a, multi, st);
+  if (c == 15) return pstream_k32_launch(a, multi, st);
   if (c == 10) {
     const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
     const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);
