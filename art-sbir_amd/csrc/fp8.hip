@@ -607,6 +607,7 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
       accumulate = 0; res = nullptr; out2 = nullptr; skip_c = 1;
     }
     const int nrd = (accumulate ? 1 : 0) + (res ? 1 : 0);
+    set_last_kernel("gemm_fp8_v2_kernel");
     if (nrd == 0) {
       FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0>), dim3((unsigned)t2), dim3(512), 0, st, M,
                                                N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
@@ -621,6 +622,7 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
                                                (bf16*)out2, skip_c, nullptr));
     }
   } else {
+    set_last_kernel("gemm_fp8_kernel");
     FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K,
                                              a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res, (bf16*)out2,
                                              skip_c, nullptr));
@@ -648,9 +650,11 @@ extern "C" int artsbir_gemm_nt_fp8_gelu(int M, int N, int K, const unsigned char
       set_error("gemm_nt_fp8_gelu: operand larger than 2 GiB");
       return -1;
     }
+    set_last_kernel("gemm_fp8_v2_kernel");
     hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa, sb,
                        bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
   } else {
+    set_last_kernel("gemm_fp8_kernel");
     hipLaunchKernelGGL(gemm_fp8_kernel<bf16>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K, a, b, sa, sb, bias,
                        (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
   }

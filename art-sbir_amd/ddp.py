@@ -24,6 +24,8 @@ under the remaining layers' backward instead of after it.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -31,6 +33,22 @@ import _hip
 from _hip import call, ptr
 
 BUCKET_BYTES = 64 << 20
+
+
+def init_distributed() -> None:
+    """one process per GPU (torch.distributed.run): RCCL ("nccl") on the GPU of
+    LOCAL_RANK; ARTSBIR_DIST_BACKEND=gloo for several ranks sharing one device
+    (tests) or CPU-only hosts"""
+    if dist.is_initialized():
+        return
+    backend = os.environ.get("ARTSBIR_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local % torch.cuda.device_count())
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
 
 
 def is_distributed() -> bool:
@@ -45,7 +63,11 @@ def allreduce_gradients(model, bucket_bytes: int = BUCKET_BYTES) -> None:
     """Average param.grad over all ranks (call after loss.backward())."""
     if not is_distributed():
         return
-    gb = model._hip_engine._grads
+    gb = getattr(getattr(model, "_hip_engine", None), "_grads", None)
+    if gb is None:
+        # a model whose gradients autograd accumulates (vit.VisionTransformer):
+        # plain param.grad tensors, all-reduced in coalesced buckets
+        return allreduce_tensors([p.grad for p in model.parameters() if p.grad is not None], bucket_bytes)
     flat = gb.flat
     world = dist.get_world_size()
     op = _avg_op()
@@ -56,6 +78,37 @@ def allreduce_gradients(model, bucket_bytes: int = BUCKET_BYTES) -> None:
     if op != dist.ReduceOp.AVG:
         # gloo (CPU tests): sum then scale in place; flat is f32
         flat.mul_(1.0 / world)
+
+
+def allreduce_tensors(tensors, bucket_bytes: int = BUCKET_BYTES) -> None:
+    """Average a list of tensors over all ranks in place: consecutive tensors of
+    one dtype / device are flattened into buckets of about bucket_bytes, each
+    bucket is one all-reduce (torch DDP's coalesced buckets), then copied back."""
+    if not is_distributed() or not tensors:
+        return
+    op = _avg_op()
+    world = dist.get_world_size()
+    buckets, cur, nbytes = [], [], 0
+    for t in tensors:
+        if cur and (t.dtype != cur[0].dtype or t.device != cur[0].device or nbytes >= bucket_bytes):
+            buckets.append(cur)
+            cur, nbytes = [], 0
+        cur.append(t)
+        nbytes += t.numel() * t.element_size()
+    if cur:
+        buckets.append(cur)
+    pending = []
+    for b in buckets:
+        flat = torch.cat([t.reshape(-1) for t in b])
+        pending.append((b, flat, dist.all_reduce(flat, op=op, async_op=True)))
+    for b, flat, w in pending:
+        w.wait()
+        if op != dist.ReduceOp.AVG:
+            flat.mul_(1.0 / world)
+        o = 0
+        for t in b:
+            t.copy_(flat[o:o + t.numel()].view_as(t))
+            o += t.numel()
 
 
 class OverlappedReducer:
@@ -184,6 +237,9 @@ def broadcast_buffers(model, src: int = 0) -> None:
         return
     for b in model.buffers():
         dist.broadcast(b, src=src)
+    eng = getattr(model, "_hip_engine", None)
+    if eng is not None and hasattr(eng, "bn_stats_changed"):
+        eng.bn_stats_changed()  # running statistics replaced: refold the eval weights
 
 
 def broadcast_parameters(model, src: int = 0) -> None:

@@ -189,6 +189,10 @@ class Engine:
         self._side_keep = []  # tensors the weight-gradient stream still reads (released at the join)
         self._eval = None      # folded conv weights + biases of the eval forward
         self._eval_key = None
+        # bumped whenever a train-mode forward updates the BN running statistics
+        # (artsbir_bn_finalize_seg writes them through raw pointers, invisible to
+        # torch's version counters), so the folded eval weights are rebuilt
+        self._bn_gen = 0
 
     # ------------------------------------------------------------------ utils
     @property
@@ -302,6 +306,8 @@ class Engine:
         updated once per segment, as by the reference's consecutive calls)"""
         C = bnmod.num_features
         G = self._G
+        if train:
+            self._bn_gen += 1
         st = BNState(torch.empty(G, 4, C, dtype=torch.float32, device=bnmod.weight.device), float(count))
         call("artsbir_bn_finalize_seg", ptr(stats_buf) if train else None, G, 2 * NSLOT * C, C, float(count),
              ptr(bnmod.weight.detach()), ptr(bnmod.bias.detach()), ptr(bnmod.running_mean), ptr(bnmod.running_var),
@@ -329,9 +335,14 @@ class Engine:
         return out
 
     # ------------------------------------------------ inference (folded BN)
+    def bn_stats_changed(self):
+        """the running statistics were written behind torch's back (e.g. a
+        broadcast from another rank): the folded eval weights are stale"""
+        self._bn_gen += 1
+
     def _eval_params_key(self):
         bns = [mod for mod in self.model.modules() if isinstance(mod, torch.nn.BatchNorm2d)]
-        return (self._params_key(), tuple((b.running_mean.data_ptr(), b.running_mean._version,
+        return (self._params_key(), self._bn_gen, tuple((b.running_mean.data_ptr(), b.running_mean._version,
                                            b.running_var._version, b.weight._version, b.bias._version) for b in bns))
 
     def _fold(self, conv, bn, ci_pad=None):

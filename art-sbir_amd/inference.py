@@ -305,8 +305,12 @@ def run_inference_sharded(model, dataset, loss_type='euclidean', start_time=None
     shard-parallel retrieval; every rank returns the same dictionary, rank 0
     wrote the feature file (its path is broadcast)."""
     import torch.distributed as dist
+    import ddp
     start_time = timer() if start_time is None else start_time
     with_classification = 'with_classification' in type(model).__name__
+    # every rank embeds its shard with the same eval model: rank 0's BatchNorm
+    # running statistics (each rank's own came from its own minibatches)
+    ddp.broadcast_buffers(model)
     inference_dataset, shard, g_base, feature_path = compute_image_features_sharded(model, dataset,
                                                                                     with_classification)
     box = [str(feature_path) if feature_path is not None else None]
@@ -343,6 +347,11 @@ def main(argv=None):
     parser.add_argument('-a', '--all', action="store_true",
                         help="Rerun inference for all Modified_ResNet* models where results folder exist")
     args = parser.parse_args(argv)
+    import ddp
+    import os
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        ddp.init_distributed()  # torchrun: gallery embedding and retrieval sharded over the ranks
+    rank0 = int(os.environ.get("RANK", "0")) == 0
     folders = [] if not args.folder else [args.folder]
     if args.all:
         folders = [p.stem for p in Path("./models").glob("ModifiedResNet*.pth")]
@@ -365,6 +374,8 @@ def main(argv=None):
         _, test_dataset = data_preparation.get_datasets(dataset=dataset, size=data_dict.get('size', 1.0),
                                                         transform=model.transform)
         inference_dict = run_inference(model, test_dataset, None, param_dict.get('loss_type', 'euclidean'))
+        if not rank0:
+            continue
         with open(Path("results") / folder / "inference_updated.json", "w") as f:
             json.dump(inference_dict, f, indent=4)
         import visualization

@@ -109,6 +109,7 @@ def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, op
 @torch.no_grad()
 def _evaluate(model, loss_fn, loader, stale, limit):
     """eval-mode loss over the test batches (or over the stale train batch, as the reference)."""
+    ddp.broadcast_buffers(model)  # eval BatchNorm with rank 0's running statistics (torch DDP semantics)
     model.eval()
     total = 0.0
     for b, tup in enumerate(loader):
@@ -165,6 +166,9 @@ def parse_args(argv=None):
     p.add_argument('--output_dim', type=int, default=1024)
     p.add_argument('--resolution', type=int, default=224)
     p.add_argument('--width', type=int, default=64)
+    p.add_argument('--vit_width', type=int, default=768, help="VisionTransformer width (ViT-B/16: 768)")
+    p.add_argument('--vit_layers', type=int, default=12, help="VisionTransformer blocks (ViT-B/16: 12)")
+    p.add_argument('--patch_size', type=int, default=16, help="VisionTransformer patch size (ViT-B/16: 16)")
     p.add_argument('--synthetic_n', type=int, default=256, help="triplets in the synthetic dataset")
     p.add_argument('--stale_eval', dest='stale_eval', action='store_true', default=True,
                    help="the reference's test loss on the stale last train batch (train.py:80,89; default)")
@@ -178,14 +182,12 @@ def main(argv=None):
     args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        ddp.init_distributed()
     utils.MARGIN = args.loss_margin
     layers = tuple(int(v) for v in args.layers.split(","))
     model = utils.build_model(args.dataset, args.model_type, layers=layers, output_dim=args.output_dim,
-                              input_resolution=args.resolution, width=args.width, heads=args.width * 32 // 64)
+                              input_resolution=args.resolution, width=args.width, heads=args.width * 32 // 64,
+                              vit_width=args.vit_width, vit_layers=args.vit_layers, patch_size=args.patch_size)
     if os.path.isfile(os.path.join("models", args.model)):
         model = utils.load_model(args.model, dataset=args.dataset, model_type=args.model_type)
     model.freeze_layers()
@@ -220,9 +222,14 @@ def main(argv=None):
         training_dict = triplet_train(model, args.epochs, train_loader, test_loader, loss_fn, optimizer,
                                       with_classification, stale_eval=args.stale_eval)
     rank0 = int(os.environ.get("RANK", "0")) == 0
-    if args.inference and rank0:
+    if args.inference:
+        # every rank takes part: with several processes the gallery embedding
+        # and the retrieval are sharded over them (collectives), and all ranks
+        # embed with rank 0's BatchNorm running statistics (DDP broadcast_buffers)
+        ddp.broadcast_buffers(model)
         inference_dict = inference.run_inference(model, test_dataset, args.feature_folder, args.loss_type)
-        print({k: v for k, v in inference_dict.items() if k != "retrieval_samples"}, flush=True)
+        if rank0:
+            print({k: v for k, v in inference_dict.items() if k != "retrieval_samples"}, flush=True)
     if rank0 and not args.no_save:
         folder = utils.save_model(model, data_dict, training_dict, param_dict, inference_dict)
         visualization.visualize(folder, training_dict, inference_dict)  # train.py:195

@@ -116,7 +116,11 @@ def build_model(dataset: str = None, model_type: str = None, layers=(3, 4, 6, 3)
     """The ModifiedResNet branches of utils.load_model (utils.py:166-197), and the
     ViT-B/16 encoder of configuration C5 (model_type 'VisionTransformer')."""
     if model_type in ('VisionTransformer', 'ViT-B/16'):
-        return models.VisionTransformer(kw.get('input_resolution', 224), 16, 768, 12, 12, output_dim)
+        # ViT-B/16 by default; vit_width / vit_layers / patch_size select a smaller one (tests)
+        width = kw.get('vit_width', 768)
+        return models.VisionTransformer(kw.get('input_resolution', 224), kw.get('patch_size', 16), width,
+                                        kw.get('vit_layers', 12), width // 64, output_dim)
+    kw = {k: v for k, v in kw.items() if k not in ('vit_width', 'vit_layers', 'patch_size')}
     if model_type == 'ModifiedResNet' or dataset in DATASETS_V1:
         return models.ModifiedResNet(layers=layers, output_dim=output_dim, **kw)
     if model_type == 'ModifiedResNet_with_classification' and dataset in ['SketchyV2', 'SketchyDatasetV2']:
@@ -141,6 +145,18 @@ def load_model(name: str, dataset: str = None, model_type: str = None, max_seq_l
         loaded = torch.load(path, map_location=torch.device('cpu'), weights_only=True)
         if not isinstance(loaded, dict):
             raise Exception(f"{path}: expected a state_dict")
+        own = model.state_dict()
+        shared = [k for k in loaded if k in own]
+        if not shared:
+            # strict=False would load nothing and train from random weights while
+            # reporting a loaded checkpoint (e.g. an RN50 file for --model_type VisionTransformer)
+            raise Exception(f"{path} shares no parameter name with {type(model).__name__}: wrong --model / "
+                            f"--model_type?")
+        skipped = len(loaded) - len(shared)
+        missing = len(own) - len(shared)
+        if skipped or missing:
+            print(f"load_model: {len(shared)} tensors loaded, {skipped} in the file unused, {missing} of the model "
+                  f"not in the file (strict=False, as utils.py:168)")
         try:
             model.load_state_dict(loaded, strict=False)
         except RuntimeError:

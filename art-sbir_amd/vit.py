@@ -81,7 +81,9 @@ def _gemm(a: torch.Tensor, b_nk: torch.Tensor, M: int, N: int, K: int, bias=None
         out = torch.empty(M, N, dtype=torch.float32 if out_f32 else a.dtype, device=a.device)
     call("artsbir_gemm_nt", _dt(a), M, N, K, a.data_ptr(), K, b_nk.data_ptr(), out.data_ptr(), N,
          1 if (acc or out.dtype == torch.float32) else 0, 1 if acc else 0,
-         bias.data_ptr() if bias is not None else None, None, _st())
+         bias.data_ptr() if bias is not None else None, None, _st(), kernel="auto", flops=2.0 * M * N * K,
+         nbytes=float(a.element_size() * (M * K + N * K) + out.element_size() * M * N * (2 if acc else 1)),
+         tag=f"vit gemm_nt {M}x{N}x{K}")
     return out
 
 
@@ -89,7 +91,9 @@ def _wgrad(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor):
     """dw[N][K] += sum_m dy[m][n] x[m][k]"""
     M, N = dy.shape
     K = x.shape[1]
-    call("artsbir_gemm_tn", _dt(dy), M, N, K, dy.data_ptr(), N, x.data_ptr(), K, dw.data_ptr(), _st())
+    call("artsbir_gemm_tn", _dt(dy), M, N, K, dy.data_ptr(), N, x.data_ptr(), K, dw.data_ptr(), _st(),
+         kernel="auto", flops=2.0 * M * N * K, nbytes=float(dy.element_size() * (M * N + M * K) + 8 * N * K),
+         tag=f"vit gemm_tn {M}x{N}x{K}")
 
 
 def _colsum(x: torch.Tensor, out: torch.Tensor):
@@ -146,7 +150,8 @@ def _fp8(x: torch.Tensor, pmax=None):
         call("artsbir_quantize_fp8", _dt(x), x.data_ptr(), x.numel(), q.data_ptr(), sc.data_ptr(), _st())
     else:
         call("artsbir_quantize_fp8_pmax", _dt(x), x.data_ptr(), x.numel(), pmax.data_ptr(), pmax.numel(),
-             q.data_ptr(), sc.data_ptr(), _st())
+             q.data_ptr(), sc.data_ptr(), _st(), kernel="fp8_quant_kernel",
+             nbytes=float(x.numel() * (x.element_size() + 1)), tag=f"vit quantize {x.numel()}")
     return q, sc
 
 
@@ -162,10 +167,14 @@ def _gemm_fp8(a: torch.Tensor, w: torch.Tensor, bias, out=None, out_dtype=torch.
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype, device=a.device)
     b = bias.detach().float().contiguous() if bias is not None else None
+    es = out.element_size()
+    nb = M * K + N * K + M * N * ((0 if skip_c else es) + (es if acc else 0) + (2 if res is not None else 0)
+                                  + (2 if out2 is not None else 0))
     call("artsbir_gemm_nt_fp8_ex", M, N, K, qa.data_ptr(), qw.data_ptr(), sa.data_ptr(), sw.data_ptr(),
          b.data_ptr() if b is not None else None, out.data_ptr(), _hip.dtype_code(out.dtype), 1 if acc else 0,
          res.data_ptr() if res is not None else None, out2.data_ptr() if out2 is not None else None,
-         1 if skip_c else 0, _st())
+         1 if skip_c else 0, _st(), kernel="auto", flops=2.0 * M * N * K, nbytes=float(nb),
+         tag=f"vit gemm_fp8 {M}x{N}x{K}")
     return out
 
 
@@ -180,7 +189,9 @@ def _gemm_fp8_gelu(a: torch.Tensor, w: torch.Tensor, bias, a_pmax, g_pmax):
     g = torch.empty_like(f)
     b = bias.detach().float().contiguous() if bias is not None else None
     call("artsbir_gemm_nt_fp8_gelu", M, N, K, qa.data_ptr(), qw.data_ptr(), sa.data_ptr(), sw.data_ptr(),
-         b.data_ptr() if b is not None else None, f.data_ptr(), g.data_ptr(), g_pmax.data_ptr(), _st())
+         b.data_ptr() if b is not None else None, f.data_ptr(), g.data_ptr(), g_pmax.data_ptr(), _st(),
+         kernel="auto", flops=2.0 * M * N * K, nbytes=float(M * K + N * K + 4 * M * N),
+         tag=f"vit gemm_fp8_gelu {M}x{N}x{K}")
     return f, g
 
 
@@ -268,7 +279,8 @@ class _BlockFunction(torch.autograd.Function):
         if fp8:
             call("artsbir_mha_fwd_lse_pmax", _dt(x), qkv.data_ptr(), L, N, heads,
                  mask.data_ptr() if mask is not None else None, att.data_ptr(), lse.data_ptr(), pm[1].data_ptr(),
-                 _st())
+                 _st(), kernel="attn_fwd_kernel", flops=4.0 * N * heads * L * L * 64,
+                 nbytes=float(qkv.element_size() * M * 4 * E), tag=f"vit attn fwd L{L} N{N}")
         else:
             call("artsbir_mha_fwd_lse", _dt(x), qkv.data_ptr(), L, N, heads,
                  mask.data_ptr() if mask is not None else None, att.data_ptr(), lse.data_ptr(), _st())
@@ -330,7 +342,8 @@ class _BlockFunction(torch.autograd.Function):
             # the c_fc bias gradient as its column sums (per-slot partials, then summed)
             slots = torch.zeros(_hip.NSLOT, 2, 4 * E, dtype=torch.float32, device=dev)
             call("artsbir_gemm_nt_gate", M, 4 * E, E, dy2.data_ptr(), E, _t(w_pr, T).data_ptr(), df.data_ptr(),
-                 4 * E, f.data_ptr(), slots.data_ptr(), _st())
+                 4 * E, f.data_ptr(), slots.data_ptr(), _st(), kernel="auto", flops=2.0 * M * 4 * E * E,
+                 nbytes=float(2 * (M * E + 4 * E * E + 2 * M * 4 * E)), tag=f"vit gemm_gate {M}x{4 * E}x{E}")
             call("artsbir_colsum", _hip.DT_F32, slots.data_ptr(), _hip.NSLOT, 8 * E, 4 * E, db_fc.data_ptr(), _st())
         else:
             da = _gemm(dy2, _t(w_pr, T), M, 4 * E, E)
@@ -349,7 +362,9 @@ class _BlockFunction(torch.autograd.Function):
         dsc = torch.empty(M * heads, dtype=torch.float32, device=dev)
         mask = ctx.mask
         call("artsbir_mha_bwd", _dt(qkv), qkv.data_ptr(), att.data_ptr(), datt.data_ptr(), lse.data_ptr(), L, N,
-             heads, mask.data_ptr() if mask is not None else None, dqkv.data_ptr(), dsc.data_ptr(), _st())
+             heads, mask.data_ptr() if mask is not None else None, dqkv.data_ptr(), dsc.data_ptr(), _st(),
+             kernel="attn_bwd_kernels", flops=10.0 * N * heads * L * L * 64,
+             nbytes=float(qkv.element_size() * M * 8 * E), tag=f"vit attn bwd L{L} N{N}")
         _wgrad(dqkv, h, dw_in)
         _colsum(dqkv, db_in)
         dh = _gemm(dqkv, _t(w_in, T), M, E, 3 * E)

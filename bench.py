@@ -27,7 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 LAYERS, OUT_DIM, RES, WIDTH, HEADS = (3, 4, 6, 3), 512, 224, 64, 32
-MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}  # MI355X dense (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # MI355X dense (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s measured copy)
 # per-launch HBM bytes of each kernel from the committed rocprofv3 PMC passes
 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/summarize_pmc.py)
@@ -90,9 +90,77 @@ def cpu_model():
     return platform.processor() or platform.machine()
 
 
+def roofline(prof, peak_of):
+    """Roofline of the dominant kernel from a live per-launch profile (_hip.PROFILE
+    entries: kernel, algorithmic FLOPs, algorithmic bytes, HIP start / end events
+    on the launch's stream).  Launches are pooled by kernel name; the dominant
+    kernel has the largest summed time; its bound follows its arithmetic
+    intensity against the ridge peak / HBM.  peak_of(kernel) -> the dense MFMA
+    TFLOP/s of that kernel's operand type.  Each launch is also priced at its own
+    roofline time max(bytes / HBM peak, FLOPs / MFMA peak): a kernel name pools
+    MFMA-bound and HBM-bound shapes, whose pooled GB/s or TFLOP/s alone
+    understates both; sum(roofline time) / sum(time) does not."""
+    agg = {}
+    for kname, fl, nb, e0, e1, *_ in prof:
+        a = agg.setdefault(kname, [0.0, 0.0, 0, 0.0, 0.0])
+        a[0] += fl
+        a[1] += e0.elapsed_time(e1) / 1e3
+        a[2] += 1
+        a[3] += nb
+        a[4] += max(nb / (HBM_PEAK_GBS * 1e9), fl / (peak_of(kname) * 1e12))
+    dom = max(agg, key=lambda k: agg[k][1])
+    fl, secs, cnt, nb, rt = agg[dom]
+    peak_fl = peak_of(dom)
+    ridge = peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if nb > 0 and fl / nb < ridge:
+        achieved = nb / secs / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4)}
+    else:
+        achieved = fl / secs / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_fl, "unit": "TFLOP/s",
+                "frac": round(achieved / peak_fl, 4)}
+    roof.update({"traffic": pmc_traffic(dom), "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT),
+                 "kernel": dom, "launches": cnt, "avg_launch_us": round(secs / cnt * 1e6, 2),
+                 "avg_launch_flops": fl / cnt, "avg_launch_bytes": nb / cnt,
+                 "intensity_flop_per_byte": round(fl / nb, 1) if nb else None,
+                 "frac_launch_roofline": round(rt / secs, 4),
+                 "step_launch_roofline": round(sum(v[4] for v in agg.values()) / sum(v[1] for v in agg.values()), 4),
+                 "per_kernel": {k: {"launches": v[2], "avg_us": round(v[1] / v[2] * 1e6, 2),
+                                    "tflops": round(v[0] / v[1] / 1e12, 1),
+                                    "gbs": round(v[3] / v[1] / 1e9, 1), "share_s": round(v[1], 4),
+                                    "roof_frac": round(v[4] / v[1], 4)}
+                                for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}})
+    return roof
+
+
+def cgroup_cpu_quota():
+    """the CPU bandwidth limit of this process's cgroup in cores (cgroup v2
+    cpu.max "quota period"), or None when unlimited / unreadable"""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else float(quota) / float(period)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_cores():
-    cores = len(os.sched_getaffinity(0))
-    return max(1, min(cores, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    """every core this process may run on (torch.set_num_threads(len(
+    os.sched_getaffinity(0)))), capped only by a cgroup CPU quota if one is set
+    (threads beyond the quota would just be throttled); ARTSBIR_CPU_THREADS overrides"""
+    forced = int(os.environ.get("ARTSBIR_CPU_THREADS", "0") or 0)
+    if forced:
+        return forced
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpu_quota()
+    return max(1, min(n, int(q)) if q else n)
+
+
+def cpu_info():
+    """what the CPU baselines ran on (stated in the line)"""
+    return {"cpu": cpu_model(), "affinity_cores": len(os.sched_getaffinity(0)), "cgroup_quota_cores": cgroup_cpu_quota(),
+            "threads_used": cpu_cores()}
 
 
 def cpu_baseline(batch=32, steps=3, layers=LAYERS, out_dim=OUT_DIM):
@@ -112,7 +180,7 @@ def cpu_baseline(batch=32, steps=3, layers=LAYERS, out_dim=OUT_DIM):
         osteps.train_step(m, opt, loss, el)
     dt = time.perf_counter() - t0
     return {"value": round(3 * batch * steps / dt, 3), "unit": "triplet-images/s", "cores": cores, "kind": "port",
-            "cpu": cpu_model(),
+            "cpu": cpu_model(), "host": cpu_info(),
             "sample": f"oracle/steps.py train_step, ModifiedResNet({layers},{out_dim}) fp32 224^2, {steps} timed "
                       f"steps x {batch} triplets after 1 warm-up, torch CPU {torch.__version__}"}
 
@@ -418,47 +486,7 @@ def main():
     if rank == 0:
         images = 3 * B * world * args.steps
         value = images / elapsed
-        roof = None
-        if prof:
-            # per kernel: algorithmic FLOPs and bytes (declared by the engine per
-            # launch) over the HIP-event time of its launches; the dominant kernel
-            # (most time) is priced against the roof its arithmetic intensity hits
-            # a[4]: each launch's own roofline time max(bytes / HBM peak, FLOPs /
-            # MFMA peak), summed: a kernel name pools MFMA-bound (3x3) and
-            # HBM-bound (1x1) shapes, whose pooled GB/s or TFLOP/s alone
-            # understates both; sum(roofline time) / sum(time) does not
-            peak_fl = MFMA_PEAK_TFLOPS[args.dtype]
-            agg = {}
-            for kname, fl, nb, e0, e1, *_ in prof:
-                a = agg.setdefault(kname, [0.0, 0.0, 0, 0.0, 0.0])
-                a[0] += fl
-                a[1] += e0.elapsed_time(e1) / 1e3
-                a[2] += 1
-                a[3] += nb
-                a[4] += max(nb / (HBM_PEAK_GBS * 1e9), fl / (peak_fl * 1e12))
-            dom = max(agg, key=lambda k: agg[k][1])
-            fl, secs, cnt, nb, rt = agg[dom]
-            ridge = peak_fl * 1e12 / (HBM_PEAK_GBS * 1e9)
-            if nb > 0 and fl / nb < ridge:
-                achieved = nb / secs / 1e9
-                roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(achieved / HBM_PEAK_GBS, 4)}
-            else:
-                achieved = fl / secs / 1e12
-                roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_fl, "unit": "TFLOP/s",
-                        "frac": round(achieved / peak_fl, 4)}
-            roof.update({"traffic": pmc_traffic(dom), "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT),
-                         "kernel": dom, "launches": cnt, "avg_launch_us": round(secs / cnt * 1e6, 2),
-                         "avg_launch_flops": fl / cnt, "avg_launch_bytes": nb / cnt,
-                         "intensity_flop_per_byte": round(fl / nb, 1) if nb else None,
-                         "frac_launch_roofline": round(rt / secs, 4),
-                         "step_launch_roofline": round(sum(v[4] for v in agg.values()) /
-                                                       sum(v[1] for v in agg.values()), 4),
-                         "per_kernel": {k: {"launches": v[2], "avg_us": round(v[1] / v[2] * 1e6, 2),
-                                            "tflops": round(v[0] / v[1] / 1e12, 1),
-                                            "gbs": round(v[3] / v[1] / 1e9, 1), "share_s": round(v[1], 4),
-                                            "roof_frac": round(v[4] / v[1], 4)}
-                                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}})
+        roof = roofline(prof, lambda k: MFMA_PEAK_TFLOPS[args.dtype]) if prof else None
         step_flops = train_flops_per_triplet() * B
         line = {
             "metric": "triplet-images/sec embedded @224² bf16, 1→8 GPU; gallery kNN QPS @1M×512",
@@ -480,7 +508,8 @@ def main():
             "allocator": alloc,
         }
     emb = None if args.no_embed else embed_leg(model, batch, args.dtype, world, args.steps)
-    c5 = c5_leg(dev, rank, world, args.c5_batch, max(2, args.steps // 2)) if args.c5 else None
+    c5 = c5_leg(dev, rank, world, args.c5_batch, max(2, args.steps // 2), profile=not args.no_profile,
+                loss_check=not args.no_loss_check) if args.c5 else None
     ret = None if args.no_retrieval else retrieval_leg(dev, rank, world)
     if ret is not None:
         # the same workload with queries far from their positives (ranks spread,
@@ -503,41 +532,59 @@ def main():
                 emb["cpu_baseline"] = cpu_embed_baseline()
             if ret is not None:
                 ret["cpu_baseline"] = cpu_retrieval_baseline()
+            if c5 is not None:
+                c5["cpu_baseline"] = cpu_c5_baseline()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def c5_leg(dev, rank, world, B, steps, warmup=1):
+def c5_leg(dev, rank, world, B, steps, warmup=1, profile=True, loss_check=True):
     """BASELINE configs[4] / SURVEY C5: ViT-B/16 (CLIP VisionTransformer, 224^2, patch 16,
     12 x 768, 12 heads) -> 768-d, triplet step (3 branch calls as one batch: no
     BatchNorm in a ViT), fp8 e4m3 projection GEMMs in the forward, bf16 elsewhere,
     Adam; synthetic normalised images resident in HBM.  Algorithmic work: 3 x
-    (forward FLOPs) per image, forward = 35.1 GFLOP."""
+    (forward FLOPs) per image, forward = 35.1 GFLOP.  Step-0 check:
+    the fp8 step's loss against the f32 mode of the same library on the same batch
+    and weights (tests/test_c5_gpu.py holds every mode against the float64 oracle)."""
+    import _hip
+    import ddp
     import losses
     import optim
     import vit
     torch.manual_seed(4321)
     model = vit.VisionTransformer(224, 16, 768, 12, 12, 768).to(dev)
-    model.compute_dtype = "fp8"
     model.train()
     opt = optim.Adam(model.parameters(), lr=1e-5, weight_decay=0.002)
     loss_fn = losses.TripletMarginLoss(margin=0.2)
     g = torch.Generator(device=dev).manual_seed(200 + rank)
     xs = [torch.randn(B, 3, 224, 224, device=dev, generator=g) for _ in range(3)]
+    check = None
+    if loss_check:
+        model.compute_dtype = torch.float32
+        with torch.no_grad():
+            a, p, n = model.forward_branches(xs)
+            l32 = float(loss_fn(a, p, n).item())
+            scale = float(((a - p).norm(dim=1) + (a - n).norm(dim=1)).mean())
+        del a, p, n
+        torch.cuda.empty_cache()
+        check = {"loss_step0_f32": l32, "distance_scale": round(scale, 6)}
+    model.compute_dtype = "fp8"
 
     def step():
         outs = model.forward_branches(xs)
         loss = loss_fn(*outs)
         opt.zero_grad(set_to_none=False)
         loss.backward()
-        if world > 1:
-            for p in model.parameters():
-                dist.all_reduce(p.grad, op=dist.ReduceOp.AVG)
+        ddp.allreduce_gradients(model)  # N > 1: coalesced bucketed all-reduce of the autograd gradients
         opt.step()
         return loss
-    for _ in range(warmup):
-        step()
+    for i in range(warmup):
+        li = step()
+        if i == 0 and check is not None:
+            check["loss_step0"] = float(li.item())
+            # the hinge's argument is a difference of distances: its error scales with them
+            check["rel_to_distance_scale"] = round(abs(check["loss_step0"] - l32) / max(scale, 1e-12), 6)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -550,12 +597,56 @@ def c5_leg(dev, rank, world, B, steps, warmup=1):
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    roof = None
+    if profile:
+        prof = []
+        _hip.PROFILE = prof
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        _hip.PROFILE = None
+        roof = roofline(prof, lambda k: MFMA_PEAK_TFLOPS["fp8" if "fp8" in k else "bf16"])
     images = 3 * B * world * steps
     flops = 3 * 35.1e9 * images
-    return {"metric": "triplet-images/sec, ViT-B/16 768-d fp8 (C5)", "value": round(images / el, 2),
-            "unit": "triplet-images/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 2),
-            "triplets_per_gpu": B, "dtype": "fp8 e4m3 projections (forward), bf16 otherwise",
-            "tflops": round(flops / el / 1e12, 1), "loss": float(loss.item()), "data": "synthetic"}
+    out = {"metric": "triplet-images/sec, ViT-B/16 768-d fp8 (C5)", "value": round(images / el, 2),
+           "unit": "triplet-images/s", "steps": steps, "ms_per_step": round(el / steps * 1e3, 2),
+           "triplets_per_gpu": B, "dtype": "fp8 e4m3 projections (forward), bf16 otherwise",
+           "tflops": round(flops / el / 1e12, 1), "loss": float(loss.item()), "data": "synthetic",
+           "roofline": roof, "step0_check": check}
+    return out
+
+
+def cpu_c5_baseline(batch=2, steps=2):
+    """the oracle's ViT-B/16 (oracle/encoder.vision_transformer, CLIP keys) in torch
+    CPU fp32: three separate branch forwards, nn.TripletMarginLoss(0.2), backward,
+    torch.optim.Adam — a bounded sample of `batch` triplets per step"""
+    from oracle import encoder as oenc
+    import vit
+    cores = cpu_cores()
+    torch.set_num_threads(cores)
+    torch.manual_seed(4321)
+    sd = {k: v.detach().float().clone().requires_grad_(True)
+          for k, v in vit.VisionTransformer(224, 16, 768, 12, 12, 768).state_dict().items()}
+    opt = torch.optim.Adam(list(sd.values()), lr=1e-5, weight_decay=0.002)
+    loss_fn = torch.nn.TripletMarginLoss(margin=0.2)
+    g = torch.Generator().manual_seed(5)
+    xs = [torch.randn(batch, 3, 224, 224, generator=g) for _ in range(3)]
+
+    def step():
+        outs = [oenc.vision_transformer(x, sd, 16, 12) for x in xs]
+        loss = loss_fn(*outs)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(3 * batch * steps / dt, 3), "unit": "triplet-images/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model(), "sample": f"oracle/encoder.vision_transformer ViT-B/16 fp32 224^2, {steps} timed "
+                                          f"steps x {batch} triplets after 1 warm-up (3 branch forwards, "
+                                          f"TripletMarginLoss, Adam), torch CPU {torch.__version__}"}
 
 
 if __name__ == "__main__":

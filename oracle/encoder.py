@@ -164,15 +164,22 @@ def quick_gelu(x):
     return x * torch.sigmoid(1.702 * x)
 
 
-def residual_attention_block(x, sd, n_head, attn_mask=None, eps=1e-5):
+def _linear(a, w, b):
+    return a @ w.t() + b
+
+
+def residual_attention_block(x, sd, n_head, attn_mask=None, eps=1e-5, linear=None):
     """models.py:396-417 on a state dict with the reference keys (attn.in_proj_*,
     attn.out_proj.*, ln_1.*, mlp.c_fc.*, mlp.c_proj.*, ln_2.*): x [L, N, E],
     seq-first; self-attention of nn.MultiheadAttention written out (q scaled by
-    1/sqrt(head_dim), additive float mask, softmax over keys)."""
+    1/sqrt(head_dim), additive float mask, softmax over keys).  ``linear(a, w, b)``
+    computes the four projections (default a @ w.T + b; the C5 tests pass an
+    e4m3-quantising one to price what fp8 operands cost)."""
+    linear = linear or _linear
     L, N, E = x.shape
     hd = E // n_head
     h = layernorm_fp32(x, sd["ln_1.weight"], sd["ln_1.bias"], eps)
-    qkv = h @ sd["attn.in_proj_weight"].t() + sd["attn.in_proj_bias"]
+    qkv = linear(h, sd["attn.in_proj_weight"], sd["attn.in_proj_bias"])
     q, k, v = qkv.split(E, dim=-1)
 
     def heads(t):  # [L, N, E] -> [N, heads, L, hd]
@@ -181,10 +188,10 @@ def residual_attention_block(x, sd, n_head, attn_mask=None, eps=1e-5):
     if attn_mask is not None:
         s = s + attn_mask
     o = (torch.softmax(s, dim=-1) @ heads(v)).permute(2, 0, 1, 3).reshape(L, N, E)
-    x = x + (o @ sd["attn.out_proj.weight"].t() + sd["attn.out_proj.bias"])
+    x = x + linear(o, sd["attn.out_proj.weight"], sd["attn.out_proj.bias"])
     h = layernorm_fp32(x, sd["ln_2.weight"], sd["ln_2.bias"], eps)
-    f = quick_gelu(h @ sd["mlp.c_fc.weight"].t() + sd["mlp.c_fc.bias"])
-    return x + (f @ sd["mlp.c_proj.weight"].t() + sd["mlp.c_proj.bias"])
+    f = quick_gelu(linear(h, sd["mlp.c_fc.weight"], sd["mlp.c_fc.bias"]))
+    return x + linear(f, sd["mlp.c_proj.weight"], sd["mlp.c_proj.bias"])
 
 
 def init_params(model: nn.Module, seed: int = 1234) -> None:
@@ -221,7 +228,7 @@ def synthetic_triplet(batch: int, res: int, seed: int = 0):
     return tuple(out)
 
 
-def vision_transformer(x, sd, patch, n_head, eps=1e-5):
+def vision_transformer(x, sd, patch, n_head, eps=1e-5, linear=None):
     """CLIP's VisionTransformer.forward (the C5 encoder; the reference ships only
     its blocks, models.py:382-417) on a state dict with CLIP's keys: conv1
     patch embedding, class token, positional embedding, ln_pre, resblocks,
@@ -237,7 +244,7 @@ def vision_transformer(x, sd, patch, n_head, eps=1e-5):
     while f"transformer.resblocks.{i}.ln_1.weight" in sd:
         pre = f"transformer.resblocks.{i}."
         t = residual_attention_block(t, {k[len(pre):]: v for k, v in sd.items() if k.startswith(pre)}, n_head,
-                                     eps=eps)
+                                     eps=eps, linear=linear)
         i += 1
     t = t.permute(1, 0, 2)
     c = layernorm_fp32(t[:, 0, :], sd["ln_post.weight"], sd["ln_post.bias"], eps)

@@ -249,3 +249,32 @@ def _sharded_inference(rank, tmp, metric):
 @pytest.mark.parametrize("metric", ["euclidean", "cosine"])
 def test_sharded_gallery_inference_matches_unsharded(tmp_path, metric):
     _run(_sharded_inference, str(tmp_path), metric)
+
+
+def _allreduce_autograd_model(rank):
+    """a model without the HIP engine's flat buffer (vit.VisionTransformer's
+    gradients are autograd's param.grad): coalesced buckets of mixed sizes and
+    dtypes, every tensor averaged exactly once"""
+    import ddp
+    m = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.Linear(5, 3))
+    for i, p in enumerate(m.parameters()):
+        p.grad = torch.full(p.shape, float((rank + 1) * (i + 1)))
+    m[1].bias.grad = None  # a parameter without a gradient is skipped
+    ddp.allreduce_gradients(m, bucket_bytes=64)  # several buckets, split at tensor boundaries
+    for i, p in enumerate(m.parameters()):
+        if p.grad is not None:
+            assert torch.allclose(p.grad, torch.full(p.shape, 1.5 * (i + 1))), i
+    ts = [torch.arange(5, dtype=torch.float64) * (rank + 1), torch.ones(3, dtype=torch.bfloat16) * (rank + 1)]
+    ddp.allreduce_tensors(ts, bucket_bytes=1 << 20)  # a dtype change starts a new bucket
+    assert torch.allclose(ts[0], torch.arange(5, dtype=torch.float64) * 1.5)
+    assert torch.allclose(ts[1].float(), torch.full((3,), 1.5))
+    r = ddp.attach_overlapped_reducer(m)  # no engine: finish() is the plain coalesced all-reduce
+    for p in m.parameters():
+        if p.grad is not None:
+            p.grad.fill_(float(rank))
+    r.finish()
+    assert all(torch.allclose(p.grad, torch.full(p.shape, 0.5)) for p in m.parameters() if p.grad is not None)
+
+
+def test_allreduce_gradients_without_engine():
+    _run(_allreduce_autograd_model)

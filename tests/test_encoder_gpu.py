@@ -194,3 +194,30 @@ def test_fused_eval_matches_unfused(dtype, tol, dev):
         with torch.no_grad():
             e_ref = ref(s)
         assert torch.allclose(e_fused, e_ref, atol=1e-3, rtol=1e-3), _rel(e_fused, e_ref)
+
+
+def test_fused_eval_refolds_after_train_forward_without_step(dev):
+    """the folded eval weights cache the BN running statistics; a train-mode
+    forward with no optimizer step (BN recalibration under no_grad) updates those
+    statistics through raw pointers, so the next eval must refold: it must equal
+    the unfused eval path and the oracle run through the same sequence"""
+    import engine
+    cfg = TINY
+    ref, mine = _pair(cfg, dev)
+    s, p, _ = oenc.synthetic_triplet(4, cfg["res"])
+    ref.eval(); mine.eval()
+    with torch.no_grad():
+        mine(s.to(dev))  # builds the folded cache
+        ref.train(); mine.train()
+        ref(p); mine(p.to(dev))  # running statistics move, no parameter changes
+        ref.eval(); mine.eval()
+        e_ref = ref(s)
+        e = mine(s.to(dev)).float().cpu()
+        old = engine.FUSED_EVAL
+        try:
+            engine.FUSED_EVAL = False
+            e_plain = mine(s.to(dev)).float().cpu()
+        finally:
+            engine.FUSED_EVAL = old
+    assert torch.allclose(e, e_plain, atol=1e-4, rtol=1e-4), _rel(e, e_plain)
+    assert torch.allclose(e, e_ref, atol=1e-3, rtol=1e-3), _rel(e, e_ref)
