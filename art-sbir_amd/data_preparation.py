@@ -55,11 +55,64 @@ def synthetic_sketch(path, photo_path, res: int) -> torch.Tensor:
     return torch.from_numpy((img - MEAN) / STD)
 
 
+# ---------------------------------------------------------------- pixel mode
+# The reference's datasets open image FILES (PIL) and run the model's transform
+# (models.py:289-295) in DataLoader workers (train.py:154-155).  Pixel mode
+# reproduces that input pipeline: an image is the decoded file when it exists,
+# else a deterministic stand-in of the same kind (a decoded photo of 256..640 px
+# per side, RGB; a 256 x 256 grayscale sketch, like Sketchy's PNGs), and then
+#   decode_only=False  the CPU transform (PIL resize / crop / normalise), as the reference;
+#   decode_only=True   the uint8 pixels only: the GPU transform runs on the whole
+#                      batch in one library call (preprocess.ClipPreprocess,
+#                      SURVEY §8f row 3), so the workers only decode.
+
+def synthetic_pixels(path, kind: str) -> np.ndarray:
+    rng = _rng(path)
+    if kind == "sketch":
+        img = np.full((256, 256), 255, np.uint8)
+        img[rng.random((256, 256)) < 0.1] = 0
+        return img
+    w, h = (int(v) for v in rng.integers(256, 641, size=2))
+    base = rng.integers(0, 256, size=(h // 8 + 1, w // 8 + 1, 3), dtype=np.uint8)  # blocky content plus noise
+    img = np.repeat(np.repeat(base, 8, axis=0), 8, axis=1)[:h, :w]
+    return np.ascontiguousarray(img ^ rng.integers(0, 32, size=(h, w, 3), dtype=np.uint8))
+
+
+def load_pixels(path, kind: str) -> np.ndarray:
+    """the decoded image file (HxW 'L' or HxWx3 'RGB' uint8), or its stand-in"""
+    if Path(path).is_file():
+        from PIL import Image
+        with Image.open(path) as im:
+            if im.mode not in ("L", "RGB"):
+                im = im.convert("RGB")
+            return np.asarray(im).copy()
+    return synthetic_pixels(path, kind)
+
+
+def pixels_item(path, kind, transform, decode_only):
+    a = load_pixels(path, kind)
+    if decode_only:
+        return torch.from_numpy(a)
+    from PIL import Image
+    return transform(Image.fromarray(a))
+
+
+def collate_decoded(batch):
+    """DataLoader collate for decode-only items: ragged uint8 images stay lists
+    (one list per element of the item), everything else is stacked as usual"""
+    from torch.utils.data import default_collate
+    if isinstance(batch[0], torch.Tensor):
+        return list(batch) if batch[0].dtype == torch.uint8 else default_collate(batch)
+    return [collate_decoded([b[i] for b in batch]) for i in range(len(batch[0]))]
+
+
 class InferenceDataset(Dataset):
-    def __init__(self, image_paths: List[Path], transform=None, resolution: int = 224):
+    def __init__(self, image_paths: List[Path], transform=None, resolution: int = 224, pixels: bool = False,
+                 decode_only: bool = False):
         super().__init__()
         self.transform = transform
         self.resolution = resolution
+        self.pixels, self.decode_only = pixels or decode_only, decode_only
         self.image_paths = list(dict.fromkeys(image_paths))
         self.image_paths.sort()
 
@@ -68,6 +121,8 @@ class InferenceDataset(Dataset):
 
     def __getitem__(self, idx: int) -> torch.Tensor:
         p = self.image_paths[idx]
+        if self.pixels:
+            return pixels_item(p, "photo", self.transform, self.decode_only)
         if Path(p).is_file() and self.transform is not None:
             from PIL import Image
             return self.transform(Image.open(p))
@@ -76,8 +131,10 @@ class InferenceDataset(Dataset):
 
 class SyntheticTripletDataset(Dataset):
     def __init__(self, n: int = 256, resolution: int = 224, mode: str = "train", split_ratio: float = 0.1,
-                 size: float = 1.0, seed: int = 42, transform=None, dups: int = 1, name: str = None):
+                 size: float = 1.0, seed: int = 42, transform=None, dups: int = 1, name: str = None,
+                 pixels: bool = False, decode_only: bool = False):
         super().__init__()
+        self.pixels, self.decode_only = pixels or decode_only, decode_only
         self.name = name or self.__class__.__name__
         if mode not in ("train", "test"):
             raise ValueError("invalid mode: [train, test]")
@@ -102,10 +159,15 @@ class SyntheticTripletDataset(Dataset):
 
     def __getitem__(self, idx):
         s, p, n = self.load_image_sketch_tuple(idx)
+        if self.pixels:
+            return tuple(pixels_item(x, k, self.transform, self.decode_only)
+                         for x, k in ((s, "sketch"), (p, "photo"), (n, "photo")))
         r = self.resolution
         return synthetic_sketch(s, p, r), synthetic_photo(p, r), synthetic_photo(n, r)
 
     def sketch(self, idx):
+        if self.pixels:
+            return pixels_item(self.sketch_paths[idx], "sketch", self.transform, self.decode_only)
         return synthetic_sketch(self.sketch_paths[idx], self.photo_paths[idx], self.resolution)
 
     @property
@@ -117,8 +179,9 @@ class SyntheticTripletDataset(Dataset):
 
 class SyntheticKaggleInferenceDataset(Dataset):
     def __init__(self, photo_paths: List[Path], sketch_type: str = 'sketches', sketch_format: str = 'png',
-                 transform=None, resolution: int = 224):
+                 transform=None, resolution: int = 224, pixels: bool = False, decode_only: bool = False):
         super().__init__()
+        self.pixels, self.decode_only = pixels or decode_only, decode_only
         self.sketch_type, self.sketch_format, self.transform = sketch_type, sketch_format, transform
         self.resolution = resolution
         root = Path("data/kaggle") / sketch_type
@@ -133,6 +196,8 @@ class SyntheticKaggleInferenceDataset(Dataset):
         return len(self.sketch_paths)
 
     def sketch(self, idx):
+        if self.pixels:
+            return pixels_item(self.sketch_paths[idx], "sketch", self.transform, self.decode_only)
         return synthetic_sketch(self.sketch_paths[idx], self.photo_of[idx], self.resolution)
 
     def __getitem__(self, idx):
@@ -149,15 +214,20 @@ _LAST_TEST = [None]  # the gallery the Kaggle inference sketches refer to (the r
 
 def get_datasets(dataset: str = "Synthetic", size: float = 1.0, sketch_format: str = 'png', img_format: str = 'jpg',
                  sketch_type: str = 'placeholder', img_type: str = 'photos', split_ratio: float = 0.1, seed: int = 42,
-                 transform=None, n: int = 256, resolution: int = 224, **kw):
+                 transform=None, n: int = 256, resolution: int = 224, pixels: bool = False, decode_only: bool = False,
+                 **kw):
+    """pixels / decode_only: pixel mode (see synthetic_pixels above)"""
+    px = dict(pixels=pixels, decode_only=decode_only)
     if dataset.startswith("Synthetic"):
         name = None if dataset == "Synthetic" else dataset  # e.g. "SyntheticKaggleV1", "SyntheticMixedV1"
-        tr = SyntheticTripletDataset(n, resolution, "train", split_ratio, size, seed, transform, name=name)
-        te = SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform, name=name)
+        tr = SyntheticTripletDataset(n, resolution, "train", split_ratio, size, seed, transform, name=name, **px)
+        te = SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform, name=name, **px)
         _LAST_TEST[0] = te
         return tr, te
     if dataset in ('KaggleInferenceV1', 'KaggleInferencedatasetV1'):
         te = _LAST_TEST[0] or SyntheticTripletDataset(n, resolution, "test", split_ratio, size, seed, transform)
+        if not (pixels or decode_only):  # follow the gallery's mode
+            px = dict(pixels=te.pixels, decode_only=te.decode_only)
         return None, SyntheticKaggleInferenceDataset(te.photo_paths, sketch_type, sketch_format, transform,
-                                                     te.resolution)
+                                                     te.resolution, **px)
     raise Exception(f"{dataset} is not available (no datasets ship with this build; use Synthetic)")

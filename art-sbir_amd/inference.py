@@ -77,20 +77,46 @@ def get_topk_images(k: int, image_paths: List[Path], sketch_feature: torch.Tenso
     return [(str(image_paths[i]), float(d)) for i, d in zip(idx[0].tolist(), dist[0].tolist())]
 
 
+def _decoded(ds) -> bool:
+    base = ds.dataset if isinstance(ds, torch.utils.data.Subset) else ds
+    base = getattr(base, "ds", base)  # _Sketches
+    return bool(getattr(base, "decode_only", False))
+
+
+def _loader(ds, batch_size=50):
+    """the reference's DataLoader(bs=50, workers=0); decode-only datasets keep
+    their ragged uint8 images as lists (GPU preprocessing in _embed)"""
+    return DataLoader(ds, batch_size=batch_size, num_workers=0, shuffle=False,
+                      collate_fn=data_preparation.collate_decoded if _decoded(ds) else None)
+
+
 @torch.no_grad()
 def _embed(model, loader, with_classification):
+    import preprocess
     feats = []
+    res = getattr(model, "input_resolution", 224)
     for batch in loader:
-        x = batch[0] if isinstance(batch, (list, tuple)) else batch
-        out = model(x.to(device))
+        if isinstance(batch, (list, tuple)) and len(batch) and isinstance(batch[0], torch.Tensor) \
+                and batch[0].dtype == torch.uint8:
+            x = preprocess.to_device_batch(batch, res, device)  # decoded images: one GPU transform call
+        else:
+            x = batch[0] if isinstance(batch, (list, tuple)) else batch
+            x = x.to(device)
+        out = model(x)
         feats.append(out[0] if with_classification else out)
     return torch.cat(feats) if feats else torch.empty(0)
 
 
+def _gallery(dataset):
+    """InferenceDataset of the dataset's photos (data_preparation.py:24-41), in the dataset's pixel mode"""
+    return data_preparation.InferenceDataset(dataset.photo_paths, dataset.transform,
+                                             getattr(dataset, "resolution", 224), getattr(dataset, "pixels", False),
+                                             getattr(dataset, "decode_only", False))
+
+
 def compute_image_features(model, dataset, with_classification: bool):
-    inference_dataset = data_preparation.InferenceDataset(dataset.photo_paths, dataset.transform,
-                                                          getattr(dataset, "resolution", 224))
-    loader = DataLoader(inference_dataset, batch_size=50, num_workers=0, shuffle=False)
+    inference_dataset = _gallery(dataset)
+    loader = _loader(inference_dataset)
     model.to(device)
     model.eval()
     image_features = _embed(model, loader, with_classification)
@@ -202,8 +228,7 @@ def _embed_shard(model, ds, with_classification, batch_size=50):
     import torch.distributed as dist
     b = shard_bounds(len(ds), dist.get_world_size())
     r = dist.get_rank()
-    loader = DataLoader(torch.utils.data.Subset(ds, range(b[r], b[r + 1])), batch_size=batch_size, num_workers=0,
-                        shuffle=False)
+    loader = _loader(torch.utils.data.Subset(ds, range(b[r], b[r + 1])), batch_size)
     with torch.no_grad():
         feats = _embed(model, loader, with_classification)
     if feats.numel() == 0:  # an empty shard still needs the feature width for the gather
@@ -214,8 +239,7 @@ def _embed_shard(model, ds, with_classification, batch_size=50):
 def compute_image_features_sharded(model, dataset, with_classification: bool, save: bool = True):
     """-> (inference_dataset, this rank's gallery rows, g_base, feature_path or None)"""
     import torch.distributed as dist
-    inference_dataset = data_preparation.InferenceDataset(dataset.photo_paths, dataset.transform,
-                                                          getattr(dataset, "resolution", 224))
+    inference_dataset = _gallery(dataset)
     model.to(device)
     model.eval()
     feats, b = _embed_shard(model, inference_dataset, with_classification)
@@ -233,7 +257,7 @@ def _widen(feats, model, ds, with_classification):
     if feats.shape[0] > 0 or len(ds) == 0:
         return feats
     with torch.no_grad():
-        probe = _embed(model, DataLoader(torch.utils.data.Subset(ds, [0]), batch_size=1), with_classification)
+        probe = _embed(model, _loader(torch.utils.data.Subset(ds, [0]), 1), with_classification)
     return probe[:0]
 
 
@@ -266,7 +290,7 @@ def _second_pass(model, dataset, inference_dataset, image_features, first, with_
         shard, g_base = sharded
         return process_inference_sharded(model, dataset2, inference_dataset, _Sketches(dataset2), shard, g_base,
                                          first['inference_time'], with_classification, loss_type, **search)
-    loader2 = DataLoader(_Sketches(dataset2), batch_size=50, num_workers=0, shuffle=False)
+    loader2 = _loader(_Sketches(dataset2))
     return process_inference(model, dataset2, inference_dataset, loader2, image_features, first['inference_time'],
                              with_classification, loss_type)
 
@@ -289,7 +313,7 @@ def run_inference(model, dataset, folder_name: str = None, loss_type='euclidean'
         print("Image features loaded from file")
     else:
         inference_dataset, image_features, feature_folder = compute_image_features(model, dataset, with_classification)
-    dataloader = DataLoader(_Sketches(dataset), batch_size=50, num_workers=0, shuffle=False)
+    dataloader = _loader(_Sketches(dataset))
     inference_dict = process_inference(model, dataset, inference_dataset, dataloader, image_features, start_time,
                                        with_classification, loss_type)
     if not _needs_second_pass(dataset):

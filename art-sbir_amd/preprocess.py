@@ -49,7 +49,9 @@ def plan(w: int, h: int, res: int) -> Tuple[int, int, int, int]:
 
 def _pixels(img) -> np.ndarray:
     """HxW (L) or HxWx3 (RGB) uint8 of a PIL image or array"""
-    if hasattr(img, "mode"):
+    if isinstance(img, torch.Tensor):
+        a = img.detach().cpu().numpy()
+    elif hasattr(img, "mode"):
         if img.mode not in ("L", "RGB"):
             raise NotImplementedError(f"GPU preprocessing takes 'L' / 'RGB' images, got '{img.mode}'")
         a = np.asarray(img)
@@ -69,14 +71,14 @@ class ClipPreprocess:
         self.std = (ctypes.c_float * 3)(*[float(np.float32(s)) for s in std])
         self.device = torch.device(device)
 
-    def __call__(self, images: Sequence) -> torch.Tensor:
+    def stage(self, images: Sequence):
+        """host pixels -> (device uint8 buffer, descriptors): one pinned staging
+        buffer for the batch, one asynchronous host->device copy"""
         res = self.resolution
         arrays = [_pixels(im) for im in images]
         n = len(arrays)
-        out = torch.empty(n, 3, res, res, dtype=torch.float32, device=self.device)
         if n == 0:
-            return out
-        # one pinned staging buffer for the batch, one host->device copy
+            return None, (_hip.ImageDesc * 0)()
         sizes = [a.nbytes for a in arrays]
         offs = np.concatenate([[0], np.cumsum([(s + 255) // 256 * 256 for s in sizes])]).astype(np.int64)
         host = torch.empty(int(offs[-1]), dtype=torch.uint8, pin_memory=True)
@@ -90,17 +92,54 @@ class ClipPreprocess:
             c = 1 if a.ndim == 2 else a.shape[2]
             rw, rh, left, top = plan(w, h, res)
             descs[i] = _hip.ImageDesc(dev.data_ptr() + int(o), h, w, c, w * c, rw, rh, left, top)
+        return dev, descs
+
+    def run(self, dev: torch.Tensor, descs, out: torch.Tensor | None = None, nbytes: float = 0.0) -> torch.Tensor:
+        """the transform of images already in HBM (dev holds them, descs describes
+        them): [n,3,res,res] f32 in one library call"""
+        res = self.resolution
+        n = len(descs)
+        if out is None:
+            out = torch.empty(n, 3, res, res, dtype=torch.float32, device=self.device)
+        if n == 0:
+            return out
         ws_bytes = _hip.lib().artsbir_clip_preprocess_workspace(n, descs, res)
         if ws_bytes < 0:
             raise _hip.HipError(_hip.lib().artsbir_last_error().decode())
         ws = torch.empty(int(ws_bytes), dtype=torch.uint8, device=self.device)
         call("artsbir_clip_preprocess", n, descs, res, self.mean, self.std, out.data_ptr(), ws.data_ptr(), int(ws_bytes),
-             _hip.stream())
+             _hip.stream(), kernel="clip_preprocess", nbytes=nbytes, tag=f"clip_preprocess n{n}")
         dev.record_stream(torch.cuda.current_stream(self.device))
         return out
 
+    def __call__(self, images: Sequence) -> torch.Tensor:
+        dev, descs = self.stage(images)
+        return self.run(dev, descs)
+
     def __repr__(self):
         return f"ClipPreprocess(resize={self.resolution}, bicubic, center_crop, RGB, ToTensor, Normalize(CLIP), gpu)"
+
+
+_PRE = {}
+
+
+def clip_preprocessor(resolution: int = 224, device=None) -> ClipPreprocess:
+    """the per-(resolution, device) ClipPreprocess of the data path (train.py /
+    inference.py with --gpu_preprocess: DataLoader workers only decode)"""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (resolution, str(dev))
+    if key not in _PRE:
+        _PRE[key] = ClipPreprocess(resolution, device=dev)
+    return _PRE[key]
+
+
+def to_device_batch(batch, resolution: int, device=None):
+    """a collated batch element -> a normalised [n,3,res,res] f32 tensor on the
+    GPU: a list of decoded uint8 images goes through ClipPreprocess, a tensor
+    (already transformed on the CPU) is just moved"""
+    if isinstance(batch, (list, tuple)):
+        return clip_preprocessor(resolution, device)(batch)
+    return batch.to(device if device is not None else "cuda")
 
 
 # ------------------------------------------------------------ augmentation

@@ -83,7 +83,7 @@ def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, op
         if hasattr(train_dataloader.sampler, "set_epoch"):
             train_dataloader.sampler.set_epoch(epoch)  # DistributedSampler: a new shuffle per epoch
         for batch, tup in enumerate(train_dataloader):
-            elements = [e.to(device) for e in tup]
+            elements = _to_device(tup, model)
             loss = get_loss(loss_fn, model, elements)
             optimizer.zero_grad()
             loss.backward()  # gradient all-reduce buckets start inside (ddp.OverlappedReducer)
@@ -106,6 +106,16 @@ def _triplet_train(model, epochs, train_dataloader, test_dataloader, loss_fn, op
             "iteration_test_size": itest_size, "training_time": timer() - start_time}
 
 
+def _to_device(tup, model):
+    """one collated batch on the GPU: tensors are moved; with --gpu_preprocess the
+    images arrive as lists of decoded uint8 pixels and each branch is transformed
+    by ONE library call (preprocess.ClipPreprocess: Resize bicubic, CenterCrop,
+    RGB, ToTensor, Normalize of models.py:289-295, bit-identical to the CPU path)"""
+    import preprocess
+    res = getattr(model, "input_resolution", 224)
+    return [preprocess.to_device_batch(e, res, device) if isinstance(e, list) else e.to(device) for e in tup]
+
+
 @torch.no_grad()
 def _evaluate(model, loss_fn, loader, stale, limit):
     """eval-mode loss over the test batches (or over the stale train batch, as the reference)."""
@@ -113,7 +123,7 @@ def _evaluate(model, loss_fn, loader, stale, limit):
     model.eval()
     total = 0.0
     for b, tup in enumerate(loader):
-        el = stale if stale is not None else [e.to(device) for e in tup]
+        el = stale if stale is not None else _to_device(tup, model)
         total += float(get_loss(loss_fn, model, el).item())
         if limit is not None and b >= limit:
             break
@@ -169,6 +179,13 @@ def parse_args(argv=None):
     p.add_argument('--vit_width', type=int, default=768, help="VisionTransformer width (ViT-B/16: 768)")
     p.add_argument('--vit_layers', type=int, default=12, help="VisionTransformer blocks (ViT-B/16: 12)")
     p.add_argument('--patch_size', type=int, default=16, help="VisionTransformer patch size (ViT-B/16: 16)")
+    p.add_argument('--data_pixels', action='store_true',
+                   help="synthetic datasets as decoded image files of varied sizes (or the files, if present) "
+                        "through the model's CPU transform in the DataLoader workers, as the reference")
+    p.add_argument('--gpu_preprocess', action='store_true',
+                   help="DataLoader workers only decode; the transform runs on the GPU per batch "
+                        "(preprocess.ClipPreprocess; implies --data_pixels)")
+    p.add_argument('--workers', type=int, default=None, help="DataLoader workers (reference: min(4, cpus))")
     p.add_argument('--synthetic_n', type=int, default=256, help="triplets in the synthetic dataset")
     p.add_argument('--stale_eval', dest='stale_eval', action='store_true', default=True,
                    help="the reference's test loss on the stale last train batch (train.py:80,89; default)")
@@ -198,14 +215,19 @@ def main(argv=None):
     ddp.broadcast_parameters(model)
     train_dataset, test_dataset = data_preparation.get_datasets(dataset=args.dataset, size=args.dsize,
                                                                 transform=model.transform, n=args.synthetic_n,
-                                                                resolution=args.resolution)
+                                                                resolution=args.resolution,
+                                                                pixels=args.data_pixels or args.gpu_preprocess,
+                                                                decode_only=args.gpu_preprocess)
     sampler = None
     if world > 1:
         sampler = torch.utils.data.distributed.DistributedSampler(train_dataset, shuffle=True)
-    train_loader = DataLoader(train_dataset, batch_size=args.batch_size, num_workers=min(4, os.cpu_count()),
-                              shuffle=sampler is None, sampler=sampler)
-    test_loader = DataLoader(test_dataset, batch_size=args.batch_size, num_workers=min(4, os.cpu_count()),
-                             shuffle=False)
+    workers = args.workers if args.workers is not None else min(4, os.cpu_count())  # train.py:154-155
+    collate = data_preparation.collate_decoded if args.gpu_preprocess else None
+    train_loader = DataLoader(train_dataset, batch_size=args.batch_size, num_workers=workers,
+                              shuffle=sampler is None, sampler=sampler, collate_fn=collate,
+                              pin_memory=torch.cuda.is_available() and not args.gpu_preprocess)
+    test_loader = DataLoader(test_dataset, batch_size=args.batch_size, num_workers=workers, shuffle=False,
+                             collate_fn=collate)
     optimizer = optim.Adam(model.parameters(), lr=args.learning_rate, weight_decay=args.weight_decay)
     with_classification = 'with_classification' in type(model).__name__ and 'V2' in train_dataset.state_dict['dataset']
     loss_fn = make_loss(args.loss_type, with_classification, train_dataset.state_dict['dataset'], utils.MARGIN)

@@ -134,6 +134,111 @@ def roofline(prof, peak_of):
     return roof
 
 
+def preprocess_leg(dev, rank, world, n_triplets=384, reps=5):
+    """the input transform of the training step (models.py:289-295:
+    Resize(224, bicubic) -> CenterCrop -> RGB -> ToTensor -> Normalize) for one
+    step's 3 x n_triplets decoded images, as train.py --gpu_preprocess runs it:
+    one preprocess.ClipPreprocess call on a batch whose uint8 pixels are already
+    in HBM.  Images: data_preparation.synthetic_pixels stand-ins of decoded files
+    (sketches 256 x 256 grayscale, photos RGB 256..640 px per side, ragged).
+    Algorithmic bytes per image: its decoded pixels read once + the 3 x 224 x 224
+    f32 output written once.  Also: the PCIe-inclusive rate (host pixels ->
+    pinned staging -> HBM -> transform), the host's JPEG decode rate per core
+    (what the DataLoader workers still do) and the CPU transform as cpu_baseline."""
+    import _hip
+    import data_preparation as dp
+    import preprocess
+    imgs = []
+    for i in range(n_triplets):
+        imgs.append(dp.synthetic_pixels(f"bench/sketches/s{rank}_{i}.png", "sketch"))
+        imgs.append(dp.synthetic_pixels(f"bench/photos/p{rank}_{i}.jpg", "photo"))
+        imgs.append(dp.synthetic_pixels(f"bench/photos/n{rank}_{i}.jpg", "photo"))
+    pre = preprocess.ClipPreprocess(RES, device=dev)
+    in_bytes = float(sum(a.nbytes for a in imgs))
+    out_bytes = float(len(imgs) * 3 * RES * RES * 4)
+    devbuf, descs = pre.stage(imgs)
+    out = pre.run(devbuf, descs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = []
+    _hip.PROFILE = prof
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pre.run(devbuf, descs, out=out, nbytes=in_bytes + out_bytes)
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / reps
+    _hip.PROFILE = None
+    kern_s = sum(e0.elapsed_time(e1) for _, _, _, e0, e1, *_ in prof) / 1e3 / len(prof)
+    # PCIe-inclusive: host pixels staged to pinned memory, copied, transformed
+    t1 = time.perf_counter()
+    for _ in range(2):
+        pre(imgs)
+    torch.cuda.synchronize()
+    pcie = (time.perf_counter() - t1) / 2
+    if world > 1:
+        t = torch.tensor([el], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    n = len(imgs)
+    achieved = (in_bytes + out_bytes) / kern_s / 1e9
+    return {"metric": "images/s through the GPU input transform (train.py --gpu_preprocess)",
+            "value": round(n * world / el, 1), "unit": "images/s", "images_per_call": n, "n_gpus": world,
+            "ms_per_call": round(el * 1e3, 3), "pcie_inclusive_images_per_s": round(n / pcie, 1),
+            "input_mb_per_call": round(in_bytes / 1e6, 1),
+            "bit_exact_vs": "models.ClipTransform (Pillow) — tests/test_preprocess_gpu.py",
+            "roofline": {"bound": "hbm", "kernel": "pp_horizontal_kernel + pp_vertical_kernel (one call)",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "avg_launch_us": round(kern_s * 1e6, 2),
+                         "avg_launch_bytes": in_bytes + out_bytes, "traffic": None}}
+
+
+def cpu_preprocess_baseline(n=96, budget_s=10.0):
+    """the reference's input path on the host cores: JPEG/PNG decode (PIL) and
+    the model transform (models.ClipTransform = models.py:289-295 on Pillow) in a
+    thread pool of every core; decode is also timed alone, per core"""
+    import io
+    from concurrent.futures import ThreadPoolExecutor
+    from PIL import Image
+    import data_preparation as dp
+    import models
+    cores = cpu_cores()
+    files = []
+    for i in range(n):
+        kind = "sketch" if i % 3 == 0 else "photo"
+        a = dp.synthetic_pixels(f"bench/cpu/{i}", kind)
+        buf = io.BytesIO()
+        Image.fromarray(a).save(buf, format="PNG" if kind == "sketch" else "JPEG", quality=90)
+        files.append(buf.getvalue())
+    tr = models.ClipTransform(RES)
+
+    def decode(b):
+        with Image.open(io.BytesIO(b)) as im:
+            im.load()
+            return im.copy()
+    t0 = time.perf_counter()
+    done = 0
+    while time.perf_counter() - t0 < budget_s / 4 and done < 4 * n:
+        decode(files[done % n])
+        done += 1
+    dec1 = done / (time.perf_counter() - t0)
+
+    def full(b):
+        return tr(decode(b))
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(full, files[:cores]))
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < budget_s and done < 20 * n:
+            list(ex.map(full, files))
+            done += n
+        dt = time.perf_counter() - t0
+    return {"value": round(done / dt, 1), "unit": "images/s", "cores": cores, "kind": "port", "cpu": cpu_model(),
+            "decode_only_per_core": round(dec1, 1),
+            "sample": f"{done} images (1/3 256^2 PNG sketches, 2/3 JPEG q90 photos 256..640 px): PIL decode + "
+                      f"models.ClipTransform in a {cores}-thread pool; decode alone on 1 core"}
+
+
 def cgroup_cpu_quota():
     """the CPU bandwidth limit of this process's cgroup in cores (cgroup v2
     cpu.max "quota period"), or None when unlimited / unreadable"""
@@ -352,6 +457,7 @@ def main():
     ap.add_argument("--unbatched", dest="batched", action="store_false",
                     help="three separate encoder calls per step instead of forward_branches")
     ap.add_argument("--no-embed", action="store_true", help="skip the embed-only (eval-BN) leg")
+    ap.add_argument("--no-preprocess", action="store_true", help="skip the GPU input-transform leg")
     ap.add_argument("--sync-warmup", action="store_true", help="synchronize after every warmup step")
     ap.add_argument("--c5", action="store_true", default=True,
                     help="the C5 leg: ViT-B/16 768-d triplet training step, fp8 projections, 512 triplets (default)")
@@ -510,6 +616,7 @@ def main():
     emb = None if args.no_embed else embed_leg(model, batch, args.dtype, world, args.steps)
     c5 = c5_leg(dev, rank, world, args.c5_batch, max(2, args.steps // 2), profile=not args.no_profile,
                 loss_check=not args.no_loss_check) if args.c5 else None
+    pre = None if args.no_preprocess else preprocess_leg(dev, rank, world, args.batch)
     ret = None if args.no_retrieval else retrieval_leg(dev, rank, world)
     if ret is not None:
         # the same workload with queries far from their positives (ranks spread,
@@ -524,6 +631,8 @@ def main():
             line["retrieval"] = ret
         if c5 is not None:
             line["c5"] = c5
+        if pre is not None:
+            line["preprocess"] = pre
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
             # C1 (BASELINE configs[0]): the "ResNet18 128-d" config = ModifiedResNet((2,2,2,2),128), batch 32
@@ -534,6 +643,8 @@ def main():
                 ret["cpu_baseline"] = cpu_retrieval_baseline()
             if c5 is not None:
                 c5["cpu_baseline"] = cpu_c5_baseline()
+            if pre is not None:
+                pre["cpu_baseline"] = cpu_preprocess_baseline()
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

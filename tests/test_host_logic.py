@@ -141,3 +141,35 @@ def test_preprocess_plan_matches_torchvision_rules():
     assert preprocess.plan(224, 227, 224) == (224, 227, 0, 2)   # 1.5 -> 2
     assert preprocess.plan(97, 331, 224) == (224, 764, 0, 270)
     assert preprocess.plan(513, 1024, 224) == (224, 447, 0, 112)  # 111.5 -> 112
+
+
+def test_pixel_mode_datasets_decode_only_and_cpu_transform():
+    """pixel mode (SURVEY §8f row 3 data path): a decode-only item is the decoded
+    uint8 image; the CPU-transform item is the model transform of exactly those
+    pixels (models.py:289-295 through models.ClipTransform); ragged batches
+    collate to lists"""
+    import data_preparation
+    import models
+    from PIL import Image
+    from torch.utils.data import DataLoader
+    tr = models.ClipTransform(64)
+    a, _ = data_preparation.get_datasets("Synthetic", n=20, resolution=64, decode_only=True)
+    b, _ = data_preparation.get_datasets("Synthetic", n=20, resolution=64, pixels=True, transform=tr)
+    assert a.pixels and a.decode_only and b.pixels and not b.decode_only
+    import random
+    random.seed(3)
+    ia = a[2]
+    random.seed(3)
+    ib = b[2]
+    assert ia[0].dtype == torch.uint8 and ia[0].shape == (256, 256)        # grayscale sketch
+    assert ia[1].dtype == torch.uint8 and ia[1].ndim == 3 and ia[1].shape[2] == 3
+    assert 256 <= ia[1].shape[0] <= 640 and 256 <= ia[1].shape[1] <= 640  # varied photo sizes
+    for u8, t in zip(ia, ib):
+        want = tr(Image.fromarray(u8.numpy()))
+        assert torch.equal(t, want)
+    shapes = {tuple(a[i][1].shape) for i in range(len(a))}
+    assert len(shapes) > 1  # ragged
+    batch = next(iter(DataLoader(a, batch_size=4, collate_fn=data_preparation.collate_decoded)))
+    assert len(batch) == 3 and all(isinstance(x, list) and len(x) == 4 for x in batch)
+    g = data_preparation.InferenceDataset(a.photo_paths, None, 64, decode_only=True)
+    assert g[0].dtype == torch.uint8

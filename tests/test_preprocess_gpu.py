@@ -109,3 +109,48 @@ def test_gpu_warp_kinds_against_pillow(dev):
         got = aug.apply(rgb, [([(what, co)], [])]).cpu()[0]
         want = _pil_sketch_pipeline(src, [(what, co)], [], res)
         assert (got != want).sum().item() == 0, what
+
+
+def test_gpu_data_path_matches_cpu_transform_path(dev):
+    """train.py's input pipeline with --gpu_preprocess (DataLoader workers only
+    decode, one ClipPreprocess call per branch) gives bit-identically the batch
+    of the reference's pipeline (the model transform in the workers,
+    train.py:152-155) on the same decoded images, sketches (grayscale, 256^2) and
+    photos (RGB, ragged 256..640 px) alike"""
+    import random
+
+    import data_preparation
+    import models
+    import train
+    from torch.utils.data import DataLoader
+    res = 224
+    tr = models.ClipTransform(res)
+    gpu_ds, _ = data_preparation.get_datasets("Synthetic", n=40, resolution=res, decode_only=True, transform=tr)
+    cpu_ds, _ = data_preparation.get_datasets("Synthetic", n=40, resolution=res, pixels=True, transform=tr)
+    model = types_ns(res)
+    random.seed(9)
+    gb = next(iter(DataLoader(gpu_ds, batch_size=12, collate_fn=data_preparation.collate_decoded)))
+    random.seed(9)
+    cb = next(iter(DataLoader(cpu_ds, batch_size=12)))
+    g = train._to_device(gb, model)
+    c = [t.to(dev) for t in cb]
+    for x, y in zip(g, c):
+        assert x.shape == y.shape == (12, 3, res, res)
+        assert torch.equal(x, y), (x - y).abs().max().item()
+
+
+def types_ns(res):
+    import types
+    return types.SimpleNamespace(input_resolution=res)
+
+
+def test_train_cli_gpu_preprocess(tmp_path, dev, monkeypatch):
+    """train.py --gpu_preprocess --inference end to end (gallery embedding and
+    sketch queries through the GPU transform too)"""
+    import train
+    monkeypatch.chdir(tmp_path)
+    training, inf = train.main(["--layers", "1,1,1,1", "--width", "16", "--resolution", "64", "--output_dim", "32",
+                                "-b", "4", "--synthetic_n", "40", "-e", "1", "--inference", "--dtype", "bf16",
+                                "--gpu_preprocess", "--no_save"])
+    assert training["train_losses"][0] == training["train_losses"][0]
+    assert inf["size"] == 4 and inf["count"] == 4
