@@ -32,6 +32,8 @@ struct PrepDev {
   int rw, rh, left, top;
   int row0, nrows;        // source rows [row0, row0 + nrows) feed the crop
   long long tmp_off;      // byte offset of this image's [nrows][res][C] intermediate
+  long long htab, vtab;   // byte offsets of the per-axis tap tables (-1: axis not resampled)
+  int hn, vn;             // taps per table entry (entry = xmin, n, hn / vn weights)
 };
 
 #pragma clang fp contract(off)
@@ -82,29 +84,64 @@ __device__ __forceinline__ unsigned char pp_clip8(int v) {
   return (unsigned char)(v < 0 ? 0 : v > 255 ? 255 : v);
 }
 
+// tap tables: for each crop output index i of a resampled axis, the Resample.c
+// span (xmin, n) and its n 22-bit weights, computed ONCE per image and axis
+// (Pillow's precompute_coeffs) instead of per output pixel and tap
+__global__ void __launch_bounds__(256) pp_coeffs_kernel(const PrepDev* __restrict__ imgs, int res,
+                                                        unsigned char* __restrict__ ws) {
+  const PrepDev d = imgs[blockIdx.y];
+  const int axis = blockIdx.z;
+  const long long off = axis ? d.vtab : d.htab;
+  if (off < 0) return;
+  const int nt = axis ? d.vn : d.hn;
+  int* tab = reinterpret_cast<int*>(ws + off);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < res; i += gridDim.x * 256) {
+    const PpSpan sp = axis ? pp_span(d.H, d.rh, d.top + i) : pp_span(d.W, d.rw, d.left + i);
+    int* e = tab + (long long)i * (2 + nt);
+    e[0] = sp.xmin;
+    e[1] = sp.n;
+    for (int k = 0; k < nt; ++k) e[2 + k] = k < sp.n ? pp_weight(sp, k) : 0;
+  }
+}
+
 // horizontal pass: tmp[r][x][c] = row (row0 + r), crop column x, resampled W -> rw
+template <int C>
+__device__ __forceinline__ void pp_hpix(const PrepDev& d, const unsigned char* __restrict__ row,
+                                        const int* __restrict__ tab, int x, unsigned char* __restrict__ o) {
+  if (d.htab < 0) {  // this axis is not resampled
+    const int xo = d.left + x;
+#pragma unroll
+    for (int c = 0; c < C; ++c) o[c] = row[xo * C + c];
+    return;
+  }
+  const int* e = tab + (long long)x * (2 + d.hn);
+  const int xmin = e[0], n = e[1];
+  int acc[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) acc[c] = 1 << (PP_BITS - 1);
+  const unsigned char* p = row + xmin * C;
+  for (int k = 0; k < n; ++k) {
+    const int w = e[2 + k];
+#pragma unroll
+    for (int c = 0; c < C; ++c) acc[c] += (int)p[k * C + c] * w;
+  }
+#pragma unroll
+  for (int c = 0; c < C; ++c) o[c] = pp_clip8(acc[c]);
+}
+
 __global__ void __launch_bounds__(256) pp_horizontal_kernel(const PrepDev* __restrict__ imgs, int res,
-                                                            unsigned char* __restrict__ tmp) {
+                                                            unsigned char* __restrict__ tmp,
+                                                            const unsigned char* __restrict__ ws) {
   const PrepDev d = imgs[blockIdx.y];
   const long long total = (long long)d.nrows * res;
   unsigned char* t = tmp + d.tmp_off;
+  const int* tab = d.htab >= 0 ? reinterpret_cast<const int*>(ws + d.htab) : nullptr;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += gridDim.x * 256LL) {
     const int r = (int)(i / res), x = (int)(i % res);
     const unsigned char* row = d.src + (long long)(d.row0 + r) * d.pitch;
     unsigned char* o = t + ((long long)r * res + x) * d.C;
-    const int xo = d.left + x;
-    if (d.rw == d.W) {  // this axis is not resampled
-      for (int c = 0; c < d.C; ++c) o[c] = row[xo * d.C + c];
-      continue;
-    }
-    const PpSpan s = pp_span(d.W, d.rw, xo);
-    int acc[3] = {1 << (PP_BITS - 1), 1 << (PP_BITS - 1), 1 << (PP_BITS - 1)};
-    for (int k = 0; k < s.n; ++k) {
-      const int w = pp_weight(s, k);
-      const unsigned char* p = row + (s.xmin + k) * d.C;
-      for (int c = 0; c < d.C; ++c) acc[c] += (int)p[c] * w;
-    }
-    for (int c = 0; c < d.C; ++c) o[c] = pp_clip8(acc[c]);
+    if (d.C == 3) pp_hpix<3>(d, row, tab, x, o);
+    else pp_hpix<1>(d, row, tab, x, o);
   }
 }
 
@@ -115,6 +152,7 @@ __global__ void __launch_bounds__(256) pp_vertical_kernel(const PrepDev* __restr
                                                           float* __restrict__ out, unsigned char* __restrict__ out_u8) {
   const PrepDev d = imgs[blockIdx.y];
   const unsigned char* t = tmp + d.tmp_off;
+  const int* tab = d.vtab >= 0 ? reinterpret_cast<const int*>(tmp + d.vtab) : nullptr;
   float* o = out ? out + (long long)blockIdx.y * 3 * res * res : nullptr;
   unsigned char* o8 = out_u8 ? out_u8 + (long long)blockIdx.y * 3 * res * res : nullptr;
   const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
@@ -122,15 +160,17 @@ __global__ void __launch_bounds__(256) pp_vertical_kernel(const PrepDev* __restr
     const int y = i / res, x = i % res;
     const int yo = d.top + y;
     unsigned char v[3];
-    if (d.rh == d.H) {
+    if (!tab) {
       for (int c = 0; c < d.C; ++c) v[c] = t[((long long)(yo - d.row0) * res + x) * d.C + c];
     } else {
-      const PpSpan s = pp_span(d.H, d.rh, yo);
+      const int* e = tab + (long long)y * (2 + d.vn);
+      const int ymin = e[0], n = e[1];
       int acc[3] = {1 << (PP_BITS - 1), 1 << (PP_BITS - 1), 1 << (PP_BITS - 1)};
-      for (int k = 0; k < s.n; ++k) {
-        const int w = pp_weight(s, k);
-        const unsigned char* p = t + ((long long)(s.xmin + k - d.row0) * res + x) * d.C;
-        for (int c = 0; c < d.C; ++c) acc[c] += (int)p[c] * w;
+      const unsigned char* p = t + ((long long)(ymin - d.row0) * res + x) * d.C;
+      const long long step = (long long)res * d.C;
+      for (int k = 0; k < n; ++k) {
+        const int w = e[2 + k];
+        for (int c = 0; c < d.C; ++c) acc[c] += (int)p[k * step + c] * w;
       }
       for (int c = 0; c < d.C; ++c) v[c] = pp_clip8(acc[c]);
     }
@@ -188,13 +228,32 @@ static int pp_plan(int n, const artsbir_image_desc* descs, int res, PrepDev* out
         if (c + nc > r1) r1 = c + nc;
       }
     }
+    // taps per table entry: the widest span the crop's outputs use
+    int hn = 0, vn = 0;
+    if (s.rw != s.W)
+      for (int x = s.left; x < s.left + res; ++x) {
+        int a, na;
+        pp_span_host(s.W, s.rw, x, a, na);
+        if (na > hn) hn = na;
+      }
+    if (s.rh != s.H)
+      for (int y = s.top; y < s.top + res; ++y) {
+        int a, na;
+        pp_span_host(s.H, s.rh, y, a, na);
+        if (na > vn) vn = na;
+      }
+    const long long tmp_off = off;
+    off += ((long long)(r1 - r0) * res * s.C + 255) / 256 * 256;
+    long long htab = -1, vtab = -1;
+    if (s.rw != s.W) { htab = off; off += ((long long)res * (2 + hn) * 4 + 255) / 256 * 256; }
+    if (s.rh != s.H) { vtab = off; off += ((long long)res * (2 + vn) * 4 + 255) / 256 * 256; }
     if (out) {
       PrepDev& d = out[i];
       d.src = s.src; d.H = s.H; d.W = s.W; d.C = s.C; d.pitch = s.pitch;
       d.rw = s.rw; d.rh = s.rh; d.left = s.left; d.top = s.top;
-      d.row0 = r0; d.nrows = r1 - r0; d.tmp_off = off;
+      d.row0 = r0; d.nrows = r1 - r0; d.tmp_off = tmp_off;
+      d.htab = htab; d.vtab = vtab; d.hn = hn; d.vn = vn;
     }
-    off += ((long long)(r1 - r0) * res * s.C + 255) / 256 * 256;
   }
   bytes = off;
   return 0;
@@ -251,7 +310,10 @@ static int pp_run(int n, const artsbir_image_desc* descs, int res, const float* 
   const PrepDev* dimgs = reinterpret_cast<const PrepDev*>(workspace);
   unsigned char* tmp = reinterpret_cast<unsigned char*>(workspace);
   const unsigned gx = (unsigned)((res * res + 255) / 256 < 64 ? (res * res + 255) / 256 : 64);
-  hipLaunchKernelGGL(pp_horizontal_kernel, dim3(gx * 4, n), dim3(256), 0, st, dimgs, res, tmp);
+  hipLaunchKernelGGL(pp_coeffs_kernel, dim3((unsigned)((res + 255) / 256), n, 2), dim3(256), 0, st, dimgs, res, tmp);
+  ARTSBIR_CHECK_LAUNCH("clip_preprocess coefficients");
+  hipLaunchKernelGGL(pp_horizontal_kernel, dim3(gx * 4, n), dim3(256), 0, st, dimgs, res, tmp,
+                     (const unsigned char*)tmp);
   ARTSBIR_CHECK_LAUNCH("clip_preprocess horizontal");
   hipLaunchKernelGGL(pp_vertical_kernel, dim3(gx, n), dim3(256), 0, st, dimgs, res, tmp, mean3[0], mean3[1],
                      mean3[2], std3[0], std3[1], std3[2], out, out_u8);
