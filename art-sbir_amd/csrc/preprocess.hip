@@ -31,7 +31,7 @@ struct PrepDev {
   int H, W, C, pitch;
   int rw, rh, left, top;
   int row0, nrows;        // source rows [row0, row0 + nrows) feed the crop
-  long long tmp_off;      // byte offset of this image's [nrows][res][C] intermediate
+  long long tmp_off;      // byte offset of this image's planar [C][nrows][res] intermediate
   long long htab, vtab;   // byte offsets of the per-axis tap tables (-1: axis not resampled)
   int hn, vn;             // taps per table entry (entry = xmin, n, hn / vn weights)
 };
@@ -104,48 +104,70 @@ __global__ void __launch_bounds__(256) pp_coeffs_kernel(const PrepDev* __restric
   }
 }
 
-// horizontal pass: tmp[r][x][c] = row (row0 + r), crop column x, resampled W -> rw
-template <int C>
-__device__ __forceinline__ void pp_hpix(const PrepDev& d, const unsigned char* __restrict__ row,
-                                        const int* __restrict__ tab, int x, unsigned char* __restrict__ o) {
-  if (d.htab < 0) {  // this axis is not resampled
-    const int xo = d.left + x;
-#pragma unroll
-    for (int c = 0; c < C; ++c) o[c] = row[xo * C + c];
-    return;
-  }
-  const int* e = tab + (long long)x * (2 + d.hn);
-  const int xmin = e[0], n = e[1];
-  int acc[C];
-#pragma unroll
-  for (int c = 0; c < C; ++c) acc[c] = 1 << (PP_BITS - 1);
-  const unsigned char* p = row + xmin * C;
-  for (int k = 0; k < n; ++k) {
-    const int w = e[2 + k];
-#pragma unroll
-    for (int c = 0; c < C; ++c) acc[c] += (int)p[k * C + c] * w;
-  }
-#pragma unroll
-  for (int c = 0; c < C; ++c) o[c] = pp_clip8(acc[c]);
-}
+// The intermediate is PLANAR: tmp[c][r][x], bytes, rows of res bytes, so both
+// passes move 4 outputs per lane as one dword (res % 4 == 0; other widths
+// take the 1-output-per-lane form of the same arithmetic).
 
+// horizontal pass: tmp[c][r][x] = row (row0 + r), crop column x, channel c,
+// resampled W -> rw; a lane makes 4 consecutive x of one row, every channel
+// (one tap-table entry read per x serves all channels), and stores one dword
+// per channel plane.  Source bytes come through the L1 / L2 (a row is re-read
+// by its neighbouring lanes' overlapping spans).
 __global__ void __launch_bounds__(256) pp_horizontal_kernel(const PrepDev* __restrict__ imgs, int res,
                                                             unsigned char* __restrict__ tmp,
                                                             const unsigned char* __restrict__ ws) {
   const PrepDev d = imgs[blockIdx.y];
-  const long long total = (long long)d.nrows * res;
   unsigned char* t = tmp + d.tmp_off;
   const int* tab = d.htab >= 0 ? reinterpret_cast<const int*>(ws + d.htab) : nullptr;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += gridDim.x * 256LL) {
-    const int r = (int)(i / res), x = (int)(i % res);
-    const unsigned char* row = d.src + (long long)(d.row0 + r) * d.pitch;
-    unsigned char* o = t + ((long long)r * res + x) * d.C;
-    if (d.C == 3) pp_hpix<3>(d, row, tab, x, o);
-    else pp_hpix<1>(d, row, tab, x, o);
+  const int C = d.C;
+  const bool vec = (res & 3) == 0;
+  const int xg = vec ? res / 4 : res;
+  const int nx = vec ? 4 : 1;
+  const long long plane = (long long)d.nrows * res;
+  const long long total = (long long)d.nrows * xg;
+  for (long long it = blockIdx.x * 256LL + threadIdx.x; it < total; it += gridDim.x * 256LL) {
+    const int r = (int)(it / xg), g = (int)(it - (it / xg) * xg);
+    const unsigned char* src = d.src + (long long)(d.row0 + r) * d.pitch;
+    const int x0 = vec ? 4 * g : g;
+    unsigned packed[3] = {0u, 0u, 0u};
+    for (int j = 0; j < nx; ++j) {
+      const int x = x0 + j;
+      int acc[3] = {1 << (PP_BITS - 1), 1 << (PP_BITS - 1), 1 << (PP_BITS - 1)};
+      if (!tab) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          if (c < C) acc[c] = (int)src[(d.left + x) * C + c] << PP_BITS;
+      } else {
+        const int* e = tab + (long long)x * (2 + d.hn);
+        const int xmin = e[0], n = e[1];
+        const unsigned char* p = src + xmin * C;
+        if (C == 3) {
+          for (int k = 0; k < n; ++k) {
+            const int w = e[2 + k];
+            acc[0] += (int)p[3 * k] * w;
+            acc[1] += (int)p[3 * k + 1] * w;
+            acc[2] += (int)p[3 * k + 2] * w;
+          }
+        } else {
+          for (int k = 0; k < n; ++k) acc[0] += (int)p[k] * e[2 + k];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) packed[c] |= (unsigned)pp_clip8(acc[c]) << (8 * j);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      if (c >= C) break;
+      unsigned char* o = t + c * plane + (long long)r * res + x0;
+      if (vec) *reinterpret_cast<unsigned*>(o) = packed[c];
+      else *o = (unsigned char)packed[c];
+    }
   }
 }
 
-// vertical pass + RGB + ToTensor + Normalize: out[n][c][y][x] f32
+// vertical pass + RGB + ToTensor + Normalize: out[n][c][y][x] f32 (or the
+// uint8 HWC rows of the augmentation's input); a lane makes 4 consecutive x of
+// one (channel, y): per tap one dword of the planar intermediate, 4 MACs
 __global__ void __launch_bounds__(256) pp_vertical_kernel(const PrepDev* __restrict__ imgs, int res,
                                                           const unsigned char* __restrict__ tmp, float m0, float m1,
                                                           float m2, float s0, float s1, float s2,
@@ -156,32 +178,46 @@ __global__ void __launch_bounds__(256) pp_vertical_kernel(const PrepDev* __restr
   float* o = out ? out + (long long)blockIdx.y * 3 * res * res : nullptr;
   unsigned char* o8 = out_u8 ? out_u8 + (long long)blockIdx.y * 3 * res * res : nullptr;
   const float mean[3] = {m0, m1, m2}, sd[3] = {s0, s1, s2};
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < res * res; i += gridDim.x * 256) {
-    const int y = i / res, x = i % res;
-    const int yo = d.top + y;
-    unsigned char v[3];
+  const bool vec = (res & 3) == 0;
+  const int xg = vec ? res / 4 : res;
+  const long long plane = (long long)d.nrows * res;
+  const int total = 3 * res * xg;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int c = i / (res * xg), rem = i - c * (res * xg);
+    const int y = rem / xg, g = rem - (rem / xg) * xg;
+    const int cs = d.C == 1 ? 0 : c;  // convert('RGB') of a grayscale source: replicate
+    const int nx = vec ? 4 : 1, x0 = vec ? 4 * g : g;
+    const unsigned char* pl = t + cs * plane + x0;
+    unsigned char v[4];
     if (!tab) {
-      for (int c = 0; c < d.C; ++c) v[c] = t[((long long)(yo - d.row0) * res + x) * d.C + c];
+      const unsigned char* p = pl + (long long)(d.top + y - d.row0) * res;
+      for (int j = 0; j < nx; ++j) v[j] = p[j];
     } else {
       const int* e = tab + (long long)y * (2 + d.vn);
       const int ymin = e[0], n = e[1];
-      int acc[3] = {1 << (PP_BITS - 1), 1 << (PP_BITS - 1), 1 << (PP_BITS - 1)};
-      const unsigned char* p = t + ((long long)(ymin - d.row0) * res + x) * d.C;
-      const long long step = (long long)res * d.C;
-      for (int k = 0; k < n; ++k) {
-        const int w = e[2 + k];
-        for (int c = 0; c < d.C; ++c) acc[c] += (int)p[k * step + c] * w;
+      int acc[4] = {1 << (PP_BITS - 1), 1 << (PP_BITS - 1), 1 << (PP_BITS - 1), 1 << (PP_BITS - 1)};
+      const unsigned char* p = pl + (long long)(ymin - d.row0) * res;
+      if (vec) {
+        for (int k = 0; k < n; ++k) {
+          const unsigned q = *reinterpret_cast<const unsigned*>(p + (long long)k * res);
+          const int w = e[2 + k];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] += (int)((q >> (8 * j)) & 255u) * w;
+        }
+      } else {
+        for (int k = 0; k < n; ++k) acc[0] += (int)p[(long long)k * res] * e[2 + k];
       }
-      for (int c = 0; c < d.C; ++c) v[c] = pp_clip8(acc[c]);
+      for (int j = 0; j < nx; ++j) v[j] = pp_clip8(acc[j]);
     }
-    if (o8) {  // uint8 RGB rows (the augmentation's input)
-      for (int c = 0; c < 3; ++c) o8[(long long)i * 3 + c] = v[d.C == 1 ? 0 : c];
+    if (o8) {  // uint8 RGB rows (HWC)
+      for (int j = 0; j < nx; ++j) o8[((long long)y * res + x0 + j) * 3 + c] = v[j];
       continue;
     }
-    for (int c = 0; c < 3; ++c) {
-      const float f = (float)v[d.C == 1 ? 0 : c] / 255.0f;
-      o[(long long)c * res * res + i] = (f - mean[c]) / sd[c];
-    }
+    float f[4];
+    for (int j = 0; j < nx; ++j) f[j] = ((float)v[j] / 255.0f - mean[c]) / sd[c];
+    float* q = o + (long long)c * res * res + (long long)y * res + x0;
+    if (vec) *reinterpret_cast<float4*>(q) = make_float4(f[0], f[1], f[2], f[3]);
+    else q[0] = f[0];
   }
 }
 
@@ -309,13 +345,18 @@ static int pp_run(int n, const artsbir_image_desc* descs, int res, const float* 
   if (e != hipSuccess) { set_error("clip_preprocess: descriptor upload: %s", hipGetErrorString(e)); return -2; }
   const PrepDev* dimgs = reinterpret_cast<const PrepDev*>(workspace);
   unsigned char* tmp = reinterpret_cast<unsigned char*>(workspace);
-  const unsigned gx = (unsigned)((res * res + 255) / 256 < 64 ? (res * res + 255) / 256 : 64);
+  const int xg = (res & 3) == 0 ? res / 4 : res;
+  const unsigned gv = (unsigned)((3 * res * xg + 255) / 256 < 64 ? (3 * res * xg + 255) / 256 : 64);
+  int maxrows = 1;
+  for (int i = 0; i < n; ++i) maxrows = descs[i].H > maxrows ? descs[i].H : maxrows;
+  const long long hwork = (long long)maxrows * xg;
+  const unsigned gh = (unsigned)((hwork + 255) / 256 < 256 ? (hwork + 255) / 256 : 256);
   hipLaunchKernelGGL(pp_coeffs_kernel, dim3((unsigned)((res + 255) / 256), n, 2), dim3(256), 0, st, dimgs, res, tmp);
   ARTSBIR_CHECK_LAUNCH("clip_preprocess coefficients");
-  hipLaunchKernelGGL(pp_horizontal_kernel, dim3(gx * 4, n), dim3(256), 0, st, dimgs, res, tmp,
+  hipLaunchKernelGGL(pp_horizontal_kernel, dim3(gh, n), dim3(256), 0, st, dimgs, res, tmp,
                      (const unsigned char*)tmp);
   ARTSBIR_CHECK_LAUNCH("clip_preprocess horizontal");
-  hipLaunchKernelGGL(pp_vertical_kernel, dim3(gx, n), dim3(256), 0, st, dimgs, res, tmp, mean3[0], mean3[1],
+  hipLaunchKernelGGL(pp_vertical_kernel, dim3(gv, n), dim3(256), 0, st, dimgs, res, tmp, mean3[0], mean3[1],
                      mean3[2], std3[0], std3[1], std3[2], out, out_u8);
   ARTSBIR_CHECK_LAUNCH("clip_preprocess vertical");
   return 0;

@@ -190,7 +190,10 @@ def preprocess_leg(dev, rank, world, n_triplets=384, reps=5):
             "roofline": {"bound": "hbm", "kernel": "pp_horizontal_kernel + pp_vertical_kernel (one call)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "avg_launch_us": round(kern_s * 1e6, 2),
-                         "avg_launch_bytes": in_bytes + out_bytes, "traffic": None}}
+                         "avg_launch_bytes": in_bytes + out_bytes, "traffic": None,
+                         "note": "priced against HBM as the contract asks; the passes are bound by byte-gather "
+                                 "issue (Pillow's integer bicubic taps: ~3 byte loads + 3 MACs per tap and channel, "
+                                 "profiles/r3_preprocess_kernel_stats.csv), not by HBM bytes"}}
 
 
 def cpu_preprocess_baseline(n=96, budget_s=10.0):
