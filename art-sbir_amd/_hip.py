@@ -168,6 +168,7 @@ SIGNATURES = {
     "artsbir_scan_profile": [_c_int],
     "artsbir_knn_set_unc_cap": [_c_int],
     "artsbir_scan_profile_read": [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_int)],
+    "artsbir_knn_stat_read": [ctypes.POINTER(ctypes.c_ulonglong), _c_int],
     "artsbir_topk_merge": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "artsbir_positive_key": [_c_int, _vp, _c_int, _vp, _c_ll, _c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_pairwise_l2_bwd": [_vp, _c_ll, _vp, _c_ll, _c_int, _c_float, _vp, _vp, _vp, _vp, _vp],

@@ -482,6 +482,12 @@ __device__ __forceinline__ float kb_bound(unsigned u, float eps) {
 }
 
 constexpr int V2_ROWS = 32;  // gallery rows per tile
+// tiles between two exchanges of the shared per-query bound (power of two; env
+// ARTSBIR_KNN_KB=0 turns the exchange off in the one-call path)
+#ifndef KB_SYNC_TILES
+#define KB_SYNC_TILES 16
+#endif
+constexpr int KB_SYNC = KB_SYNC_TILES;
 constexpr int V2_WAVES = 8;  // 8 x 32 = 256 queries per workgroup
 
 template <int KB>
@@ -498,8 +504,17 @@ struct V2 {
   static_assert((NI + V2_WAVES - 1) / V2_WAVES <= 5, "rvm_wait_n covers at most 5 DMA per wave");
 };
 
+// scan statistics (diagnostics, ARTSBIR_KNN_STAT=1): wave-tiles, slow-path
+// entries, list insertions, shared-bound exchanges; summed per wave, one
+// atomic per wave at the end
+__device__ unsigned long long g_knn_stat[4];
+static bool knn_stat_on() {
+  static const bool on = [] { const char* e = getenv("ARTSBIR_KNN_STAT"); return e && atoi(e) != 0; }();
+  return on;
+}
+
 template <int KB>
-__global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
+__global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int stat) {
   using C = V2<KB>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   float* s_stage = reinterpret_cast<float*>(smem + C::NST * C::STAGE);
@@ -595,6 +610,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
   float thr_g = s_thr[R_own];  // best shared bound seen (with thr0)
 
   bool atom = false;  // this wave issued a global atomic since its last DMA wait
+  unsigned st_entries = 0, st_ins = 0, st_late = 0;
   for (int t = 0; t < ntiles; ++t) {
     if (t + 2 < ntiles) issue_tile(t + 2);
     const char* st = smem + (t % C::NST) * C::STAGE;
@@ -636,6 +652,8 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[e], gsq) <= critp[e];
     if (__builtin_amdgcn_ballot_w64(any)) {
+      ++st_entries;
+      if (t >= 64) ++st_late;
       // stage the raw dot products of every row with a prefilter hit; the owner
       // of each row re-evaluates its hits exactly (d2 with the same formula as
       // knn_scan_kernel): list insertion, certainly-closer count, uncertain queue
@@ -665,6 +683,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
           const float g2 = stg[c * C::SP + 32];
           const float d2 = fmaf(-2.f, srow[c], qs + g2);
           if (d2 < thr) {
+            ++st_ins;
             float x = d2;
             int xi = bn + c;
 #pragma unroll
@@ -694,19 +713,6 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
         if (changed) {
           s_thr[R_own] = thr;
           s_crit[R_own] = fmaxf(thr, hi);
-          if (a.kb) {  // publish this chunk's k-th smallest
-            float kth = INFINITY;
-#pragma unroll
-            for (int i = 0; i < KT; ++i) kth = (i == a.kq - 1 && lst_i[i] >= 0) ? lst_d[i] : kth;
-            if (kth < INFINITY) {
-              const float g = kb_bound(kb_enc(kth), eps_own);
-              if (g < thr_g) {
-                thr_g = g;
-                atomicMin(a.kb + q_own, kb_enc(kth));
-                atom = true;
-              }
-            }
-          }
         }
       }
       if (__builtin_amdgcn_ballot_w64(changed)) {
@@ -723,12 +729,23 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
         }
       }
     }
-    if (a.kb && (t & 7) == 7 && t + 1 < ntiles) {
-      // every 8 tiles: tighten the thresholds with the bounds other chunks published
+    if (a.kb && (t & (KB_SYNC - 1)) == KB_SYNC - 1 && t + 1 < ntiles) {
+      // every KB_SYNC tiles, the query's bound shared by every chunk (one
+      // returning atomicMin per row): publish this chunk's kq-th smallest so far
+      // and take the best any chunk has published.  The pipeline drains here
+      // once (the atomic's value is used at once), instead of at every list
+      // change: the chunks running beside this one, and those that ran before
+      // it, then cut its slow-path entries to the items that can still reach
+      // the global top k (kb_bound above).
+      rvm_wait<0>();
       bool upd = false;
       if (lane < 32 && q_own < a.Nq) {
-        const unsigned u = __hip_atomic_load(a.kb + q_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const float g = kb_bound(u, eps_own);
+        float kth = INFINITY;
+#pragma unroll
+        for (int i = 0; i < KT; ++i) kth = (i == a.kq - 1 && lst_i[i] >= 0) ? lst_d[i] : kth;
+        const unsigned mine = kb_enc(kth);
+        const unsigned old = atomicMin(a.kb + q_own, mine);
+        const float g = kb_bound(old < mine ? old : mine, eps_own);
         if (g < thr_g) {
           thr_g = g;
           const float cur = s_thr[R_own];
@@ -739,12 +756,22 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a) {
           }
         }
       }
-      atom = true;  // the compiler waited for this load with vmcnt(0) anyway
+      atom = false;  // drained above; the atomic's own completion was waited for at its use
       if (__builtin_amdgcn_ballot_w64(upd)) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         load_crit();
       }
+    }
+  }
+  if (stat) {
+    unsigned ins = st_ins;
+    for (int off = 32; off; off >>= 1) ins += __shfl_xor(ins, off, 64);
+    if (lane == 0) {
+      atomicAdd(&g_knn_stat[0], (unsigned long long)ntiles);
+      atomicAdd(&g_knn_stat[1], (unsigned long long)st_entries);
+      atomicAdd(&g_knn_stat[2], (unsigned long long)ins);
+      atomicAdd(&g_knn_stat[3], (unsigned long long)st_late);
     }
   }
   if (lane < 32) {
@@ -1272,10 +1299,10 @@ extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float*
   const unsigned grid = (unsigned)(a.nchunks * ((nq + 255) / 256));
   hipStream_t s = (hipStream_t)stream;
   switch (Dp) {
-    case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, s, a); break;
-    case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, s, a); break;
-    case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, s, a); break;
-    default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, s, a); break;
+    case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, s, a, 0); break;
+    case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, s, a, 0); break;
+    case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, s, a, 0); break;
+    default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, s, a, 0); break;
   }
   ARTSBIR_CHECK_LAUNCH("knn_scan_aug");
   return 0;
@@ -1304,7 +1331,8 @@ struct TopkPlan {
 constexpr int TOPK_KMAX = 64;
 int g_topk_unc_cap = 1 << 20;  // artsbir_knn_set_unc_cap (tests force the overflow path)
 
-enum { W_QSQ, W_GSQ, W_EXT, W_QEPS, W_QC, W_GC, W_LO, W_HI, W_DPOS, W_CNT, W_UNC, W_CD, W_CI, W_FLAG, W_PK, W_PI, W_END };
+enum { W_QSQ, W_GSQ, W_EXT, W_QEPS, W_QC, W_GC, W_LO, W_HI, W_DPOS, W_CNT, W_UNC, W_CD, W_CI, W_FLAG, W_PK, W_PI, W_KB,
+       W_END };
 
 int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan& p) {
   if (Q < 0 || N < 1 || D < 1 || k < 1 || k > TOPK_KMAX || N > 0x7fffffffLL) {
@@ -1343,6 +1371,7 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   sz[W_CD] = sz[W_CI] = 4 * (size_t)Q * p.ncand;
   sz[W_FLAG] = 4 * (size_t)Q;
   sz[W_PK] = sz[W_PI] = 8 * (size_t)Q * W * k;
+  sz[W_KB] = 4 * (size_t)Q;
   size_t o = 0;
   for (int i = 0; i < W_END; ++i) {
     p.off[i] = o;
@@ -1352,6 +1381,15 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   return 0;
 }
 }  // namespace
+
+extern "C" int artsbir_knn_stat_read(unsigned long long* out4, int reset) {
+  if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_knn_stat), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[4] = {0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_knn_stat), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
 
 extern "C" long long artsbir_pairwise_l2_topk_workspace(int dtype, int Q, long long N, int D, int k,
                                                         int tiles_per_chunk) {
@@ -1392,11 +1430,14 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
   int* flag = reinterpret_cast<int*>(w + p.off[W_FLAG]);
   double* pkey = reinterpret_cast<double*>(w + p.off[W_PK]);
   long long* pidx = reinterpret_cast<long long*>(w + p.off[W_PI]);
+  unsigned* kbuf = reinterpret_cast<unsigned*>(w + p.off[W_KB]);
+  static const bool kb_on = [] { const char* e = getenv("ARTSBIR_KNN_KB"); return !e || atoi(e) != 0; }();
   const int ng = (int)N;
   const float rel = dtype == ARTSBIR_DT_BF16 ? (float)(0x1p-6 + 0x1p-12) : (float)0x1p-14;
 
   if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext), 0, 1, st) != hipSuccess ||
-      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext + 1), 0x7f800000, 1, st) != hipSuccess) {
+      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext + 1), 0x7f800000, 1, st) != hipSuccess ||
+      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kbuf), (int)0xff800000u, Q, st) != hipSuccess) {  // kb_enc(+inf)
     set_error("pairwise_l2_topk: memset failed");
     return -2;
   }
@@ -1428,18 +1469,19 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
   }
   KnnScanArgs a;
   a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.gsq_max_p = reinterpret_cast<const float*>(ext);
-  a.thr0 = nullptr; a.kb = nullptr; a.kq = k; a.rel = rel; a.Nq = Q; a.Ng = ng; a.D = p.Dp;
+  a.thr0 = nullptr; a.kb = (p.v2 && kb_on) ? kbuf : nullptr; a.kq = k; a.rel = rel; a.Nq = Q; a.Ng = ng; a.D = p.Dp;
   a.tiles_per_chunk = p.tpc;
   a.nchunks = p.nchunks;
   a.lo = positives ? lo : nullptr; a.hi = positives ? hi : nullptr;
   a.cnt = cnt; a.unc = unc; a.unc_cap = p.unc_cap; a.cand_d = cand_d; a.cand_i = cand_i;
   if (p.v2) {
     const unsigned grid = (unsigned)(p.nchunks * ((Q + 255) / 256));
+    const int sstat = knn_stat_on() ? 1 : 0;
     switch (p.Dp) {
-      case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, st, a); break;
-      case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, st, a); break;
-      case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, st, a); break;
-      default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, st, a); break;
+      case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, st, a, sstat); break;
+      case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, st, a, sstat); break;
+      case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, st, a, sstat); break;
+      default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, st, a, sstat); break;
     }
     set_last_kernel("knn_scan_v2_kernel");
   } else {
