@@ -488,9 +488,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        # RCCL ("nccl") over xGMI, one GPU per rank; ARTSBIR_DIST_BACKEND=gloo lets
+        # several ranks share one device (a rehearsal of the N > 1 code path)
+        ddp.init_distributed()
+    dev = torch.device("cuda", torch.cuda.current_device())
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
     torch.manual_seed(1234)
