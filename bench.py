@@ -31,12 +31,18 @@ MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}  # MI355X dense
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s measured copy)
 # per-launch HBM bytes of each kernel from the committed rocprofv3 PMC passes
 # (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE; profiles/summarize_pmc.py)
-PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r2b_pmc_traffic.json"))
+# One file per leg: a kernel name pools different launch shapes in each leg
+# (training step + retrieval scan, eval-BN embed pass, C5 ViT step), so a leg's
+# roofline only takes traffic measured on that leg's own launches.
+PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r3_pmc_traffic.json"))
+PMC_TRAFFIC_EMBED = os.environ.get("ARTSBIR_PMC_TRAFFIC_EMBED",
+                                   os.path.join(ROOT, "profiles", "r3_embed_pmc_traffic.json"))
+PMC_TRAFFIC_C5 = os.environ.get("ARTSBIR_PMC_TRAFFIC_C5", os.path.join(ROOT, "profiles", "r3_c5_pmc_traffic.json"))
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, path=None):
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(path or PMC_TRAFFIC) as f:
             ks = json.load(f)["kernels"]
         k = ks.get(kernel) or ks.get(kernel.split("<")[0])  # template arguments not in the profiler name
     except (OSError, ValueError, KeyError):
@@ -90,7 +96,7 @@ def cpu_model():
     return platform.processor() or platform.machine()
 
 
-def roofline(prof, peak_of):
+def roofline(prof, peak_of, traffic_file=None):
     """Roofline of the dominant kernel from a live per-launch profile (_hip.PROFILE
     entries: kernel, algorithmic FLOPs, algorithmic bytes, HIP start / end events
     on the launch's stream).  Launches are pooled by kernel name; the dominant
@@ -120,7 +126,10 @@ def roofline(prof, peak_of):
         achieved = fl / secs / 1e12
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak_fl, "unit": "TFLOP/s",
                 "frac": round(achieved / peak_fl, 4)}
-    roof.update({"traffic": pmc_traffic(dom), "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT),
+    tf = traffic_file or PMC_TRAFFIC
+    traffic = pmc_traffic(dom, tf)
+    roof.update({"traffic": traffic, "traffic_source": os.path.relpath(tf, ROOT) if traffic is not None else None,
+                 "traffic_over_algorithmic": round(traffic / (nb / cnt), 3) if traffic and nb else None,
                  "kernel": dom, "launches": cnt, "avg_launch_us": round(secs / cnt * 1e6, 2),
                  "avg_launch_flops": fl / cnt, "avg_launch_bytes": nb / cnt,
                  "intensity_flop_per_byte": round(fl / nb, 1) if nb else None,
@@ -422,7 +431,7 @@ def embed_leg(model, batch, dtype_name, world, reps):
     gpu_s = sum(e0.elapsed_time(e1) for _, _, _, e0, e1, *_ in prof) / 1e3
     fl = encoder_flops_per_image() * images / world
     # the dominant kernel of the pass, priced per launch like the step's
-    roof = roofline(prof, lambda k: MFMA_PEAK_TFLOPS[dtype_name]) if prof else None
+    roof = roofline(prof, lambda k: MFMA_PEAK_TFLOPS[dtype_name], PMC_TRAFFIC_EMBED) if prof else None
     return {"metric": "triplet-images/s embedded (eval BatchNorm, no backward)", "value": round(images / el, 2),
             "unit": "triplet-images/s", "ms_per_pass": round(el / reps * 1e3, 3), "n_gpus": world,
             "images_per_pass": sum(x.shape[0] for x in batch), "dtype": dtype_name,
@@ -726,7 +735,7 @@ def c5_leg(dev, rank, world, B, steps, warmup=1, profile=True, loss_check=True):
             step()
         torch.cuda.synchronize()
         _hip.PROFILE = None
-        roof = roofline(prof, lambda k: MFMA_PEAK_TFLOPS["fp8" if "fp8" in k else "bf16"])
+        roof = roofline(prof, lambda k: MFMA_PEAK_TFLOPS["fp8" if "fp8" in k else "bf16"], PMC_TRAFFIC_C5)
     images = 3 * B * world * steps
     flops = 3 * 35.1e9 * images
     out = {"metric": "triplet-images/sec, ViT-B/16 768-d fp8 (C5)", "value": round(images / el, 2),

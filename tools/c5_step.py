@@ -15,6 +15,13 @@ import vit  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 128
 mode = sys.argv[2] if len(sys.argv) > 2 else "fp8"
 dev = torch.device("cuda", 0)
+# ARTSBIR_TUNE_CACHE: autotuner choices loaded when the file exists, saved after
+# the first step (a profiled re-run then launches no tuning trials)
+tc = os.environ.get("ARTSBIR_TUNE_CACHE")
+if tc and os.path.exists(tc):
+    import _hip
+    if _hip.lib().artsbir_tune_load(tc.encode()) < 0:
+        raise RuntimeError(_hip.lib().artsbir_last_error().decode())
 torch.manual_seed(1)
 m = vit.VisionTransformer(224, 16, 768, 12, 12, 768).to(dev)
 m.compute_dtype = {"fp8": "fp8", "bf16": torch.bfloat16}[mode]
@@ -33,4 +40,7 @@ for it in range(3):
     opt.step()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
+    if it == 0 and tc:
+        import _hip
+        _hip.lib().artsbir_tune_save(tc.encode())
     print(f"step {it}: fwd {1e3 * (t1 - t0):.1f} ms, bwd+adam {1e3 * (t2 - t1):.1f} ms", flush=True)
