@@ -194,6 +194,8 @@ struct KnnScanArgs {
   const float* gsq_max_p;  // knn_scan_v2: if set, max |g|^2 read from device memory (one-call path, no host sync)
   const float* thr0;  // knn_scan_v2: optional per-query initial list threshold (see knn.py)
   unsigned* kb;       // knn_scan_v2: optional [Nq] shared k-th bound (kb_enc of an approx d2), atomicMin
+  unsigned* hist;     // knn_scan_v2 (with kb): optional [Nq][HB_BINS] counts of published list items (zeroed)
+  unsigned* hbase;    //   [Nq] the histogram's first bin key (0: not chosen yet; zeroed)
   int kq;             //   k of the final top-k (1..KT)
   float rel;          //   error bound factor of the approximate d2 (eps = rel |q| max|g| + 1e-3)
   int Nq, Ng, D;
@@ -481,11 +483,46 @@ __device__ __forceinline__ float kb_bound(unsigned u, float eps) {
   return (v + 2.f * eps) * (1.f + 0x1p-18f) + 1e-3f;
 }
 
+// Per-query histogram of the approximate d2 of published list items: bins of
+// 2^-7 octave (the float's exponent and top 7 mantissa bits), HB_BINS of them
+// from a base key chosen once per query (atomicCAS, from the first chunk to
+// publish: its kq-th smallest + 2 eps is the top bin).  A gallery item is
+// counted at most once (each chunk publishes the list items it inserted since
+// its previous exchange, once), so when the counts of bins <= b reach kq, at
+// least kq distinct items have approx d2 < hb_edge(b): an upper bound of the
+// gallery's kq-th smallest approx d2, exactly what kb holds (kb_bound).  Unlike
+// one chunk's own kq-th smallest it tightens with everything every chunk has
+// scanned so far: 570 -> ~130 items per query under the bound by mid-scan at
+// C4 (1M x 512, randn rows).
+constexpr int HB_BINS = 64;
+__device__ __forceinline__ unsigned hb_key(float v) { return v > 0.f ? __float_as_uint(v) >> 16 : 0u; }
+__device__ __forceinline__ int hb_bin(float v, unsigned base) {
+  const unsigned kk = hb_key(v);
+  return kk <= base ? 0 : (int)min(kk - base, (unsigned)HB_BINS);  // HB_BINS: above the top bin, not counted
+}
+__device__ __forceinline__ float hb_edge(unsigned base, int b) { return __uint_as_float((base + b + 1) << 16); }
+// the smallest bin edge with >= kq counted items below it (+INF if none); the
+// counts are read at agent scope (other XCDs' adds are not in this XCD's L2)
+__device__ float hb_bound(const unsigned* hq, unsigned base, int kq) {
+  unsigned cum = 0;
+  for (int b0 = 0; b0 < HB_BINS; b0 += 8) {
+    unsigned c[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = __hip_atomic_load(hq + b0 + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      cum += c[j];
+      if (cum >= (unsigned)kq) return hb_edge(base, b0 + j);
+    }
+  }
+  return INFINITY;
+}
+
 constexpr int V2_ROWS = 32;  // gallery rows per tile
 // tiles between two exchanges of the shared per-query bound (power of two; env
 // ARTSBIR_KNN_KB=0 turns the exchange off in the one-call path)
 #ifndef KB_SYNC_TILES
-#define KB_SYNC_TILES 16
+#define KB_SYNC_TILES 64
 #endif
 constexpr int KB_SYNC = KB_SYNC_TILES;
 constexpr int V2_WAVES = 8;  // 8 x 32 = 256 queries per workgroup
@@ -608,6 +645,8 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   const int q_own = qb + R_own;
   const float eps_own = q_own < a.Nq ? a.rel * sqrtf(a.qsq[q_own] * gmax) * 1.001f + 1e-3f : 0.f;
   float thr_g = s_thr[R_own];  // best shared bound seen (with thr0)
+  int pub_wm = g0;              // list items with a gallery index >= pub_wm are not yet in the histogram
+  unsigned hbq = 0;             // the query's histogram base key (0: not known yet)
 
   bool atom = false;  // this wave issued a global atomic since its last DMA wait
   unsigned st_entries = 0, st_ins = 0, st_late = 0;
@@ -686,10 +725,13 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
             ++st_ins;
             float x = d2;
             int xi = bn + c;
+            // compare-swap down the sorted list.  Items reach a chunk's list in
+            // increasing gallery index (tiles in order, columns in ctz order), so
+            // a listed item equal in value always has the lower index and stays
+            // ahead: the strict compare alone keeps the (value, index) order
 #pragma unroll
-            for (int i = 0; i < KT; ++i) {  // compare-swap down the sorted list
-              // branch-free (the short-circuit form compiles to an exec-mask branch per step)
-              const bool sw = (int)(x < lst_d[i]) | ((int)(x == lst_d[i]) & (int)(xi < lst_i[i]) & (int)(lst_i[i] >= 0));
+            for (int i = 0; i < KT; ++i) {
+              const bool sw = x < lst_d[i];
               const float td = lst_d[i];
               const int ti = lst_i[i];
               lst_d[i] = sw ? x : td;
@@ -738,12 +780,39 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
       // it, then cut its slow-path entries to the items that can still reach
       // the global top k (kb_bound above).
       rvm_wait<0>();
-      bool upd = false;
+      bool upd = false, pub = false;
       if (lane < 32 && q_own < a.Nq) {
         float kth = INFINITY;
 #pragma unroll
         for (int i = 0; i < KT; ++i) kth = (i == a.kq - 1 && lst_i[i] >= 0) ? lst_d[i] : kth;
-        const unsigned mine = kb_enc(kth);
+        float bnd = kth;
+        if (a.hist) {
+          if (!hbq) {
+            if (kth < INFINITY) {
+              const unsigned want = max(hb_key(kth + 2.f * eps_own), (unsigned)HB_BINS) - (HB_BINS - 1);
+              const unsigned old = atomicCAS(a.hbase + q_own, 0u, want);
+              hbq = old ? old : want;
+            } else {
+              hbq = __hip_atomic_load(a.hbase + q_own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+          if (hbq) {
+            unsigned* hq = a.hist + (long long)q_own * HB_BINS;
+#pragma unroll
+            for (int i = 0; i < KT; ++i) {
+              if (lst_i[i] >= pub_wm) {
+                const int b = hb_bin(lst_d[i], hbq);
+                if (b < HB_BINS) {
+                  atomicAdd(hq + b, 1u);
+                  pub = true;
+                }
+              }
+            }
+            pub_wm = g0 + (t + 1) * V2_ROWS;
+            if (pub) bnd = fminf(bnd, hb_bound(hq, hbq, a.kq));
+          }
+        }
+        const unsigned mine = kb_enc(bnd);
         const unsigned old = atomicMin(a.kb + q_own, mine);
         const float g = kb_bound(old < mine ? old : mine, eps_own);
         if (g < thr_g) {
@@ -756,7 +825,9 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
           }
         }
       }
-      atom = false;  // drained above; the atomic's own completion was waited for at its use
+      // drained above; the returning atomics were waited for at their use, the
+      // histogram adds were not: they force the next tile's full wait
+      atom = pub;
       if (__builtin_amdgcn_ballot_w64(upd)) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1224,7 +1295,7 @@ extern "C" int artsbir_knn_scan(int dtype, const void* qc, const void* gc, const
   if (D % (8 * EPC)) { set_error("knn_scan: D=%d must be a multiple of %d", D, 8 * EPC); return -1; }
   if (nq <= 0 || ng <= 0) return 0;
   KnnScanArgs a;
-  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.gsq_max_p = nullptr; a.thr0 = nullptr; a.kb = nullptr; a.kq = 0; a.rel = 0.f; a.Nq = nq; a.Ng = ng; a.D = D;
+  a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.gsq_max_p = nullptr; a.thr0 = nullptr; a.kb = nullptr; a.hist = nullptr; a.hbase = nullptr; a.kq = 0; a.rel = 0.f; a.Nq = nq; a.Ng = ng; a.D = D;
   a.tiles_per_chunk = tiles_per_chunk;
   const int tiles = (ng + 127) / 128;
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
@@ -1291,7 +1362,7 @@ extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float*
   if (kbound && (k < 1 || k > KT)) { set_error("knn_scan_aug: k=%d must be in 1..%d with a shared bound", k, KT); return -1; }
   if (nq <= 0 || ng <= 0) return 0;
   KnnScanArgs a;
-  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.gsq_max_p = nullptr; a.thr0 = thr0; a.kb = kbound; a.kq = k; a.rel = rel; a.Nq = nq; a.Ng = ng; a.D = Dp;
+  a.q = qc; a.g = ga; a.qsq = qsq; a.gsq = nullptr; a.gsq_max = gsq_max; a.gsq_max_p = nullptr; a.thr0 = thr0; a.kb = kbound; a.hist = nullptr; a.hbase = nullptr; a.kq = k; a.rel = rel; a.Nq = nq; a.Ng = ng; a.D = Dp;
   a.tiles_per_chunk = tiles_per_chunk;
   const int tiles = (ng + 127) / 128;
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
@@ -1332,7 +1403,7 @@ constexpr int TOPK_KMAX = 64;
 int g_topk_unc_cap = 1 << 20;  // artsbir_knn_set_unc_cap (tests force the overflow path)
 
 enum { W_QSQ, W_GSQ, W_EXT, W_QEPS, W_QC, W_GC, W_LO, W_HI, W_DPOS, W_CNT, W_UNC, W_CD, W_CI, W_FLAG, W_PK, W_PI, W_KB,
-       W_END };
+       W_HB, W_HIST, W_END };
 
 int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan& p) {
   if (Q < 0 || N < 1 || D < 1 || k < 1 || k > TOPK_KMAX || N > 0x7fffffffLL) {
@@ -1372,6 +1443,8 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   sz[W_FLAG] = 4 * (size_t)Q;
   sz[W_PK] = sz[W_PI] = 8 * (size_t)Q * W * k;
   sz[W_KB] = 4 * (size_t)Q;
+  sz[W_HB] = 4 * (size_t)Q;
+  sz[W_HIST] = 4 * (size_t)Q * HB_BINS;
   size_t o = 0;
   for (int i = 0; i < W_END; ++i) {
     p.off[i] = o;
@@ -1432,12 +1505,17 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
   long long* pidx = reinterpret_cast<long long*>(w + p.off[W_PI]);
   unsigned* kbuf = reinterpret_cast<unsigned*>(w + p.off[W_KB]);
   static const bool kb_on = [] { const char* e = getenv("ARTSBIR_KNN_KB"); return !e || atoi(e) != 0; }();
+  // the published-item histogram tightening kb (ARTSBIR_KNN_HIST=0: kb from each chunk's own k-th only)
+  static const bool hist_on = [] { const char* e = getenv("ARTSBIR_KNN_HIST"); return !e || atoi(e) != 0; }();
+  unsigned* hbase = reinterpret_cast<unsigned*>(w + p.off[W_HB]);
+  unsigned* hist = reinterpret_cast<unsigned*>(w + p.off[W_HIST]);
   const int ng = (int)N;
   const float rel = dtype == ARTSBIR_DT_BF16 ? (float)(0x1p-6 + 0x1p-12) : (float)0x1p-14;
 
   if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext), 0, 1, st) != hipSuccess ||
       hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ext + 1), 0x7f800000, 1, st) != hipSuccess ||
-      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kbuf), (int)0xff800000u, Q, st) != hipSuccess) {  // kb_enc(+inf)
+      hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(kbuf), (int)0xff800000u, Q, st) != hipSuccess ||  // kb_enc(+inf)
+      hipMemsetAsync(w + p.off[W_HB], 0, p.off[W_HIST] - p.off[W_HB] + 4 * (size_t)Q * HB_BINS, st) != hipSuccess) {
     set_error("pairwise_l2_topk: memset failed");
     return -2;
   }
@@ -1469,7 +1547,8 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
   }
   KnnScanArgs a;
   a.q = qc; a.g = gc; a.qsq = qsq; a.gsq = gsq; a.gsq_max = 0.f; a.gsq_max_p = reinterpret_cast<const float*>(ext);
-  a.thr0 = nullptr; a.kb = (p.v2 && kb_on) ? kbuf : nullptr; a.kq = k; a.rel = rel; a.Nq = Q; a.Ng = ng; a.D = p.Dp;
+  a.thr0 = nullptr; a.kb = (p.v2 && kb_on) ? kbuf : nullptr; a.kq = k;
+  a.hist = a.kb && hist_on ? hist : nullptr; a.hbase = a.hist ? hbase : nullptr; a.rel = rel; a.Nq = Q; a.Ng = ng; a.D = p.Dp;
   a.tiles_per_chunk = p.tpc;
   a.nchunks = p.nchunks;
   a.lo = positives ? lo : nullptr; a.hi = positives ? hi : nullptr;
