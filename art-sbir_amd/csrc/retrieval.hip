@@ -81,6 +81,26 @@ __device__ __forceinline__ float row_scale(const float* r, int D, int lane, int 
   return (float)(1.0 / fmax(sqrt(s), 1e-8));
 }
 
+// Rows whose columns allow 16-B loads are read 8 consecutive columns per lane
+// (columns lane*8 + 512 j + i); rows_prep and rows_prep_aug both sum |x|^2 in
+// that order then, so the two give bit-identical norms (the two scans must
+// see the same d2); other rows column-strided per lane, in both.
+__device__ __forceinline__ bool row_vec_ok(const float* r, int D) {
+  return (D & 3) == 0 && (reinterpret_cast<unsigned long long>(r) & 15) == 0;
+}
+__device__ __forceinline__ void row_load8(const float* r, int D, int d0, float sc, float* v) {
+  if (d0 + 8 <= D) {
+    const float4 a = *reinterpret_cast<const float4*>(r + d0);
+    const float4 b = *reinterpret_cast<const float4*>(r + d0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = d0 + j < D ? r[d0 + j] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] *= sc;
+}
+
 template <typename T>
 __global__ void rows_prep_kernel(const float* __restrict__ x, int n, int D, float* __restrict__ sq, T* __restrict__ xc,
                                  int ldc, int normalize) {
@@ -90,10 +110,22 @@ __global__ void rows_prep_kernel(const float* __restrict__ x, int n, int D, floa
   const float* r = x + (long long)row * D;
   const float sc = row_scale(r, D, lane, normalize);
   float s = 0.f;
-  for (int d = lane; d < ldc; d += 64) {  // the compute copy is zero-padded to ldc columns
-    const float v = d < D ? r[d] * sc : 0.f;
-    s += v * v;
-    if (xc) xc[(long long)row * ldc + d] = from_f<T>(v);
+  if (row_vec_ok(r, D)) {
+    for (int d0 = lane * 8; d0 < ldc; d0 += 512) {
+      float v[8];
+      row_load8(r, D, d0, sc, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s = fmaf(v[j], v[j], s);  // explicit fma: the same rounding in both kernels
+        if (xc && d0 + j < ldc) xc[(long long)row * ldc + d0 + j] = from_f<T>(v[j]);
+      }
+    }
+  } else {
+    for (int d = lane; d < ldc; d += 64) {  // the compute copy is zero-padded to ldc columns
+      const float v = d < D ? r[d] * sc : 0.f;
+      s = fmaf(v, v, s);
+      if (xc) xc[(long long)row * ldc + d] = from_f<T>(v);
+    }
   }
   s = warp_sum(s);
   if (lane == 0) sq[row] = s;
@@ -870,10 +902,26 @@ __global__ void rows_prep_aug_kernel(const float* __restrict__ x, int n, int D, 
   const float sc = row_scale(r, D, lane, normalize);
   bf16* o = xa + (long long)row * (Dp + 8);
   float s = 0.f;
-  for (int d = lane; d < Dp; d += 64) {
-    const float v = d < D ? r[d] * sc : 0.f;
-    s += v * v;
-    o[d] = (bf16)v;
+  if (row_vec_ok(r, D)) {
+    // 8 consecutive columns per lane: two 16-B loads, one 16-B store of the
+    // bf16 copy (the row pitch 2 (Dp + 8) B is a multiple of 16)
+    for (int d0 = lane * 8; d0 < Dp; d0 += 512) {
+      float v[8];
+      row_load8(r, D, d0, sc, v);
+      bf16 h[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s = fmaf(v[j], v[j], s);  // explicit fma: the same rounding in both kernels
+        h[j] = (bf16)v[j];
+      }
+      *reinterpret_cast<uint4*>(o + d0) = *reinterpret_cast<const uint4*>(h);
+    }
+  } else {
+    for (int d = lane; d < Dp; d += 64) {
+      const float v = d < D ? r[d] * sc : 0.f;
+      s = fmaf(v, v, s);
+      o[d] = (bf16)v;
+    }
   }
   s = warp_sum(s);
   if (lane < 8) {
@@ -994,6 +1042,181 @@ __global__ void __launch_bounds__(256) knn_merge_kernel(const float* __restrict_
     if (n_g > 0 && valid < (n_g < k ? n_g : (long long)k)) bad = 1;
     flag[qi] = bad;
   }
+}
+
+// The same merge with one wave per query and no workgroup barriers (the block
+// version above spends most of its time in k rounds of block-wide argmin
+// behind __syncthreads): the candidates of a query sit in registers, NPL per
+// lane (nc <= 64 NPL); a_k by bisection over their order-preserving u32 keys;
+// the live candidates compacted into LDS by ballot; their exact keys four at a
+// time (more gathers in flight per wave; each key summed in exactly the order
+// of exact_key, so results are bit-identical); k rounds of wave argmin on
+// (exact key, index).  Outputs, flag and semantics as knn_merge_kernel.
+__device__ __forceinline__ void exact_keys4(const float* q, const float* const* gr, int n, int D, int lane, int metric,
+                                            double* out) {
+  double s0[4] = {0.0, 0.0, 0.0, 0.0}, s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int d = lane; d < D; d += 64) {
+    const double a = q[d];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u < n) {
+        const double b = gr[u][d];
+        if (metric == 0) {
+          const double t = (a - b) + 1e-6;
+          s0[u] += t * t;
+        } else {
+          s0[u] += a * b;
+          s1[u] += a * a;
+          s2[u] += b * b;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s0[u] += __shfl_xor(s0[u], o, 64);
+      if (metric) {
+        s1[u] += __shfl_xor(s1[u], o, 64);
+        s2[u] += __shfl_xor(s2[u], o, 64);
+      }
+    }
+    out[u] = metric == 0 ? sqrt(s0[u]) : 1.0 - s0[u] / (fmax(sqrt(s1[u]), 1e-8) * fmax(sqrt(s2[u]), 1e-8));
+  }
+}
+
+template <int NPL>
+__global__ void __launch_bounds__(64) knn_merge_wave_kernel(const float* __restrict__ q, const float* __restrict__ g,
+                                                            int D, int nchunks, const float* __restrict__ cand_d,
+                                                            const int* __restrict__ cand_i,
+                                                            const float* __restrict__ qsq, float gsq_max, float rel,
+                                                            long long g_base, int k, long long* __restrict__ out_i,
+                                                            double* __restrict__ out_d, int* __restrict__ flag,
+                                                            int metric, const float* __restrict__ qeps, long long n_g) {
+  extern __shared__ char sm[];
+  const int nc = nchunks * KT;
+  double* ed = reinterpret_cast<double*>(sm);  // [nc] exact keys of the live candidates (compacted)
+  int* ei = reinterpret_cast<int*>(ed + nc);   // [nc] their gallery indices (-1: taken)
+  const int qi = blockIdx.x, lane = threadIdx.x;
+  const float* qr = q + (long long)qi * D;
+  const float* cd = cand_d + (long long)qi * nc;
+  const int* ci = cand_i + (long long)qi * nc;
+  const double eps = qeps ? (double)qeps[qi] : rel * sqrt((double)qsq[qi] * gsq_max) + 1e-3;
+  float av[NPL];
+  int ai[NPL];
+  unsigned nvalid = 0;
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    const int c = lane + 64 * j;
+    ai[j] = c < nc ? ci[c] : -1;
+    av[j] = ai[j] >= 0 ? cd[c] : INFINITY;
+    nvalid += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(ai[j] >= 0));
+  }
+  // (1) a_k, the k-th smallest approximate value (as knn_merge_kernel step 1)
+  double ak = INFINITY;
+  if (nvalid >= (unsigned)k) {
+    unsigned lo = 0u, hi = 0xffffffffu;
+    while (lo < hi) {
+      const unsigned mid = lo + ((hi - lo) >> 1);
+      unsigned cnt = 0;
+#pragma unroll
+      for (int j = 0; j < NPL; ++j)
+        cnt += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(ai[j] >= 0 && kb_enc(av[j]) <= mid));
+      if (cnt >= (unsigned)k) hi = mid; else lo = mid + 1;
+    }
+    ak = (double)kb_dec(lo);
+  }
+  const double cut = ak + 2.0 * eps;
+  // (2) compact the live candidates
+  int L = 0;
+#pragma unroll
+  for (int j = 0; j < NPL; ++j) {
+    const bool live = ai[j] >= 0 && (double)av[j] <= cut;
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(live);
+    if (live) {
+      const int pos = L + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      ei[pos] = ai[j];
+    }
+    L += (int)__popcll(m);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // (3) exact keys, four candidates per pass
+  for (int j0 = 0; j0 < L; j0 += 4) {
+    const int n = min(4, L - j0);
+    const float* gr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gr[u] = g + (long long)ei[j0 + (u < n ? u : 0)] * D;
+    double kk[4];
+    exact_keys4(qr, gr, n, D, lane, metric, kk);
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (u < n) ed[j0 + u] = kk[u];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // (4) k rounds of wave argmin on (exact key, index)
+  double kth = INFINITY;
+  for (int r = 0; r < k; ++r) {
+    double bd = INFINITY;
+    int bi = 0x7fffffff, bs = -1;
+    for (int j = lane; j < L; j += 64) {
+      const int i = ei[j];
+      const double d = ed[j];
+      if (i >= 0 && (d < bd || (d == bd && i < bi))) { bd = d; bi = i; bs = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const double od = __shfl_xor(bd, o, 64);
+      const int oi = __shfl_xor(bi, o, 64), os = __shfl_xor(bs, o, 64);
+      if (od < bd || (od == bd && oi < bi)) { bd = od; bi = oi; bs = os; }
+    }
+    if (lane == 0) {
+      out_i[(long long)qi * k + r] = bs >= 0 ? g_base + bi : -1;
+      out_d[(long long)qi * k + r] = bd;
+      if (bs >= 0) ei[bs] = -1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    kth = bd;
+  }
+  // (5) verification, as knn_merge_kernel
+  int bad = 0;
+  long long valid = 0;
+  for (int c = lane; c < nchunks; c += 64) {
+    const float last = cd[c * KT + KT - 1];
+    if (ci[c * KT + KT - 1] >= 0 && (double)last - eps <= key_d2(kth, metric)) bad = 1;
+  }
+  valid = nvalid;
+  bad = __builtin_amdgcn_ballot_w64(bad != 0) != 0;
+  if (n_g > 0 && valid < (n_g < k ? n_g : (long long)k)) bad = 1;
+  if (lane == 0) flag[qi] = bad;
+}
+
+// launches the one-wave merge when the candidates fit its registers (nc <= 1024)
+static bool launch_merge_wave(int Q, hipStream_t st, const float* q, const float* g, int D, int nchunks,
+                              const float* cand_d, const int* cand_i, const float* qsq, float gsq_max, float rel,
+                              long long g_base, int k, long long* out_i, double* out_d, int* flag, int metric,
+                              const float* qeps, long long n_g) {
+  static const bool on = [] { const char* e = getenv("ARTSBIR_KNN_MERGE_WAVE"); return !e || atoi(e) != 0; }();
+  const int nc = nchunks * KT;
+  if (!on || nc > 1024) return false;
+  const size_t sh = (size_t)nc * (sizeof(double) + sizeof(int));
+#define ARTSBIR_MW(NPL)                                                                                            \
+  hipLaunchKernelGGL(knn_merge_wave_kernel<NPL>, dim3(Q), dim3(64), sh, st, q, g, D, nchunks, cand_d, cand_i, qsq, \
+                     gsq_max, rel, g_base, k, out_i, out_d, flag, metric, qeps, n_g)
+  if (nc <= 128) ARTSBIR_MW(2);
+  else if (nc <= 256) ARTSBIR_MW(4);
+  else if (nc <= 512) ARTSBIR_MW(8);
+  else ARTSBIR_MW(16);
+#undef ARTSBIR_MW
+  return true;
 }
 
 // exact checks of the uncertain items of the rank count
@@ -1316,8 +1539,10 @@ extern "C" int artsbir_knn_merge(const float* q, const float* g, int D, int nq, 
   if (k > nchunks * KT) { set_error("knn_merge: k=%d exceeds candidates %d", k, nchunks * KT); return -1; }
   const size_t sh = (size_t)nchunks * KT * (sizeof(double) + sizeof(int));
   if (sh > 60000) { set_error("knn_merge: too many candidates (%d chunks)", nchunks); return -1; }
-  hipLaunchKernelGGL(knn_merge_kernel, dim3(nq), dim3(256), sh, (hipStream_t)stream, q, g, D, nchunks, cand_d, cand_i,
-                     qsq, gsq_max, rel, g_base, k, out_i, out_d, flag, 0, nullptr, 0LL);
+  if (!launch_merge_wave(nq, (hipStream_t)stream, q, g, D, nchunks, cand_d, cand_i, qsq, gsq_max, rel, g_base, k, out_i,
+                         out_d, flag, 0, nullptr, 0LL))
+    hipLaunchKernelGGL(knn_merge_kernel, dim3(nq), dim3(256), sh, (hipStream_t)stream, q, g, D, nchunks, cand_d, cand_i,
+                       qsq, gsq_max, rel, g_base, k, out_i, out_d, flag, 0, nullptr, 0LL);
   ARTSBIR_CHECK_LAUNCH("knn_merge");
   return 0;
 }
@@ -1575,8 +1800,10 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
   ARTSBIR_CHECK_LAUNCH("pairwise_l2_topk scan");
   if (ev1) (void)hipEventRecord(ev1, st);
   const size_t sh = (size_t)p.ncand * (sizeof(double) + sizeof(int));
-  hipLaunchKernelGGL(knn_merge_kernel, dim3(Q), dim3(256), sh, st, q, g, D, p.nchunks, cand_d, cand_i, qsq, 0.f, rel,
-                     g_base, k, out_idx, out_dist, flag, metric, qeps, N);
+  if (!launch_merge_wave(Q, st, q, g, D, p.nchunks, cand_d, cand_i, qsq, 0.f, rel, g_base, k, out_idx, out_dist, flag,
+                         metric, qeps, N))
+    hipLaunchKernelGGL(knn_merge_kernel, dim3(Q), dim3(256), sh, st, q, g, D, p.nchunks, cand_d, cand_i, qsq, 0.f, rel,
+                       g_base, k, out_idx, out_dist, flag, metric, qeps, N);
   if (positives) {
     hipLaunchKernelGGL(knn_uncertain_kernel, dim3(1024), dim3(256), 0, st, q, g, D, unc, p.unc_cap, dpos, positives,
                        g_base, cnt, metric);
