@@ -574,8 +574,8 @@ struct V2 {
 };
 
 // scan statistics (diagnostics, ARTSBIR_KNN_STAT=1): wave-tiles, slow-path
-// entries, list insertions, shared-bound exchanges; summed per wave, one
-// atomic per wave at the end
+// entries, list insertions (summed per wave, one atomic per wave at the end)
+// and the exact merge's live candidates (summed over queries)
 __device__ unsigned long long g_knn_stat[4];
 static bool knn_stat_on() {
   static const bool on = [] { const char* e = getenv("ARTSBIR_KNN_STAT"); return e && atoi(e) != 0; }();
@@ -681,7 +681,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   unsigned hbq = 0;             // the query's histogram base key (0: not known yet)
 
   bool atom = false;  // this wave issued a global atomic since its last DMA wait
-  unsigned st_entries = 0, st_ins = 0, st_late = 0;
+  unsigned st_entries = 0, st_ins = 0;
   for (int t = 0; t < ntiles; ++t) {
     if (t + 2 < ntiles) issue_tile(t + 2);
     const char* st = smem + (t % C::NST) * C::STAGE;
@@ -724,7 +724,6 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[e], gsq) <= critp[e];
     if (__builtin_amdgcn_ballot_w64(any)) {
       ++st_entries;
-      if (t >= 64) ++st_late;
       // stage the raw dot products of every row with a prefilter hit; the owner
       // of each row re-evaluates its hits exactly (d2 with the same formula as
       // knn_scan_kernel): list insertion, certainly-closer count, uncertain queue
@@ -874,7 +873,6 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
       atomicAdd(&g_knn_stat[0], (unsigned long long)ntiles);
       atomicAdd(&g_knn_stat[1], (unsigned long long)st_entries);
       atomicAdd(&g_knn_stat[2], (unsigned long long)ins);
-      atomicAdd(&g_knn_stat[3], (unsigned long long)st_late);
     }
   }
   if (lane < 32) {
@@ -1086,6 +1084,50 @@ __device__ __forceinline__ void exact_keys4(const float* q, const float* const* 
   }
 }
 
+// the same keys with the whole rows loaded first (D <= 64 NI): every gather of a
+// pass is in flight at once instead of one column block per round trip; the
+// per-lane sums still run over d = lane, lane + 64, ... in order, so the keys
+// are bit-identical to exact_key's
+template <int NI>
+__device__ __forceinline__ void exact_keys4_reg(const float* qreg, const float* const* gr, int n, int D, int lane,
+                                                int metric, double* out) {
+  // unconditional loads (clamped column; rows u >= n repeat row 0) so that all
+  // 4 NI gathers are in flight together: a predicated load compiles to a branch
+  // with a wait at its join, one round trip per load
+  float gv[4][NI];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) gv[u][i] = gr[u][min(lane + 64 * i, D - 1)];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      if (lane + 64 * i < D) {
+        const double a = qreg[i], b = gv[u][i];
+        if (metric == 0) {
+          const double t = (a - b) + 1e-6;
+          s0 += t * t;
+        } else {
+          s0 += a * b;
+          s1 += a * a;
+          s2 += b * b;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o, 64);
+      if (metric) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+    }
+    out[u] = metric == 0 ? sqrt(s0) : 1.0 - s0 / (fmax(sqrt(s1), 1e-8) * fmax(sqrt(s2), 1e-8));
+  }
+}
+
 template <int NPL>
 __global__ void __launch_bounds__(64) knn_merge_wave_kernel(const float* __restrict__ q, const float* __restrict__ g,
                                                             int D, int nchunks, const float* __restrict__ cand_d,
@@ -1093,7 +1135,8 @@ __global__ void __launch_bounds__(64) knn_merge_wave_kernel(const float* __restr
                                                             const float* __restrict__ qsq, float gsq_max, float rel,
                                                             long long g_base, int k, long long* __restrict__ out_i,
                                                             double* __restrict__ out_d, int* __restrict__ flag,
-                                                            int metric, const float* __restrict__ qeps, long long n_g) {
+                                                            int metric, const float* __restrict__ qeps, long long n_g,
+                                                            int stat) {
   extern __shared__ char sm[];
   const int nc = nchunks * KT;
   double* ed = reinterpret_cast<double*>(sm);  // [nc] exact keys of the live candidates (compacted)
@@ -1107,10 +1150,15 @@ __global__ void __launch_bounds__(64) knn_merge_wave_kernel(const float* __restr
   int ai[NPL];
   unsigned nvalid = 0;
 #pragma unroll
+  for (int j = 0; j < NPL; ++j) {  // unconditional (clamped) loads, masked after
+    const int c = min(lane + 64 * j, nc - 1);
+    ai[j] = ci[c];
+    av[j] = cd[c];
+  }
+#pragma unroll
   for (int j = 0; j < NPL; ++j) {
-    const int c = lane + 64 * j;
-    ai[j] = c < nc ? ci[c] : -1;
-    av[j] = ai[j] >= 0 ? cd[c] : INFINITY;
+    if (lane + 64 * j >= nc) ai[j] = -1;
+    if (ai[j] < 0) av[j] = INFINITY;
     nvalid += (unsigned)__popcll(__builtin_amdgcn_ballot_w64(ai[j] >= 0));
   }
   // (1) a_k, the k-th smallest approximate value (as knn_merge_kernel step 1)
@@ -1140,17 +1188,25 @@ __global__ void __launch_bounds__(64) knn_merge_wave_kernel(const float* __restr
     }
     L += (int)__popcll(m);
   }
+  if (stat && lane == 0) atomicAdd(&g_knn_stat[3], (unsigned long long)L);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // (3) exact keys, four candidates per pass
+  constexpr int NI = 8;  // rows of up to 512 columns held in registers
+  float qreg[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) qreg[i] = qr[min(lane + 64 * i, D - 1)];  // columns >= D are never summed
   for (int j0 = 0; j0 < L; j0 += 4) {
     const int n = min(4, L - j0);
     const float* gr[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) gr[u] = g + (long long)ei[j0 + (u < n ? u : 0)] * D;
     double kk[4];
-    exact_keys4(qr, gr, n, D, lane, metric, kk);
+    if (D <= 64 * NI)
+      exact_keys4_reg<NI>(qreg, gr, n, D, lane, metric, kk);
+    else
+      exact_keys4(qr, gr, n, D, lane, metric, kk);
     if (lane == 0) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -1210,7 +1266,7 @@ static bool launch_merge_wave(int Q, hipStream_t st, const float* q, const float
   const size_t sh = (size_t)nc * (sizeof(double) + sizeof(int));
 #define ARTSBIR_MW(NPL)                                                                                            \
   hipLaunchKernelGGL(knn_merge_wave_kernel<NPL>, dim3(Q), dim3(64), sh, st, q, g, D, nchunks, cand_d, cand_i, qsq, \
-                     gsq_max, rel, g_base, k, out_i, out_d, flag, metric, qeps, n_g)
+                     gsq_max, rel, g_base, k, out_i, out_d, flag, metric, qeps, n_g, knn_stat_on() ? 1 : 0)
   if (nc <= 128) ARTSBIR_MW(2);
   else if (nc <= 256) ARTSBIR_MW(4);
   else if (nc <= 512) ARTSBIR_MW(8);
@@ -1284,7 +1340,14 @@ __global__ void sq_minmax_kernel(const float* __restrict__ sq, long long n, unsi
     mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     mn = fminf(mn, __shfl_xor(mn, o, 64));
   }
-  if ((threadIdx.x & 63) == 0) {
+  // one atomic pair per workgroup (the atomics on two words serialise: one pair
+  // per wave of a 1024-workgroup grid took ~95 us)
+  __shared__ float smx[16], smn[16];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smx[w] = mx; smn[w] = mn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) { mx = fmaxf(mx, smx[i]); mn = fminf(mn, smn[i]); }
     atomicMax(ext, __float_as_uint(mx));
     atomicMin(ext + 1, __float_as_uint(mn));
   }
@@ -1318,21 +1381,24 @@ __global__ void __launch_bounds__(256) knn_count_exhaustive_kernel(const float* 
                                                                    const double* __restrict__ dpos,
                                                                    const long long* __restrict__ pos,
                                                                    long long g_base, int* __restrict__ cnt,
-                                                                   int metric) {
-  if (*unc_n <= unc_cap) return;
-  const int qi = blockIdx.y;
-  const double dp = dpos[qi];
-  if (dp < 0) return;
+                                                                   int metric, int nq) {
+  if (*unc_n <= unc_cap) return;  // the usual case: the grid is small so this costs ~nothing
   const int lane = threadIdx.x & 63;
-  const long long W = (long long)gridDim.x * (blockDim.x / 64);
-  const long long w = blockIdx.x * (long long)(blockDim.x / 64) + (threadIdx.x >> 6);
-  const long long p = pos[qi];
-  int c = 0;
-  for (long long r = w; r < n; r += W) {
-    const double d = exact_key(q + (long long)qi * D, g + r * D, D, lane, metric);
-    c += (d < dp || (d == dp && g_base + r < p)) ? 1 : 0;
+  constexpr int SLICES = 64;  // workgroups per query
+  for (long long job = blockIdx.x; job < (long long)nq * SLICES; job += gridDim.x) {
+    const int qi = (int)(job / SLICES);
+    const double dp = dpos[qi];
+    if (dp < 0) continue;
+    const long long W = (long long)SLICES * (blockDim.x / 64);
+    const long long w = (job % SLICES) * (long long)(blockDim.x / 64) + (threadIdx.x >> 6);
+    const long long p = pos[qi];
+    int c = 0;
+    for (long long r = w; r < n; r += W) {
+      const double d = exact_key(q + (long long)qi * D, g + r * D, D, lane, metric);
+      c += (d < dp || (d == dp && g_base + r < p)) ? 1 : 0;
+    }
+    if (lane == 0 && c) atomicAdd(cnt + qi, c);
   }
-  if (lane == 0 && c) atomicAdd(cnt + qi, c);
 }
 
 // exhaustive exact top-k of the flagged queries (a chunk list could have hidden
@@ -1757,7 +1823,7 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
     hipLaunchKernelGGL(rows_prep_kernel<float>, dim3(gg), dim3(256), 0, st, g, ng, D, gsq, (float*)gc, p.Dp, metric);
   {
     long long b = (N + 255) / 256;
-    if (b > 1024) b = 1024;
+    if (b > 256) b = 256;
     hipLaunchKernelGGL(sq_minmax_kernel, dim3((unsigned)b), dim3(256), 0, st, gsq, N, ext);
   }
   hipLaunchKernelGGL(knn_init_kernel, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, st, qsq, ext, Q, rel, metric,
@@ -1809,8 +1875,8 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
                        g_base, cnt, metric);
     hipLaunchKernelGGL(knn_count_reset_kernel, dim3((unsigned)((Q + 255) / 256)), dim3(256), 0, st,
                        unc + 2 * p.unc_cap, p.unc_cap, Q, cnt);
-    hipLaunchKernelGGL(knn_count_exhaustive_kernel, dim3(64, Q), dim3(256), 0, st, q, g, D, N, unc + 2 * p.unc_cap,
-                       p.unc_cap, dpos, positives, g_base, cnt, metric);
+    hipLaunchKernelGGL(knn_count_exhaustive_kernel, dim3(2048), dim3(256), 0, st, q, g, D, N, unc + 2 * p.unc_cap,
+                       p.unc_cap, dpos, positives, g_base, cnt, metric, Q);
   }
   hipLaunchKernelGGL(knn_exact_topk_part_kernel, dim3(KNN_XB, Q), dim3(256), 0, st, q, g, D, N, k, metric, flag, pkey,
                      pidx);

@@ -24,5 +24,5 @@ if __name__ == "__main__":
         print(json.dumps({"noise": noise, "qps": r["value"], "ms": r["ms"], "map@10": r["map@10"],
                           "scan_us": r["roofline"]["avg_launch_us"], "scan_frac": r["roofline"]["frac"],
                           "kb": os.environ.get("ARTSBIR_KNN_KB", "1"),
-                          "wave_tiles": st[0], "entries": st[1], "insertions": st[2], "entries_t64": st[3],
+                          "wave_tiles": st[0], "entries": st[1], "insertions": st[2], "merge_live_per_query": round(st[3] / (4 * 10_000), 2),
                           "entry_frac": round(st[1] / max(st[0], 1), 4)}), flush=True)
