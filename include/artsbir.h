@@ -422,8 +422,9 @@ int artsbir_knn_set_unc_cap(int cap);
  * on = 1 starts collecting, 0 stops; read returns the summed scan time and count. */
 int artsbir_scan_profile(int on);
 int artsbir_scan_profile_read(double* total_ms, int* count);
-/* Diagnostics of the bf16 scan (env ARTSBIR_KNN_STAT=1): out4 = {wave-tiles,
- * slow-path entries, list insertions, 0} summed since the last reset. */
+/* Diagnostics of the bf16 scan and the exact merge (env ARTSBIR_KNN_STAT=1):
+ * out4 = {wave-tiles, slow-path entries, list insertions, live candidates of
+ * the one-wave merge} summed since the last reset. */
 int artsbir_knn_stat_read(unsigned long long* out4, int reset);
 /* per-shard top-k lists gathered from nshard ranks, dist/idx [nshard][Q][k]
  * (index -1 = empty) -> global top-k by (distance, index) (sharded C4). */
