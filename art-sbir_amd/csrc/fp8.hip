@@ -372,7 +372,7 @@ __device__ __forceinline__ void f8_gelu_row4(T* __restrict__ C, bf16* __restrict
 // stores alike, so a load issued after a store waits for that store too: RD 1
 // issues pass p + 1's loads before pass p's stores, and no load waits behind
 // the output traffic.
-template <typename T, int RD>
+template <typename T, int RD, int BN>
 __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
                                                           const unsigned char* __restrict__ B,
                                                           const float* __restrict__ sa, const float* __restrict__ sb,
@@ -380,55 +380,79 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
                                                           int accumulate, const bf16* __restrict__ res,
                                                           bf16* __restrict__ out2, int skip_c,
                                                           unsigned* __restrict__ pmax) {
-  __shared__ __attribute__((aligned(16))) char smem[2][2][256 * 128];  // [stage][A | B]
+  // BN 256: 2 x 4 waves of 128 x 64, a 2-stage ring of 64 KB stages (one in
+  // flight while the other is consumed).  BN 128: 4 x 2 waves of 64 x 64, a
+  // 3-stage ring of 48 KB stages, two in flight: at ~1 us of MFMA per stage the
+  // single stage in flight of the 256-wide tile leaves every k-step waiting on
+  // its L2/HBM round trip
+  constexpr int NST = BN == 256 ? 2 : 3;
+  constexpr int MI = BN == 256 ? 8 : 4;             // 16-row MFMA tiles per wave
+  constexpr int SB = 256 * 128 + BN * 128;          // stage bytes: A [256][128] | B [BN][128]
+  constexpr int NPB = BN / 64;                      // B pieces per wave
+  constexpr int PER_STAGE = 4 + NPB;                // LDS-DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NST][SB];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_n = (N + 255) / 256;
+  const int tiles_n = (N + BN - 1) / BN;
   const long long G = gridDim.x;
   long long lid = blockIdx.x;
   if (G >= 8) {  // consecutive tiles (one A panel) on one XCD
     const long long q = G / 8, r = G % 8, x = lid % 8;
     lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
   }
-  const int m0 = (int)(lid / tiles_n) * 256, n0 = (int)(lid % tiles_n) * 256;
-  const int wm = (wid >> 2) * 128, wn = (wid & 3) * 64;
+  const int m0 = (int)(lid / tiles_n) * 256, n0 = (int)(lid % tiles_n) * BN;
+  const int wm = BN == 256 ? (wid >> 2) * 128 : (wid >> 1) * 64;
+  const int wn = BN == 256 ? (wid & 3) * 64 : (wid & 1) * 64;
   const int nk = K / 128;
   const __amdgpu_buffer_rsrc_t ra = f8_rsrc(A + (long long)m0 * K, (long long)(M - m0) * K);
   const __amdgpu_buffer_rsrc_t rb = f8_rsrc(B + (long long)n0 * K, (long long)(N - n0) * K);
-  // loader: wave w moves 1-KB pieces w, w + 8, w + 16, w + 24 of each operand
-  // (8 rows each); lane l fills slot l & 7 of row l >> 3 with the chunk that
-  // belongs there under the swizzle
+  // loader: wave w moves 1-KB pieces w, w + 8, ... of each operand (8 rows
+  // each); lane l fills slot l & 7 of row l >> 3 with the chunk that belongs
+  // there under the swizzle
   const int lrow = lane >> 3, lslot = lane & 7;
   auto issue = [&](int kt, int buf) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int piece = wid + 8 * u, row = piece * 8 + lrow;
       const unsigned off = (unsigned)(row * K + kt * 128 + ((lslot ^ (row & 7)) << 4));
-      f8_glds16(ra, &smem[buf][0][piece * 1024], off);
-      f8_glds16(rb, &smem[buf][1][piece * 1024], off);
+      f8_glds16(ra, &smem[buf][piece * 1024], off);
+    }
+#pragma unroll
+    for (int u = 0; u < NPB; ++u) {
+      const int piece = wid + 8 * u, row = piece * 8 + lrow;
+      const unsigned off = (unsigned)(row * K + kt * 128 + ((lslot ^ (row & 7)) << 4));
+      f8_glds16(rb, &smem[buf][256 * 128 + piece * 1024], off);
     }
   };
-  f32x4 acc[8][4];
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, kq = lane >> 4;
   issue(0, 0);
+  if (NST == 3 && nk > 1) issue(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's pieces of stage kt landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // and its reads of the other stage retired
+    const int buf = NST == 2 ? (kt & 1) : kt % 3;
+    if (NST == 3 && kt + 1 < nk)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");  // stage kt landed, kt + 1 may be in flight
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of stage kt landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // and its reads of the stage refilled next retired
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-    const char* ai = &smem[buf][0][0];
-    const char* bi = &smem[buf][1][0];
+    if (NST == 2) {
+      if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    } else {
+      if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // the stage consumed at kt - 1: every wave is past it
+    }
+    const char* ai = &smem[buf][0];
+    const char* bi = &smem[buf][256 * 128];
     i32x8 bfr[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(bi, wn + 16 * j + fr, kq);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < MI; ++i) {
       const i32x8 af = f8_frag(ai, wm + 16 * i + fr, kq);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -441,7 +465,8 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
   constexpr int EP = 68;  // f32 row pitch of a wave's block
-  float* eb = reinterpret_cast<float*>(&smem[0][0][0]) + wid * 32 * EP;
+  static_assert(8 * 32 * EP * 4 <= NST * SB, "epilogue blocks fit the ring");
+  float* eb = reinterpret_cast<float*>(&smem[0][0]) + wid * 32 * EP;
   const float s = sa[0] * sb[0];
   const int ec = (lane & 15) * 4, er = lane >> 4;  // this lane's 4 columns, row phase
   const int n = n0 + wn + ec;
@@ -476,7 +501,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   float am = 0.f;
   if constexpr (RD == 1) prefetch(0, pre[0]);
 #pragma unroll
-  for (int pass = 0; pass < 4; ++pass) {
+  for (int pass = 0; pass < MI / 2; ++pass) {
 #pragma unroll
     for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
@@ -486,7 +511,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     if constexpr (RD == 1) {
-      if (pass + 1 < 4) prefetch(pass + 1, pre[(pass + 1) & 1]);
+      if (pass + 1 < MI / 2) prefetch(pass + 1, pre[(pass + 1) & 1]);
       asm volatile("" ::: "memory");  // those loads go out ahead of this pass's stores
     }
 #pragma unroll
@@ -575,6 +600,17 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
                                       const float* sa, const float* sb, const float* bias, void* c, int out_dtype,
                                       int accumulate, const void* res, void* out2, int skip_c, void* stream);
 
+// the LDS-DMA kernel's tile width: 256 (2-stage ring).  ARTSBIR_FP8_BN=128
+// selects the 256 x 128 tile with a 3-stage ring (two stages in flight): it
+// measured slower on every C5 shape (qkv 1.09 vs 0.93 ms, c_fc 1.29 vs 1.13,
+// out_proj 0.62 vs 0.58, c_proj 0.94 vs 0.83 ms; profiles/r3_fp8_tile_ab.txt):
+// the doubled A re-reads and LDS bytes per MAC cost more than the deeper ring
+// saves, so the wait per k-step is not what bounds the 256-wide tile
+static int fp8_bn(int N) {
+  static const int forced = [] { const char* e = getenv("ARTSBIR_FP8_BN"); return e ? atoi(e) : 0; }();
+  return forced == 128 ? 128 : 256;
+}
+
 extern "C" int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, const unsigned char* b,
                                    const float* sa, const float* sb, const float* bias, void* c, int out_dtype,
                                    int accumulate, void* stream) {
@@ -596,8 +632,9 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
   if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8: too many tiles"); return -1; }
   hipStream_t st = (hipStream_t)stream;
   const char* old = getenv("ARTSBIR_FP8_V1");
-  if (M >= 256 && N >= 256 && !(old && atoi(old))) {  // 256 x 256 LDS-DMA kernel
-    const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if (M >= 256 && N >= 256 && !(old && atoi(old))) {  // 256 x BN LDS-DMA kernel
+    const int bn = fp8_bn(N);
+    const long long t2 = (long long)((M + 255) / 256) * ((N + bn - 1) / bn);
     if ((long long)M * K > 0x7fffffffLL || (long long)N * K > 0x7fffffffLL) {
       set_error("gemm_nt_fp8: operand larger than 2 GiB");
       return -1;
@@ -609,17 +646,32 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
     const int nrd = (accumulate ? 1 : 0) + (res ? 1 : 0);
     set_last_kernel("gemm_fp8_v2_kernel");
     if (nrd == 0) {
-      FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0>), dim3((unsigned)t2), dim3(512), 0, st, M,
-                                               N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                               (bf16*)out2, skip_c, nullptr));
+      if (bn == 128)
+        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0, 128>), dim3((unsigned)t2), dim3(512), 0,
+                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                                 (bf16*)out2, skip_c, nullptr));
+      else
+        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0, 256>), dim3((unsigned)t2), dim3(512), 0,
+                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                                 (bf16*)out2, skip_c, nullptr));
     } else if (nrd == 1) {
-      FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1>), dim3((unsigned)t2), dim3(512), 0, st, M,
-                                               N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                               (bf16*)out2, skip_c, nullptr));
+      if (bn == 128)
+        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1, 128>), dim3((unsigned)t2), dim3(512), 0,
+                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                                 (bf16*)out2, skip_c, nullptr));
+      else
+        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1, 256>), dim3((unsigned)t2), dim3(512), 0,
+                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                                 (bf16*)out2, skip_c, nullptr));
     } else {
-      FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2>), dim3((unsigned)t2), dim3(512), 0, st, M,
-                                               N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                               (bf16*)out2, skip_c, nullptr));
+      if (bn == 128)
+        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2, 128>), dim3((unsigned)t2), dim3(512), 0,
+                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                                 (bf16*)out2, skip_c, nullptr));
+      else
+        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2, 256>), dim3((unsigned)t2), dim3(512), 0,
+                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
+                                                 (bf16*)out2, skip_c, nullptr));
     }
   } else {
     set_last_kernel("gemm_fp8_kernel");
@@ -645,14 +697,19 @@ extern "C" int artsbir_gemm_nt_fp8_gelu(int M, int N, int K, const unsigned char
   if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8_gelu: too many tiles"); return -1; }
   hipStream_t st = (hipStream_t)stream;
   if (M >= 256 && N >= 256) {
-    const long long t2 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+    const int bn = fp8_bn(N);
+    const long long t2 = (long long)((M + 255) / 256) * ((N + bn - 1) / bn);
     if ((long long)M * K > 0x7fffffffLL || (long long)N * K > 0x7fffffffLL) {
       set_error("gemm_nt_fp8_gelu: operand larger than 2 GiB");
       return -1;
     }
     set_last_kernel("gemm_fp8_v2_kernel");
-    hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa, sb,
-                       bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
+    if (bn == 128)
+      hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0, 128>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa,
+                         sb, bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
+    else
+      hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0, 256>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa,
+                         sb, bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
   } else {
     set_last_kernel("gemm_fp8_kernel");
     hipLaunchKernelGGL(gemm_fp8_kernel<bf16>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K, a, b, sa, sb, bias,
