@@ -49,17 +49,25 @@ def short(name):
     m = re.match(r"_ZN7artsbir\d+(\w+?_kernel)", name)
     if m:
         return m.group(1)
-    # demangled form: void artsbir::name<a, b, ...>(args) -> the names bench.py uses
+    # demangled form: void artsbir::name<a, b, ...>(args) -> exactly the names
+    # bench.py records (the library's set_last_kernel strings)
     m = re.match(r"(?:void )?artsbir::(\w+_kernel)<([^>]*)>", name)
     if m:
         k, t = m.group(1), [x.strip() for x in m.group(2).split(",")]
         fb = ",bnb" if t[-1] == "true" and k == "sconv_kernel" else ""
-        if k == "pgemm_kernel":
-            return f"{k}<{t[0]},{t[1]}{',bnb' if t[6] != '0' else ''}{',pf' if t[8] == 'true' else ''}>"
-        if k == "pwgrad_kernel":
-            return f"{k}<{t[0]},{t[1]}>"
-        if k == "pstream_kernel":
-            return f"{k}<{t[0]}{',bnb' if t[5] == 'true' else ''}>"
+        if k == "pgemm_kernel":  # <BPX, BCH, WPX, WCH, NSTAGE, MULTI, BK, TWO, PF, KS>
+            k32 = ",k32" if len(t) > 9 and t[9] == "32" else ""
+            return f"{k}<{t[0]},{t[1]}{k32}{',bnb' if t[6] != '0' else ''}{',pf' if t[8] == 'true' else ''}>"
+        if k == "pwgrad_kernel":  # <BM, BN, WM, WN, NSTAGE, ...>: the 256 x 256 tiles carry their wave grid
+            return f"{k}<{t[0]},{t[1]}{f',w{t[2]}x{t[3]}' if t[0] == t[1] == '256' else ''}>"
+        if k == "hwgrad_kernel":  # <CT, OT, TR, NWC>: the 4-wave 64 x 64 variant is named w4
+            return f"{k}<{t[0]},{t[1]}{',w4' if t[0] == t[1] == '64' and t[3] == '4' else ''}>"
+        if k == "pstream_kernel":  # <BCH, WPX, WCH, NSTAGE, MULTI, BNB, FWDS, BK, TWO, KS>
+            if len(t) > 9 and t[9] == "32":
+                return f"{k}<{t[0]},k32>"
+            if t[5] == "true":
+                return f"{k}<{t[0]},{'bnbk' if len(t) > 7 and t[7] != '0' else 'bnb'}>"
+            return f"{k}<{t[0]}>"
         if k == "hconv_kernel":
             return f"{k}<{t[0]},{t[1]},{t[2]}x{t[3]}{',bnb' if t[4] == 'true' else ''}>"
         if k == "sconv_kernel":
