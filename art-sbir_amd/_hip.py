@@ -43,6 +43,12 @@ class AdamTensor(ctypes.Structure):
     _fields_ = [("param", _vp), ("grad", _vp), ("exp_avg", _vp), ("exp_avg_sq", _vp), ("numel", _c_ll)]
 
 
+class PackDesc(ctypes.Structure):
+    """artsbir_pack_desc (include/artsbir.h): one entry of the batched weight re-pack"""
+    _fields_ = [("src", _vp), ("dst", _vp), ("Co", _c_int), ("Ci", _c_int), ("R", _c_int), ("S", _c_int),
+                ("ci_pad", _c_int), ("mode", _c_int), ("ldo", _c_ll), ("blk0", _c_ll)]
+
+
 class ImageDesc(ctypes.Structure):
     """artsbir_image_desc (include/artsbir.h)"""
     _fields_ = [("src", ctypes.c_void_p), ("H", ctypes.c_int), ("W", ctypes.c_int), ("C", ctypes.c_int),
@@ -98,6 +104,7 @@ SIGNATURES = {
     "artsbir_conv2d_dgrad_bnb": [_P, _vp, _vp, _vp, _vp, _c_int, _PB, _c_int, _c_ll, _vp],
     "artsbir_pack_input": [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_pack_weight": [_c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_ll, _vp, _vp],
+    "artsbir_pack_weights": [_c_int, _vp, _c_int, _c_ll, _vp],
     "artsbir_unpack_wgrad": [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_cast": [_c_int, _vp, _c_int, _vp, _c_ll, _vp],
     "artsbir_bn_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _c_float, _c_float, _c_int,

@@ -94,37 +94,85 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int C, doubl
 // order (running statistics updated once per segment, as the reference's
 // consecutive forward calls do); out[s] = {mean, istd, scale, beta}[C] — the BN
 // parameter block every consumer applies as (y - mean) * scale + beta
-__global__ void bn_finalize_seg_kernel(const float* __restrict__ stats, int nseg, long long seg_stride, int C,
-                                       double count, const float* gamma, const float* beta, float* rmean, float* rvar,
-                                       long long* nbt, float momentum, float eps, int train, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && train && nbt) nbt[0] += nseg;
-  if (c >= C) return;
-  for (int s = 0; s < nseg; ++s) {
-    double mean, var;
-    if (train) {
-      const float* st = stats + s * seg_stride;
-      double s1 = 0, s2 = 0;
-      for (int k = 0; k < ARTSBIR_NSLOT; ++k) {
-        s1 += st[(long long)k * 2 * C + c];
-        s2 += st[(long long)k * 2 * C + C + c];
+// Slot sums of a BN site: 4 lanes per channel add 8 of the ARTSBIR_NSLOT
+// replica slots each (16 independent loads in flight per lane instead of a
+// 32-long dependent chain per channel), the quarters combined in fixed order
+// through LDS; segments FIN_SEGS at a time.  grid ceil(C / 64), 256 threads.
+constexpr int FIN_CPB = 64, FIN_Q = 4, FIN_SEGS = 8;
+static_assert(ARTSBIR_NSLOT % FIN_Q == 0, "slot quarters");
+
+__device__ __forceinline__ void fin_quarter(const float* __restrict__ st, long long C, int c, int q, double& s1,
+                                            double& s2) {
+  constexpr int KQ = ARTSBIR_NSLOT / FIN_Q;
+  const float* p = st + (long long)q * KQ * 2 * C + c;
+  float v1[KQ], v2[KQ];
+#pragma unroll
+  for (int k = 0; k < KQ; ++k) {
+    v1[k] = p[(long long)k * 2 * C];
+    v2[k] = p[(long long)k * 2 * C + C];
+  }
+  s1 = 0.0;
+  s2 = 0.0;
+#pragma unroll
+  for (int k = 0; k < KQ; ++k) {
+    s1 += v1[k];
+    s2 += v2[k];
+  }
+}
+
+// all nseg BN segments of one layer in one launch: per channel the segments in
+// order (running statistics updated once per segment, as the reference's
+// consecutive forward calls do); out[s] = {mean, istd, scale, beta}[C] — the BN
+// parameter block every consumer applies as (y - mean) * scale + beta
+__global__ void __launch_bounds__(256) bn_finalize_seg_kernel(const float* __restrict__ stats, int nseg,
+                                                              long long seg_stride, int C, double count,
+                                                              const float* gamma, const float* beta, float* rmean,
+                                                              float* rvar, long long* nbt, float momentum, float eps,
+                                                              int train, float* __restrict__ out) {
+  __shared__ double red[FIN_SEGS][FIN_Q][2][FIN_CPB];
+  const int cl = threadIdx.x & (FIN_CPB - 1), q = threadIdx.x / FIN_CPB;
+  const int c = blockIdx.x * FIN_CPB + cl;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && train && nbt) nbt[0] += nseg;
+  for (int s0 = 0; s0 < nseg; s0 += FIN_SEGS) {
+    const int ns = nseg - s0 < FIN_SEGS ? nseg - s0 : FIN_SEGS;
+    if (train && c < C) {
+      for (int s = 0; s < ns; ++s) {
+        double a, b;
+        fin_quarter(stats + (long long)(s0 + s) * seg_stride, C, c, q, a, b);
+        red[s][q][0][cl] = a;
+        red[s][q][1][cl] = b;
       }
-      mean = s1 / count;
-      var = s2 / count - mean * mean;
-      if (var < 0) var = 0;
-      if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
-      if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * count / (count > 1 ? count - 1 : 1));
-    } else {
-      mean = rmean[c];
-      var = rvar[c];
     }
-    const float is = (float)(1.0 / sqrt(var + (double)eps));
-    const float sc = gamma[c] * is;
-    float* o = out + (long long)s * 4 * C;
-    o[c] = (float)mean;
-    o[C + c] = is;
-    o[2 * C + c] = sc;
-    o[3 * C + c] = beta[c];
+    __syncthreads();
+    if (q == 0 && c < C) {
+      for (int s = 0; s < ns; ++s) {
+        double mean, var;
+        if (train) {
+          double s1 = 0, s2 = 0;
+#pragma unroll
+          for (int u = 0; u < FIN_Q; ++u) {
+            s1 += red[s][u][0][cl];
+            s2 += red[s][u][1][cl];
+          }
+          mean = s1 / count;
+          var = s2 / count - mean * mean;
+          if (var < 0) var = 0;
+          if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
+          if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * count / (count > 1 ? count - 1 : 1));
+        } else {
+          mean = rmean[c];
+          var = rvar[c];
+        }
+        const float is = (float)(1.0 / sqrt(var + (double)eps));
+        const float sc = gamma[c] * is;
+        float* o = out + (long long)(s0 + s) * 4 * C;
+        o[c] = (float)mean;
+        o[C + c] = is;
+        o[2 * C + c] = sc;
+        o[3 * C + c] = beta[c];
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -565,24 +613,42 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
 // all segments of one BN backward in one launch: slots of segment s at
 // + s * seg_stride, its istd at + s * istd_stride; dgamma/dbeta accumulate the
 // segments in order; coef[s] = {c1, c2, c3}[C]
-__global__ void bn_bwd_finalize_seg_kernel(const float* __restrict__ slots, int nseg, long long seg_stride, int C,
-                                           double count, const float* gamma, const float* istd, long long istd_stride,
-                                           float* dgamma, float* dbeta, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  for (int s = 0; s < nseg; ++s) {
-    const float* sl = slots + s * seg_stride;
-    double s1 = 0, s2 = 0;
-    for (int k = 0; k < ARTSBIR_NSLOT; ++k) {
-      s1 += sl[(long long)k * 2 * C + c];
-      s2 += sl[(long long)k * 2 * C + C + c];
+__global__ void __launch_bounds__(256) bn_bwd_finalize_seg_kernel(const float* __restrict__ slots, int nseg,
+                                                                  long long seg_stride, int C, double count,
+                                                                  const float* gamma, const float* istd,
+                                                                  long long istd_stride, float* dgamma, float* dbeta,
+                                                                  float* coef) {
+  __shared__ double red[FIN_SEGS][FIN_Q][2][FIN_CPB];
+  const int cl = threadIdx.x & (FIN_CPB - 1), q = threadIdx.x / FIN_CPB;
+  const int c = blockIdx.x * FIN_CPB + cl;
+  for (int s0 = 0; s0 < nseg; s0 += FIN_SEGS) {
+    const int ns = nseg - s0 < FIN_SEGS ? nseg - s0 : FIN_SEGS;
+    if (c < C) {
+      for (int s = 0; s < ns; ++s) {
+        double a, b;
+        fin_quarter(slots + (long long)(s0 + s) * seg_stride, C, c, q, a, b);
+        red[s][q][0][cl] = a;
+        red[s][q][1][cl] = b;
+      }
     }
-    if (dbeta) dbeta[c] += (float)s1;
-    if (dgamma) dgamma[c] += (float)s2;
-    float* co = coef + (long long)s * 3 * C;
-    co[c] = gamma[c] * istd[s * istd_stride + c];
-    co[C + c] = (float)(s1 / count);
-    co[2 * C + c] = (float)(s2 / count);
+    __syncthreads();
+    if (q == 0 && c < C) {
+      for (int s = 0; s < ns; ++s) {
+        double s1 = 0, s2 = 0;
+#pragma unroll
+        for (int u = 0; u < FIN_Q; ++u) {
+          s1 += red[s][u][0][cl];
+          s2 += red[s][u][1][cl];
+        }
+        if (dbeta) dbeta[c] += (float)s1;
+        if (dgamma) dgamma[c] += (float)s2;
+        float* co = coef + (long long)(s0 + s) * 3 * C;
+        co[c] = gamma[c] * istd[(long long)(s0 + s) * istd_stride + c];
+        co[C + c] = (float)(s1 / count);
+        co[2 * C + c] = (float)(s2 / count);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -688,6 +754,68 @@ __global__ void pack_weight_kernel(const float* __restrict__ src, int Co, int Ci
       int ci = (int)(t / R);
       float v = src[(((long long)co * Ci + ci) * R + (R - 1 - r)) * S + (S - 1 - s)];
       dst[(((long long)ci * R + r) * S + s) * ldo + co] = from_f<T>(v);
+    }
+  }
+}
+
+// all packs of a model in one launch: block b finds its descriptor by binary
+// search over the blk0 prefix and packs elements [1024 (b - blk0), + 1024) of it
+// (mode 1: 64 x 64 tile b - blk0 of the flipped transpose)
+constexpr int PACK_EPB = 1024, PACK_T = 64;
+template <typename T>
+__global__ void __launch_bounds__(256) pack_weights_kernel(const artsbir_pack_desc* __restrict__ tab, int n) {
+  const long long b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last entry with blk0 <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].blk0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const artsbir_pack_desc d = tab[lo];
+  const int Co = d.Co, Ci = d.Ci, R = d.R, S = d.S;
+  if (d.mode == 1) {
+    // flipped transpose as a 64 x 64 tile of the [Co][Ci*R*S] source through
+    // LDS: coalesced reads along k, coalesced writes along co
+    __shared__ float tile[PACK_T][PACK_T + 1];
+    const int RS = R * S;
+    const long long K = (long long)Ci * RS, nk = (K + PACK_T - 1) / PACK_T;
+    const long long t = b - d.blk0;
+    const int co0 = (int)(t / nk) * PACK_T;
+    const long long k0 = (t % nk) * PACK_T;
+    const int col = threadIdx.x % PACK_T;
+    for (int rr = threadIdx.x / PACK_T; rr < PACK_T; rr += 256 / PACK_T) {
+      const int co = co0 + rr;
+      const long long k = k0 + col;
+      tile[rr][col] = (co < Co && k < K) ? d.src[(long long)co * K + k] : 0.f;
+    }
+    __syncthreads();
+    for (int rr = threadIdx.x / PACK_T; rr < PACK_T; rr += 256 / PACK_T) {
+      const long long k = k0 + rr;
+      const int co = co0 + col;
+      if (k < K && co < Co) {
+        const long long ci = k / RS;
+        const int rs = (int)(k - ci * RS);
+        reinterpret_cast<T*>(d.dst)[(ci * RS + (RS - 1 - rs)) * d.ldo + co] = from_f<T>(tile[col][rr]);
+      }
+    }
+    return;
+  }
+  const long long cnt = d.mode == 0 ? (long long)Co * R * S * d.ci_pad : Co;
+  const long long i0 = (b - d.blk0) * PACK_EPB;
+  for (int u = threadIdx.x; u < PACK_EPB; u += 256) {
+    const long long i = i0 + u;
+    if (i >= cnt) break;
+    if (d.mode == 0) {
+      const int ci = (int)(i % d.ci_pad);
+      long long t = i / d.ci_pad;
+      const int s = (int)(t % S);
+      t /= S;
+      const int r = (int)(t % R);
+      const int co = (int)(t / R);
+      const float v = ci < Ci ? d.src[(((long long)co * Ci + ci) * R + r) * S + s] : 0.f;
+      reinterpret_cast<T*>(d.dst)[i] = from_f<T>(v);
+    } else {
+      reinterpret_cast<float*>(d.dst)[i] = d.src[i];
     }
   }
 }
@@ -823,7 +951,7 @@ extern "C" int artsbir_bn_finalize_seg(const float* stats, int nseg, long long s
   if (nseg < 1) { set_error("bn_finalize_seg: nseg=%d", nseg); return -1; }
   if (train && !stats) { set_error("bn_finalize: train mode needs stats"); return -1; }
   if (!train && (!running_mean || !running_var)) { set_error("bn_finalize: eval mode needs running stats"); return -1; }
-  hipLaunchKernelGGL(bn_finalize_seg_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, stats, nseg,
+  hipLaunchKernelGGL(bn_finalize_seg_kernel, dim3((C + FIN_CPB - 1) / FIN_CPB), dim3(256), 0, (hipStream_t)stream, stats, nseg,
                      seg_stride, C, count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
                      train, out);
   ARTSBIR_CHECK_LAUNCH("bn_finalize_seg");
@@ -965,7 +1093,7 @@ extern "C" int artsbir_bn_bwd_finalize_seg(const float* slots, int nseg, long lo
                                            const float* gamma, const float* istd, long long istd_stride,
                                            float* dgamma, float* dbeta, float* coef, void* stream) {
   if (nseg < 1) { set_error("bn_bwd_finalize_seg: nseg=%d", nseg); return -1; }
-  hipLaunchKernelGGL(bn_bwd_finalize_seg_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, slots, nseg,
+  hipLaunchKernelGGL(bn_bwd_finalize_seg_kernel, dim3((C + FIN_CPB - 1) / FIN_CPB), dim3(256), 0, (hipStream_t)stream, slots, nseg,
                      seg_stride, C, count, gamma, istd, istd_stride, dgamma, dbeta, coef);
   ARTSBIR_CHECK_LAUNCH("bn_bwd_finalize_seg");
   return 0;
@@ -1046,6 +1174,18 @@ extern "C" int artsbir_pack_weight(int dtype, const float* src, int Co, int Ci, 
   DISPATCH_T(dtype, hipLaunchKernelGGL(pack_weight_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                        src, Co, Ci, R, S, ci_pad, mode, ldo, (T*)dst));
   ARTSBIR_CHECK_LAUNCH("pack_weight");
+  return 0;
+}
+
+extern "C" int artsbir_pack_weights(int dtype, const artsbir_pack_desc* table, int n, long long nblocks,
+                                    void* stream) {
+  if (n < 1 || nblocks < 1 || !table || nblocks > 0x7fffffffLL) {
+    set_error("pack_weights: n=%d nblocks=%lld", n, nblocks);
+    return -1;
+  }
+  DISPATCH_T(dtype, hipLaunchKernelGGL(pack_weights_kernel<T>, dim3((unsigned)nblocks), dim3(256), 0,
+                                       (hipStream_t)stream, table, n));
+  ARTSBIR_CHECK_LAUNCH("pack_weights");
   return 0;
 }
 

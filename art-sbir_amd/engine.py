@@ -100,6 +100,9 @@ def cu_masked_stream(device, ncu):
     return st
 
 
+PACK_EPB, PACK_T = 1024, 64  # artsbir_pack_weights blocking (PACK_EPB, PACK_T in elementwise.hip)
+
+
 def _fuse_bnb():
     """BN-backward reductions fused into the data-gradient epilogues (f32 atomics)
     except in the deterministic mode, which reduces them in a fixed order"""
@@ -211,22 +214,56 @@ class Engine:
                 tuple((p.data_ptr(), p._version) for p in self.model.parameters()))
 
     def packed(self):
+        """packed operands of the current weights.  The first pack of a set of
+        parameter storages allocates the buffers and records every pack; each
+        later re-pack (after an optimizer step) rewrites the same buffers with
+        ONE batched launch (artsbir_pack_weights) instead of ~120 small ones."""
         key = self._params_key()
         if self._packed_key != key:
-            self._packed = self._pack_all()
+            plan_key = (self.dtype, tuple((p.data_ptr(), tuple(p.shape)) for p in self.model.parameters()))
+            plan = getattr(self, "_plan", None)
+            if plan is not None and plan[0] == plan_key:
+                call("artsbir_pack_weights", self.dt, ptr(plan[1]), plan[2], plan[3], _s(),
+                     kernel="pack_weights_kernel", tag=f"pack_weights x{plan[2]}")
+            else:
+                self._recording = []
+                self._packed = self._pack_all()
+                self._plan = self._make_plan(plan_key, self._recording)
+                self._recording = None
             self._packed_key = key
         return self._packed
+
+    def _make_plan(self, plan_key, recs):
+        if not recs:
+            return None
+        dev = next(self.model.parameters()).device
+        descs = (_hip.PackDesc * len(recs))()
+        blk = 0
+        for d, (src, dst, co, ci, r, s, ci_pad, mode, ldo) in zip(descs, recs):
+            d.src, d.dst, d.Co, d.Ci, d.R, d.S, d.ci_pad, d.mode, d.ldo, d.blk0 = \
+                src, dst, co, ci, r, s, ci_pad, mode, ldo, blk
+            if mode == 1:  # 64 x 64 tiles of the flipped transpose
+                blk += -(-co // PACK_T) * -(-(ci * r * s) // PACK_T)
+            else:
+                blk += -(-(co * r * s * ci_pad if mode == 0 else co) // PACK_EPB)
+        raw = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8)
+        return (plan_key, raw.to(dev), len(recs), blk)
+
+    def _pack_one(self, src, co, ci, r, s, ci_pad, mode, ldo, dst):
+        call("artsbir_pack_weight", self.dt, ptr(src), co, ci, r, s, ci_pad, mode, ldo, ptr(dst), _s())
+        if getattr(self, "_recording", None) is not None:
+            self._recording.append((ptr(src), ptr(dst), co, ci, r, s, ci_pad, mode, ldo if ldo > 0 else co))
 
     def _pack_conv(self, conv, ci_pad=None, need_dgrad=True):
         w = conv.weight.detach()
         co, ci, r, s = w.shape
         ci_pad = ci_pad or ci
         fw = self._empty(co, r, s, ci_pad, device=w.device)
-        call("artsbir_pack_weight", self.dt, ptr(w), co, ci, r, s, ci_pad, 0, 0, ptr(fw), _s())
+        self._pack_one(w, co, ci, r, s, ci_pad, 0, 0, fw)
         dw = None
         if need_dgrad:
             dw = self._empty(ci, r, s, co, device=w.device)
-            call("artsbir_pack_weight", self.dt, ptr(w), co, ci, r, s, ci, 1, co, ptr(dw), _s())
+            self._pack_one(w, co, ci, r, s, ci, 1, co, dw)
         return fw, dw
 
     def _pack_linear_pair(self, lins, device):
@@ -240,9 +277,11 @@ class Engine:
         off = 0
         for l, o in zip(lins, outs):
             w = l.weight.detach()
-            call("artsbir_pack_weight", self.dt, ptr(w), o, fin, 1, 1, fin, 0, 0, ptr(fw[off:]), _s())
-            call("artsbir_pack_weight", self.dt, ptr(w), o, fin, 1, 1, fin, 1, tot, ptr(tw[:, off:]), _s())
+            self._pack_one(w, o, fin, 1, 1, fin, 0, 0, fw[off:])
+            self._pack_one(w, o, fin, 1, 1, fin, 1, tot, tw[:, off:])
             call("artsbir_cast", _hip.DT_F32, ptr(l.bias.detach()), _hip.DT_F32, ptr(bias[off:]), o, _s())
+            if getattr(self, "_recording", None) is not None:  # mode 2: the bias copy
+                self._recording.append((ptr(l.bias), ptr(bias[off:]), o, 1, 1, 1, 1, 2, o))
             off += o
         return fw, tw, bias
 

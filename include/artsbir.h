@@ -127,6 +127,20 @@ int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, 
  * operand); mode 1: flipped [Ci][R][S] rows of stride ldo (data-gradient operand). */
 int artsbir_pack_weight(int dtype, const float* src, int Co, int Ci, int R, int S, int ci_pad, int mode,
                         long long ldo, void* dst, void* stream);
+/* Every artsbir_pack_weight of a model in ONE launch (the re-pack after each
+ * optimizer step, train.py:70 -> the next forward): `table` is a DEVICE array of
+ * n descriptors; blk0 of entry i = the sum of the blocks of entries 0..i-1,
+ * nblocks the total; an entry takes ceil(elements / 1024) blocks, mode 1
+ * ceil(Co / 64) * ceil(Ci * R * S / 64) (64 x 64 transpose tiles).  mode 2: f32 copy of Co elements (a bias) into the
+ * f32 dst.  dtype is the packed operands' dtype. */
+typedef struct {
+  const float* src;
+  void* dst;
+  int Co, Ci, R, S, ci_pad, mode;
+  long long ldo;
+  long long blk0;
+} artsbir_pack_desc;
+int artsbir_pack_weights(int dtype, const artsbir_pack_desc* table, int n, long long nblocks, void* stream);
 /* wgrad workspace [Co][R][S][Cp] f32 -> dst[Co][Ci][R][S] += (parameter-gradient layout). */
 int artsbir_unpack_wgrad(const float* src, int Co, int Ci, int R, int S, int Cp, float* dst, void* stream);
 int artsbir_cast(int src_dtype, const void* x, int dst_dtype, void* y, long long n, void* stream);

@@ -221,3 +221,38 @@ def test_fused_eval_refolds_after_train_forward_without_step(dev):
             engine.FUSED_EVAL = old
     assert torch.allclose(e, e_plain, atol=1e-4, rtol=1e-4), _rel(e, e_plain)
     assert torch.allclose(e, e_ref, atol=1e-3, rtol=1e-3), _rel(e, e_ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+def test_batched_repack_matches_fresh_packs(dtype, dev):
+    """the one-launch re-pack after a weight update (artsbir_pack_weights) writes
+    exactly what a first-time per-tensor pack of the same weights writes"""
+    import engine
+    _, mine = _pair(SMALL, dev, dtype)
+    eng = engine.Engine(mine)
+    eng.dtype = dtype
+    eng.packed()  # first pack: records the plan
+    assert eng._plan is not None and eng._plan[2] > 50
+    with torch.no_grad():
+        for i, p in enumerate(mine.parameters()):
+            p.add_(0.01 * (i % 7 + 1) * torch.randn_like(p))
+    got = eng.packed()  # batched path
+    assert eng._plan is not None
+    fresh = engine.Engine(mine)
+    fresh.dtype = dtype
+    want = fresh.packed()
+    torch.cuda.synchronize()
+
+    def leaves(x):
+        if isinstance(x, dict):
+            for k in sorted(x):
+                yield from leaves(x[k])
+        elif isinstance(x, (list, tuple)):
+            for v in x:
+                yield from leaves(v)
+        elif x is not None:
+            yield x
+    a, b = list(leaves(got)), list(leaves(want))
+    assert len(a) == len(b)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
