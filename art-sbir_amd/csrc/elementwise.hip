@@ -267,6 +267,64 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
   }
 }
 
+// The same with each lane owning one 8-channel group for the whole launch
+// (BN parameters loaded once, no per-element index division) and UN units per
+// trip with every load issued before the trip's stores; segment = blockIdx.y
+// (Bs images each), units = output pixels.  C / 8 <= 256.
+template <typename T, int P>
+__global__ void __launch_bounds__(256) act_pool_cg_kernel(const T* __restrict__ x, const float* __restrict__ bn,
+                                                          int relu, int Bs, int H, int W, int C, int units_per_block,
+                                                          T* __restrict__ out) {
+  const int s = blockIdx.y;
+  const int CG = C / 8, RL = 256 / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  if (rl >= RL) return;
+  const int Ho = H / P, Wo = W / P;
+  const int units = Bs * Ho * Wo;
+  const T* xs = x + (long long)s * Bs * H * W * C + cg * 8;
+  T* os = out + (long long)s * units * C + cg * 8;
+  float mn[8], sc[8], bt[8];
+  if (bn) load_bn8(bn + (long long)s * 4 * C, C, cg * 8, mn, sc, bt);
+  const int u0 = blockIdx.x * units_per_block;
+  const int u1 = min(u0 + units_per_block, units);
+  constexpr int UN = P == 1 ? 4 : 2;
+  for (int ub = u0 + rl; ub < u1; ub += RL * UN) {
+    float v[UN][P * P][8];
+#pragma unroll
+    for (int i = 0; i < UN; ++i) {
+      const int u = min(ub + i * RL, u1 - 1);  // clamped tail: recomputed, stored once
+      if constexpr (P == 1) {
+        load8<T>(xs + (long long)u * C, v[i][0]);
+      } else {
+        const int ow = u % Wo, t = u / Wo;
+        const int oh = t % Ho, b = t / Ho;
+#pragma unroll
+        for (int dy = 0; dy < P; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < P; ++dx)
+            load8<T>(xs + ((long long)(b * H + oh * P + dy) * W + ow * P + dx) * C, v[i][dy * P + dx]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < UN; ++i) {
+      if (ub + i * RL >= u1) break;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int q = 0; q < P * P; ++q)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float a = bn ? (v[i][q][e] - mn[e]) * sc[e] + bt[e] : v[i][q][e];
+          if (relu) a = fmaxf(a, 0.f);
+          acc[e] += a;
+        }
+      constexpr float inv = 1.f / (P * P);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] *= inv;
+      store8<T>(os + (long long)(ub + i * RL) * C, acc);
+    }
+  }
+}
+
 // --------------------------------------------------------- bottleneck output
 // out = relu(bn3(y3) + (yd ? bnd(yd) : idn)), bn(y) = (y - mean) * scale + beta
 template <typename T>
@@ -303,6 +361,65 @@ __global__ void block_out_kernel(const T* __restrict__ y3, const float* __restri
       bits[i] = (unsigned char)m;
     }
   }
+}
+
+// block_out with each lane owning one 8-channel group (parameters loaded once),
+// segment = blockIdx.y (seg_rows rows each), 2 rows per trip with all loads
+// issued before the stores.  C / 8 <= 256.
+template <typename T>
+__global__ void __launch_bounds__(256) block_out_cg_kernel(const T* __restrict__ y3, const float* __restrict__ bn3,
+                                                           const T* __restrict__ yd, const float* __restrict__ bnd,
+                                                           const T* __restrict__ idn, int seg_rows, int C,
+                                                           int rows_per_block, T* __restrict__ out,
+                                                           unsigned char* __restrict__ bits) {
+  const int s = blockIdx.y;
+  const int CG = C / 8, RL = 256 / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  if (rl >= RL) return;
+  const long long po = (long long)s * 4 * C;
+  float m[8], sc[8], h[8], m2[8], s2[8], h2[8];
+  load_bn8(bn3 + po, C, cg * 8, m, sc, h);
+  if (yd) load_bn8(bnd + po, C, cg * 8, m2, s2, h2);
+  const T* rs = yd ? yd : idn;
+  const long long base = (long long)s * seg_rows;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(r0 + rows_per_block, seg_rows);
+  constexpr int UN = 2;
+  for (int rb = r0 + rl; rb < r1; rb += RL * UN) {
+    float a[UN][8], r[UN][8];
+#pragma unroll
+    for (int i = 0; i < UN; ++i) {
+      const long long off = (base + min(rb + i * RL, r1 - 1)) * C + cg * 8;
+      load8<T>(y3 + off, a[i]);
+      load8<T>(rs + off, r[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < UN; ++i) {
+      if (rb + i * RL >= r1) break;
+      const long long row = base + rb + i * RL;
+      if (yd) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[i][e] = (r[i][e] - m2[e]) * s2[e] + h2[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[i][e] = fmaxf((a[i][e] - m[e]) * sc[e] + h[e] + r[i][e], 0.f);
+      store8<T>(out + row * C + cg * 8, a[i]);
+      if (bits) {
+        unsigned mk = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mk |= (to_f(from_f<T>(a[i][e])) > 0.f ? 1u : 0u) << e;
+        bits[row * CG + cg] = (unsigned char)mk;
+      }
+    }
+  }
+}
+
+// units per workgroup so that a launch has ~2048 workgroups over all segments
+static int cg_units_per_block(long long units, int nseg, int C) {
+  const int RL = 256 / (C / 8);
+  long long upb = (units * nseg + 2047) / 2048;
+  if (upb < RL) upb = RL;
+  return (int)upb;
 }
 
 // ------------------------------------------------------------ BN backward
@@ -975,6 +1092,19 @@ extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int r
   if (pool > 1 && (H % pool || W % pool)) { set_error("act_pool: H,W not divisible by pool"); return -1; }
   const int Ho = pool > 1 ? H / pool : H, Wo = pool > 1 ? W / pool : W;
   long long n = (long long)B * Ho * Wo * (C / 8);
+  const long long units = (long long)(B / nseg) * Ho * Wo;
+  if (C / 8 <= 256 && (pool <= 1 || pool == 2) && units * C < (1LL << 40) && units < 0x7fffffffLL) {
+    const int upb = cg_units_per_block(units, nseg, C);
+    const dim3 g((unsigned)((units + upb - 1) / upb), (unsigned)nseg);
+    if (pool == 2)
+      DISPATCH_T(dtype, hipLaunchKernelGGL((act_pool_cg_kernel<T, 2>), g, dim3(256), 0, (hipStream_t)stream,
+                                           (const T*)x, bn, relu, B / nseg, H, W, C, upb, (T*)out));
+    else
+      DISPATCH_T(dtype, hipLaunchKernelGGL((act_pool_cg_kernel<T, 1>), g, dim3(256), 0, (hipStream_t)stream,
+                                           (const T*)x, bn, relu, B / nseg, H, W, C, upb, (T*)out));
+    ARTSBIR_CHECK_LAUNCH("act_pool");
+    return 0;
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(act_pool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)x, bn, relu, pool > 1 ? pool : 0, B, H, W, C, nseg, (T*)out));
   ARTSBIR_CHECK_LAUNCH("act_pool");
@@ -989,6 +1119,16 @@ extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn
   if (!yd && !identity) { set_error("block_out: need downsample or identity input"); return -1; }
   if (!bn3 || (yd && !bnd)) { set_error("block_out: missing BN parameter block"); return -1; }
   long long n = rows * (C / 8);
+  const long long seg_rows = rows / nseg;
+  if (C / 8 <= 256 && seg_rows < 0x7fffffffLL) {
+    const int rpb = cg_units_per_block(seg_rows, nseg, C);
+    const dim3 g((unsigned)((seg_rows + rpb - 1) / rpb), (unsigned)nseg);
+    DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_cg_kernel<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)y3, bn3,
+                                         (const T*)yd, bnd, (const T*)identity, (int)seg_rows, C, rpb, (T*)out,
+                                         mask_bits));
+    ARTSBIR_CHECK_LAUNCH("block_out");
+    return 0;
+  }
   DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, rows, C, nseg,
                                        (T*)out, mask_bits));

@@ -831,9 +831,15 @@ __device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&a
 // ((row >> 2) & 3), 16 rows per DMA instruction) — half the bytes per stage, so
 // the same LDS holds twice the stages and more of them are in flight (C % 64
 // == 0 only)
-template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false, int KS = 64>
-__global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
+// GLB (fused BN-backward only): the epilogue reads y, residual, mask and BN
+// constants straight from global memory (no LDS staging, no parameter table),
+// so the LDS is the stage ring alone and several workgroups share a CU: one's
+// epilogue streams while another's main loop runs
+template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false, int KS = 64,
+          bool GLB = false>
+__global__ void __launch_bounds__(64 * WPX * WCH, GLB ? 3 : 1) pgemm_kernel(PgArgs a) {
   constexpr bool BNB = BK != 0;
+  static_assert(!GLB || (BNB && !PF), "GLB: fused BN-backward epilogue only");
   static_assert(!PF || BK != 2, "PF: the bf16 mask operand of kind 2 is not prefetched");
   static_assert(KS == 64 || (KS == 32 && !MULTI), "32-k stages: uniform taps only");
   constexpr int ROWB = 2 * KS, RPI = 1024 / ROWB, CPR = ROWB / 16;
@@ -849,7 +855,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   static_assert(IPX >= 1 && IPX * RPI * NW == BPX, "pixel loader");
   static_assert(MTC % 2 == 0 && WTCH % 32 == 0, "channel pairs");
   // stage ring | BN statistics accumulator | (BNB) BN constants | (BNB) mask bits
-  constexpr int XTRA = BNB ? pg_prm_bytes<BCH>() + BPX * (BCH / 8) : 0;
+  constexpr int XTRA = (BNB && !GLB) ? pg_prm_bytes<BCH>() + BPX * (BCH / 8) : 0;
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE + pg_red_bytes<BCH>() + XTRA];
   float* red = reinterpret_cast<float*>(smem + NSTAGE * STAGE);
   int* red_cnt = reinterpret_cast<int*>(smem + NSTAGE * STAGE + 6 * BCH * 4);
@@ -866,7 +872,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
   const long long bpx = (lid / ntc) * BPX;
   const int bch = (int)(lid % ntc) * BCH;
   const long long seg0 = a.seg_m > 0 ? bpx / a.seg_m : 0;
-  if constexpr (BNB) pg_prm_fill<BCH, 64 * NW>(a, prm, bpx, bch, seg0);  // published by the main loop's barriers
+  if constexpr (BNB && !GLB) pg_prm_fill<BCH, 64 * NW>(a, prm, bpx, bch, seg0);  // published by the main loop's barriers
   const int HoWo = a.Ho * a.Wo;
   const long long img0 = bpx / HoWo;
   const __amdgpu_buffer_rsrc_t xr =
@@ -1013,6 +1019,14 @@ __global__ void __launch_bounds__(64 * WPX * WCH) pgemm_kernel(PgArgs a) {
     pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, true>(a, acc, bpx, bch, wpx, wch, fr, fq,
                                                                                 red, sg, &er);
     if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
+    return;
+  }
+  if constexpr (GLB) {
+    const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
+    EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
+    pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true>(a, acc, bpx, bch, wpx, wch,
+                                                                                          fr, fq, red, sgg);
+    stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
     return;
   }
   if constexpr (BNB) {
@@ -1940,6 +1954,28 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
   return true;
 }
 
+// candidate 16: the fused BN-backward data gradient on a 128 x 128 tile (4
+// waves) with 32-k stages (3-stage ring, 48 KB) and its epilogue operands read
+// from global memory (GLB): three workgroups per CU
+static bool pg_glb_launch(const PgArgs& a, bool multi, hipStream_t st) {
+  if (!a.bnb || multi) return false;
+  if (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) return false;
+  if (a.bnb != 1 && !a.res_mode) return false;
+  const long long tiles = ((a.M + 127) / 128) * ((a.Cout + 127) / 128);
+  if (tiles > 0x7fffffffLL) return false;
+  const dim3 g((unsigned)tiles);
+#define PG_GLB(BKV, TWOV) \
+  hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 3, false, BKV, TWOV, false, 32, true>), g, dim3(256), 0, st, a)
+  if (a.bnb == 1) PG_GLB(1, false);
+  else if (a.bnb == 3 && a.bnb_nt == 2) PG_GLB(3, true);
+  else if (a.bnb == 3) PG_GLB(3, false);
+  else if (a.bnb_nt == 2) PG_GLB(2, true);
+  else PG_GLB(2, false);
+#undef PG_GLB
+  set_last_kernel("pgemm_kernel<128,128,k32,glb,bnb>");
+  return true;
+}
+
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
@@ -1954,6 +1990,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (c >= 11 && c <= 13) return pg_pf_launch(c, a, multi, st);
   if (c == 14) return pstream_bnb_launch(a, multi, st);
   if (c == 15) return pstream_k32_launch(a, multi, st);
+  if (c == 16) return pg_glb_launch(a, multi, st);
   if (c == 10) {
     const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
     const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);
