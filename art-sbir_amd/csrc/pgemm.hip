@@ -1523,7 +1523,14 @@ struct HcGeom {
   static constexpr int HB = NB * 1024;
   static constexpr int WB = NKK * COUT * 64;       // filter image
   static constexpr int PRM = HC_MAXSEG * 4 * COUT * 4;  // BN-backward parameters per segment
-  static constexpr int LDS = WB + 2 * HB + PRM + pg_red_bytes<COUT>();
+  static constexpr int FIX = WB + PRM + pg_red_bytes<COUT>();
+  // halo buffers: three (two tiles in flight behind the one being computed)
+  // where that fits and keeps the workgroups per CU, else two; NB <= 31 so the
+  // loader's counted vmcnt(NB) fits the 6-bit field
+  static constexpr bool THREE = FIX + 3 * HB <= 160 * 1024 && (160 * 1024) / (FIX + 3 * HB) ==
+                                (160 * 1024) / (FIX + 2 * HB) && NB <= 31;
+  static constexpr int NBUF = THREE ? 3 : 2;
+  static constexpr int LDS = WB + NBUF * HB + PRM + pg_red_bytes<COUT>();
 };
 
 template <int C, int COUT, int TR, int TC, bool BNB>
@@ -1531,14 +1538,14 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
   using Gm = HcGeom<C, COUT, TR, TC>;
   constexpr int NWC = Gm::NWC, PB = Gm::PB, NKK = Gm::NKK, MTC = Gm::MTC, NP = Gm::NP;
   constexpr int TCB = Gm::TCB, NTP = Gm::NTP, HW = Gm::HW, NQ = Gm::NQ, NB = Gm::NB, HB = Gm::HB;
-  constexpr int WB = Gm::WB;
+  constexpr int WB = Gm::WB, NBUF = Gm::NBUF;
   static_assert(C % 32 == 0 && COUT % 32 == 0 && TC % 16 == 0, "tile shape");
   static_assert(NTP * NWC == TR * TCB, "pixel tiles per wave");
   static_assert(Gm::LDS <= 160 * 1024, "LDS");
   __shared__ __attribute__((aligned(16))) char smem[Gm::LDS];
-  float* prm = reinterpret_cast<float*>(smem + WB + 2 * HB);  // [seg][istd, mean, mask scale, mask beta][COUT]
-  float* red = reinterpret_cast<float*>(smem + WB + 2 * HB + Gm::PRM);
-  int* red_cnt = reinterpret_cast<int*>(smem + WB + 2 * HB + Gm::PRM + 6 * COUT * 4);
+  float* prm = reinterpret_cast<float*>(smem + WB + NBUF * HB);  // [seg][istd, mean, mask scale, mask beta][COUT]
+  float* red = reinterpret_cast<float*>(smem + WB + NBUF * HB + Gm::PRM);
+  int* red_cnt = reinterpret_cast<int*>(smem + WB + NBUF * HB + Gm::PRM + 6 * COUT * 4);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
@@ -1567,6 +1574,7 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
 
   if (wid == NWC) {
     if ((int)blockIdx.x < ntiles) issue_halo(blockIdx.x, 0);
+    if (NBUF == 3 && (int)blockIdx.x + G < ntiles) issue_halo(blockIdx.x + G, 1);
   } else {
     if (sums) {
       for (int i = tid; i < 6 * COUT; i += 64 * NWC) red[i] = 0.f;
@@ -1597,26 +1605,23 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
   if (wid == NWC) {
     int k = 0;
     for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
-      vm_wait<0>();  // this tile's halo has landed
+      // this tile's halo has landed (with three buffers the next tile's, issued
+      // after it, may still be in flight: its NB DMAs are the newest)
+      if (NBUF == 3 && tile + G < ntiles) vm_wait<NB>();
+      else vm_wait<0>();
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (tile + G < ntiles) issue_halo(tile + G, (k + 1) & 1);
+      // the buffer of tile k-1, which every compute wave left before this barrier
+      if (tile + (NBUF - 1) * G < ntiles) issue_halo(tile + (NBUF - 1) * G, (k + NBUF - 1) % NBUF);
     }
     vm_wait<0>();
     return;
   }
-  int k = 0;
-  for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // halo k visible; buffer (k+1)&1 and the statistics accumulator free
-    asm volatile("" ::: "memory");
+  // per MFMA pixel tile j of a tile: this lane's output pixel and its halo position
+  auto tile_px = [&](int tile, long long (&px)[NTP], bool (&pv)[NTP], int (&qb)[NTP]) {
     const int img = tile / (nth * ntw), rem = tile - img * (nth * ntw);
     const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
     const long long pimg = (long long)img * HoWo;
-    // per MFMA pixel tile j: this lane's output pixel and its halo position
-    long long px[NTP];
-    bool pv[NTP];
-    int qb[NTP];
 #pragma unroll
     for (int j = 0; j < NTP; ++j) {
       const int m = wid * NTP + j, row = m / TCB, cb = m - (m / TCB) * TCB;
@@ -1625,18 +1630,40 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
       px[j] = pv[j] ? pimg + oh * a.Wo + ow : pimg;
       qb[j] = row * HW + cb * 16 + fr;
     }
-    const long long wseg = a.seg_m > 0 ? pimg / a.seg_m : 0;
-    // ---- epilogue operands ahead of the MFMAs
-    Vec16<bf16> yp[NP][NTP];
-    if constexpr (BNB) {
+    return pimg;
+  };
+  // the BN-backward operand of a tile is loaded one tile ahead (issued after the
+  // previous tile's epilogue, consumed in this tile's), so its latency runs
+  // under the barrier and the MFMAs instead of in front of them
+  Vec16<bf16> yp[NP][NTP];
+  auto load_yp = [&](const long long (&px)[NTP]) {
 #pragma unroll
-      for (int p = 0; p < NP; ++p)
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int j = 0; j < NTP; ++j)
-          yp[p][j] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + px[j] * a.ldy + 32 * p + 8 * fq);
+      for (int j = 0; j < NTP; ++j)
+        yp[p][j] = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + px[j] * a.ldy + 32 * p + 8 * fq);
+  };
+  if constexpr (BNB) {
+    if ((int)blockIdx.x < ntiles) {
+      long long px0[NTP];
+      bool pv0[NTP];
+      int qb0[NTP];
+      tile_px(blockIdx.x, px0, pv0, qb0);
+      load_yp(px0);
     }
+  }
+  int k = 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += G, ++k) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // halo k visible; buffer (k-1) % NBUF and the statistics accumulator free
+    asm volatile("" ::: "memory");
+    long long px[NTP];
+    bool pv[NTP];
+    int qb[NTP];
+    const long long pimg = tile_px(tile, px, pv, qb);
+    const long long wseg = a.seg_m > 0 ? pimg / a.seg_m : 0;
     // ---- MFMAs: filters (A) and halo (B) from LDS
-    const char* hb = smem + WB + (k & 1) * HB;
+    const char* hb = smem + WB + (k % NBUF) * HB;
     f32x4 acc[MTC][NTP];
 #pragma unroll
     for (int i = 0; i < MTC; ++i)
@@ -1729,6 +1756,15 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
             atomicAdd(red + COUT + ch0 + e, s2[e]);
           }
         }
+      }
+    }
+    if constexpr (BNB) {
+      if (tile + G < ntiles) {
+        long long pxn[NTP];
+        bool pvn[NTP];
+        int qbn[NTP];
+        tile_px(tile + G, pxn, pvn, qbn);
+        load_yp(pxn);
       }
     }
     if (sums) stats_flush<COUT>(red, red_cnt, NWC * (k + 1) - 1, a, 0, tile % ARTSBIR_NSLOT, lane, pimg, 1);
