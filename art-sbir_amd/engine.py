@@ -47,6 +47,10 @@ BN_MOMENTUM = 0.1
 FUSE_BNB = os.environ.get("ARTSBIR_FUSE_BNB", "1") != "0"
 # ARTSBIR_OVERLAP_WGRAD=0 keeps the weight gradients on the caller's stream
 OVERLAP_WGRAD = os.environ.get("ARTSBIR_OVERLAP_WGRAD", "1") != "0"
+# ARTSBIR_WGRAD_MAIN=1x1 | 3x3: that class of weight gradients runs in order on
+# the main stream instead of the side stream (experiment: HBM-bound 1x1 wgrads
+# beside an HBM-bound main chain contend for bandwidth without hiding anything)
+WGRAD_MAIN = os.environ.get("ARTSBIR_WGRAD_MAIN", "")
 # ARTSBIR_MASK_BITS=0 makes the fused backward re-read the block output for its
 # ReLU mask instead of the bit mask written by the forward
 MASK_BITS = os.environ.get("ARTSBIR_MASK_BITS", "1") != "0"
@@ -802,7 +806,7 @@ class Engine:
         of the main stream; backward() joins the streams at the end."""
         if SKIP_WGRAD[0]:  # measurement only (tools/cu_mask_sweep.py): the main stream's critical path
             return
-        if not OVERLAP_WGRAD:
+        if not OVERLAP_WGRAD or (WGRAD_MAIN and WGRAD_MAIN == ("1x1" if conv.weight.shape[2] == 1 else "3x3")):
             return self._wgrad_sync(dy, a, conv, stride, pad, grads, ci_pad)
         main = torch.cuda.current_stream()
         side = self._side_stream(dy.device)
