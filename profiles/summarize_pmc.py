@@ -55,9 +55,10 @@ def short(name):
     if m:
         k, t = m.group(1), [x.strip() for x in m.group(2).split(",")]
         fb = ",bnb" if t[-1] == "true" and k == "sconv_kernel" else ""
-        if k == "pgemm_kernel":  # <BPX, BCH, WPX, WCH, NSTAGE, MULTI, BK, TWO, PF, KS>
+        if k == "pgemm_kernel":  # <BPX, BCH, WPX, WCH, NSTAGE, MULTI, BK, TWO, PF, KS, GLB>
             k32 = ",k32" if len(t) > 9 and t[9] == "32" else ""
-            return f"{k}<{t[0]},{t[1]}{k32}{',bnb' if t[6] != '0' else ''}{',pf' if t[8] == 'true' else ''}>"
+            glb = ",glb" if len(t) > 10 and t[10] == "true" else ""
+            return f"{k}<{t[0]},{t[1]}{k32}{glb}{',bnb' if t[6] != '0' else ''}{',pf' if t[8] == 'true' else ''}>"
         if k == "pwgrad_kernel":  # <BM, BN, WM, WN, NSTAGE, ...>: the 256 x 256 tiles carry their wave grid
             return f"{k}<{t[0]},{t[1]}{f',w{t[2]}x{t[3]}' if t[0] == t[1] == '256' else ''}>"
         if k == "hwgrad_kernel":  # <CT, OT, TR, NWC>: the 4-wave 64 x 64 variant is named w4
