@@ -775,6 +775,7 @@ static int run_old(const ConvArgs& a, hipStream_t st) {
 
 static bool run_candidate(int c, const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   if (c == -2) return a.res_mode != 3 && run_old<bf16>(a, st) == 0;
+  if (c == -3) return blt_gemm_nt(p, st);
   return pgemm_launch_cfg(p, c, st);
 }
 
@@ -806,7 +807,7 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   // caller's overlapped weight gradients) would otherwise share the chip with
   // some trials and not others and make the choice noisy
   (void)hipDeviceSynchronize();
-  static const int cands[] = {-2, 0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 20, 21};
+  static const int cands[] = {-2, -3, 0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 20, 21};
   int best = -2;
   float best_ms = 1e30f;
   for (int c : cands) {
@@ -887,6 +888,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
         g_conv_choice[key] = choice;
       }
     }
+    if (choice == -3 && blt_gemm_nt(p, st)) return 0;
     if ((choice != -2 && pgemm_launch_cfg(p, choice, st)) || (bd && force_bnb && pgemm_launch_cfg(p, 0, st))) {
       ARTSBIR_CHECK_LAUNCH("pgemm");
       return 0;

@@ -71,5 +71,8 @@ int pwgrad_level(int c);
 bool pgemm_launch_cfg(const PgArgs& a, int cfg, hipStream_t st);
 // Heuristic candidate for a shape (-1: unsupported).
 int pgemm_default_cfg(const PgArgs& a);
+// candidate -3 (blaslt.cpp): a plain dense bf16 NT GEMM (H = W = R = S = 1, no
+// fused epilogue) through hipBLASLt; false, launching nothing, otherwise
+bool blt_gemm_nt(const PgArgs& a, hipStream_t st);
 
 }  // namespace artsbir

@@ -839,7 +839,7 @@ template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bo
           bool GLB = false>
 __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? 3 : 1) pgemm_kernel(PgArgs a) {
   constexpr bool BNB = BK != 0;
-  static_assert(!GLB || (BNB && !PF), "GLB: fused BN-backward epilogue only");
+  static_assert(!GLB || !PF, "GLB: operands from global memory, not prefetched into registers");
   static_assert(!PF || BK != 2, "PF: the bf16 mask operand of kind 2 is not prefetched");
   static_assert(KS == 64 || (KS == 32 && !MULTI), "32-k stages: uniform taps only");
   constexpr int ROWB = 2 * KS, RPI = 1024 / ROWB, CPR = ROWB / 16;
@@ -1026,7 +1026,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? 3 : 1) pgemm_kernel(PgAr
     EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
     pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true>(a, acc, bpx, bch, wpx, wch,
                                                                                           fr, fq, red, sgg);
-    stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
+    if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
     return;
   }
   if constexpr (BNB) {
@@ -1990,11 +1990,21 @@ static bool pg_supported(const PgArgs& a, bool& multi) {
   return true;
 }
 
-// candidate 16: the fused BN-backward data gradient on a 128 x 128 tile (4
-// waves) with 32-k stages (3-stage ring, 48 KB) and its epilogue operands read
-// from global memory (GLB): three workgroups per CU
+// candidate 16: the fused BN-backward data gradient (or a plain one with a
+// residual / gate operand) on a 128 x 128 tile (4 waves) with 32-k stages
+// (3-stage ring, 48 KB) and its epilogue operands read from global memory
+// (GLB): three workgroups per CU
 static bool pg_glb_launch(const PgArgs& a, bool multi, hipStream_t st) {
-  if (!a.bnb || multi) return false;
+  if (multi) return false;
+  if (!a.bnb) {  // plain epilogue with a residual or gate operand (res_mode 1-3), read from global memory
+    if (!a.res_mode || a.bias || a.relu) return false;
+    const long long tiles = ((a.M + 127) / 128) * ((a.Cout + 127) / 128);
+    if (tiles > 0x7fffffffLL) return false;
+    hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 3, false, 0, false, false, 32, true>), dim3((unsigned)tiles),
+                       dim3(256), 0, st, a);
+    set_last_kernel("pgemm_kernel<128,128,k32,glb>");
+    return true;
+  }
   if (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) return false;
   if (a.bnb != 1 && !a.res_mode) return false;
   const long long tiles = ((a.M + 127) / 128) * ((a.Cout + 127) / 128);
@@ -2017,7 +2027,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
   if (act && (a.stats || a.bnb)) return false;
   // res_mode 3 (gated data gradient, pg_epilogue_k only): the plain pgemm_kernel tiles
-  if (a.res_mode == 3 && (c < 0 || c >= kNumCfg || a.bnb || a.R * a.S != 1)) return false;
+  if (a.res_mode == 3 && (c < 0 || (c >= kNumCfg && c != 16) || a.bnb || a.R * a.S != 1)) return false;
   if (c == 20) return !act && sconv_launch(a, st);
   if (c == 21) return hconv_launch(a, st);  // bias / ReLU epilogue supported
   if (act && c >= 11 && c <= 13) return false;

@@ -28,7 +28,7 @@ CASES = [
     (2, 32, 16, 32, 64, 3, 3, 1, 1),    # halo-tiled, 16 x 16 tiles, 32 -> 64 channels
     (3, 17, 23, 64, 32, 3, 3, 1, 1),    # halo-tiled, 8 x 16 tiles with row and column tails
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "20", "21"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "20", "21"]
 
 
 @pytest.fixture
@@ -255,3 +255,24 @@ def test_gemm_nt_bf16_bias(M, N, K, dev):
               biasd.data_ptr(), None, _hip.stream())
     torch.cuda.synchronize()
     assert torch.allclose(c.float().cpu(), ref, atol=3e-2, rtol=1e-2), (c.float().cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("M,N,K,lda,ldc", [(600, 512, 256, 256, 512), (1000, 768, 768, 800, 776), (4096, 2304, 768, 768, 2304),
+                                           (57, 96, 64, 64, 96)])
+def test_gemm_nt_hipblaslt_candidate(M, N, K, lda, ldc, dev, cfg_env):
+    """autotuner candidate -3 (plain dense bf16 NT GEMM through hipBLASLt, strided
+    operands) vs torch fp32 on the same bf16 operands"""
+    g = torch.Generator().manual_seed(13)
+    a = torch.randn(M, lda, generator=g).bfloat16()
+    b = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    ref = a[:, :K].float() @ b.float().T
+    c = torch.full((M, ldc), 7.0, dtype=torch.bfloat16, device=dev)
+    ad, bd = a.to(dev), b.to(dev)
+    _set("-3")
+    _hip.call("artsbir_gemm_nt", _hip.DT_BF16, M, N, K, ad.data_ptr(), lda, bd.data_ptr(), c.data_ptr(), ldc, 0, 0,
+              None, None, _hip.stream())
+    torch.cuda.synchronize()
+    assert _hip.lib().artsbir_last_kernel().decode() == "hipblaslt_gemm_nt"
+    out = c.float().cpu()
+    assert torch.allclose(out[:, :N], ref, atol=3e-2, rtol=1e-2), (out[:, :N] - ref).abs().max()
+    assert torch.all(out[:, N:] == 7.0)  # the row padding beyond N is untouched

@@ -379,12 +379,16 @@ def test_fp8_gemm_residual_and_second_output(M, N, K, dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg", ["auto", "0", "3", "16"])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 768), (1000, 3072, 768), (4096, 256, 128)])
-def test_gemm_nt_gate_matches_gemm_then_quickgelu_bwd(M, N, K, dev):
+def test_gemm_nt_gate_matches_gemm_then_quickgelu_bwd(M, N, K, cfg, dev, monkeypatch):
     """artsbir_gemm_nt_gate = (a @ b^T) * quickgelu'(x) (the c_proj input gradient
     through QuickGELU.backward, models.py:391-393) in bf16, with its column sums
-    (the c_fc bias gradient) in the statistics slots; ragged M"""
+    (the c_fc bias gradient) in the statistics slots; ragged M; per tile candidate
+    (16: the 128 x 128 tile with the gate operand read from global memory)"""
     import _hip
+    if cfg != "auto":
+        monkeypatch.setenv("ARTSBIR_PGEMM_CFG", cfg)
     g = torch.Generator(device=dev).manual_seed(31)
     a = torch.randn(M, K, device=dev, generator=g).bfloat16()
     b = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
