@@ -1875,7 +1875,8 @@ static bool pg_pf_launch(int c, const PgArgs& a, bool multi, hipStream_t st) {
   const int base = c - 10;
   if (multi || base < 1 || base > 3) return false;
   if (a.bnb == 2 || (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) || (a.bnb == 3 && !a.res_mode)) return false;
-  if (!a.bnb && (!a.res_mode || a.stats)) return false;  // plain: the data gradient with a residual
+  // plain: the data gradient with a residual, or the gated GEMM (res_mode 3, column sums in stats)
+  if (!a.bnb && (!a.res_mode || (a.stats && a.res_mode != 3))) return false;
   const PgCfg& g = kCfgs[base];
   const long long tiles = ((a.M + g.bpx - 1) / g.bpx) * ((a.Cout + g.bch - 1) / g.bch);
   if (tiles > 0x7fffffffLL) return false;
@@ -2027,7 +2028,8 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
   if (act && (a.stats || a.bnb)) return false;
   // res_mode 3 (gated data gradient, pg_epilogue_k only): the plain pgemm_kernel tiles
-  if (a.res_mode == 3 && (c < 0 || (c >= kNumCfg && c != 16) || a.bnb || a.R * a.S != 1)) return false;
+  if (a.res_mode == 3 && (c < 0 || (c >= kNumCfg && c != 16 && (c < 11 || c > 13)) || a.bnb || a.R * a.S != 1))
+    return false;
   if (c == 20) return !act && sconv_launch(a, st);
   if (c == 21) return hconv_launch(a, st);  // bias / ReLU epilogue supported
   if (act && c >= 11 && c <= 13) return false;

@@ -379,7 +379,7 @@ def test_fp8_gemm_residual_and_second_output(M, N, K, dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg", ["auto", "0", "3", "16"])
+@pytest.mark.parametrize("cfg", ["auto", "0", "3", "11", "12", "13", "16"])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 768), (1000, 3072, 768), (4096, 256, 128)])
 def test_gemm_nt_gate_matches_gemm_then_quickgelu_bwd(M, N, K, cfg, dev, monkeypatch):
     """artsbir_gemm_nt_gate = (a @ b^T) * quickgelu'(x) (the c_proj input gradient
