@@ -35,6 +35,23 @@ template <> __device__ __forceinline__ void store8<float>(float* p, const float 
 }
 __device__ __forceinline__ void loadf8(const float* p, float (&v)[8]) { load8<float>(p, v); }
 
+// streaming read of an operand the kernel is its last reader of (non-temporal:
+// no cache allocation for lines nobody reads again); ARTSBIR_NT_LOADS=0 plain
+#ifndef ARTSBIR_NT_LOADS
+#define ARTSBIR_NT_LOADS 1
+#endif
+typedef unsigned nt_u32x4 __attribute__((ext_vector_type(4)));
+template <typename T> __device__ __forceinline__ void load8_last(const T* p, float (&v)[8]) {
+  if constexpr (ARTSBIR_NT_LOADS && sizeof(T) == 2) {
+    const nt_u32x4 r = __builtin_nontemporal_load(reinterpret_cast<const nt_u32x4*>(p));
+    const bf16* b = reinterpret_cast<const bf16*>(&r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (float)b[i];
+  } else {
+    load8<T>(p, v);
+  }
+}
+
 static inline unsigned grid_for(long long n, int block = 256, long long cap = 1 << 20) {
   long long g = (n + block - 1) / block;
   if (g > cap) g = cap;
@@ -700,11 +717,16 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
 #pragma unroll
     for (int i = 0; i < UN; ++i) {
       const int u = min(ub + i * RL, u1 - 1);  // clamped: a tail unit recomputes the last one, stored once
-      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs[i], g[i], mm, ms, mh);
+      if constexpr (KIND == 2 && POOL == 1) {  // g after a fused dgrad: this is its last read
+        offs[i][0] = (long long)u * a.C + cg * 8;
+        load8_last<T>(reinterpret_cast<const T*>(a.d) + offs[i][0], g[i][0]);
+      } else {
+        bnb_unit_g<T, KIND, POOL>(a, u, cg, offs[i], g[i], mm, ms, mh);
+      }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) load8<T>(yp[t] + offs[i][q], y[i][t][q]);
+        for (int q = 0; q < NQ; ++q) load8_last<T>(yp[t] + offs[i][q], y[i][t][q]);
     }
 #pragma unroll
     for (int i = 0; i < UN; ++i) {
