@@ -28,7 +28,7 @@ struct BltPlan {
   size_t ws = 0;
   bool ok = false;
 };
-using BltKey = std::tuple<long long, int, int, long long, long long>;
+using BltKey = std::tuple<long long, int, int, long long, long long, bool>;
 std::mutex g_blt_mu;
 hipblasLtHandle_t g_blt = nullptr;
 void* g_blt_ws = nullptr;
@@ -42,12 +42,19 @@ bool blt_init() {
   return true;
 }
 
-BltPlan make_plan(long long M, int N, int K, long long lda, long long ldc) {
+BltPlan make_plan(long long M, int N, int K, long long lda, long long ldc, const float* bias) {
   BltPlan pl;
   const hipblasOperation_t tA = HIPBLAS_OP_T, tB = HIPBLAS_OP_N;
   if (hipblasLtMatmulDescCreate(&pl.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return pl;
   hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_TRANSA, &tA, sizeof(tA));
   hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tB, sizeof(tB));
+  if (bias) {  // f32 bias per row of D = per output column of the row-major C
+    const hipblasLtEpilogue_t ep = HIPBLASLT_EPILOGUE_BIAS;
+    const hipDataType bt = HIP_R_32F;
+    hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep));
+    hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt));
+    hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias, sizeof(bias));
+  }
   if (hipblasLtMatrixLayoutCreate(&pl.la, HIP_R_16BF, (uint64_t)K, (uint64_t)N, (int64_t)K) != HIPBLAS_STATUS_SUCCESS ||
       hipblasLtMatrixLayoutCreate(&pl.lb, HIP_R_16BF, (uint64_t)K, (uint64_t)M, (int64_t)lda) != HIPBLAS_STATUS_SUCCESS ||
       hipblasLtMatrixLayoutCreate(&pl.lc, HIP_R_16BF, (uint64_t)N, (uint64_t)M, (int64_t)ldc) != HIPBLAS_STATUS_SUCCESS)
@@ -70,18 +77,21 @@ BltPlan make_plan(long long M, int N, int K, long long lda, long long ldc) {
 }  // namespace
 
 // the dense NT GEMM of a PgArgs (H = W = 1, 1x1 "conv" over M rows) with a plain
-// bf16 output; false (nothing launched) when the launch fuses anything
+// bf16 output (+ an f32 bias per output column); false (nothing launched) when
+// the launch fuses anything else
 bool blt_gemm_nt(const PgArgs& a, hipStream_t st) {
   if (a.H != 1 || a.W != 1 || a.R != 1 || a.S != 1 || a.C != a.K || a.Ho != 1 || a.Wo != 1) return false;
-  if (a.stats || a.bnb || a.res_mode || a.relu || a.bias || a.M <= 0) return false;
+  if (a.stats || a.bnb || a.res_mode || a.relu || a.M <= 0) return false;
   const long long lda = a.sN, ldc = a.ldy;
   std::lock_guard<std::mutex> lk(g_blt_mu);
   if (!blt_init()) return false;
-  const BltKey key{a.M, a.Cout, a.K, lda, ldc};
+  const BltKey key{a.M, a.Cout, a.K, lda, ldc, a.bias != nullptr};
   auto it = g_blt_plans.find(key);
-  if (it == g_blt_plans.end()) it = g_blt_plans.emplace(key, make_plan(a.M, a.Cout, a.K, lda, ldc)).first;
+  if (it == g_blt_plans.end()) it = g_blt_plans.emplace(key, make_plan(a.M, a.Cout, a.K, lda, ldc, a.bias)).first;
   const BltPlan& pl = it->second;
   if (!pl.ok) return false;
+  if (a.bias)  // this call's bias vector (the cached plan was made with another one)
+    hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &a.bias, sizeof(a.bias));
   const float alpha = 1.f, beta = 0.f;
   const hipblasStatus_t s = hipblasLtMatmul(g_blt, pl.op, &alpha, a.w, pl.la, a.x, pl.lb, &beta, a.y, pl.lc, a.y, pl.lc,
                                             &pl.algo, g_blt_ws, pl.ws, st);

@@ -259,18 +259,21 @@ def test_gemm_nt_bf16_bias(M, N, K, dev):
 
 @pytest.mark.parametrize("M,N,K,lda,ldc", [(600, 512, 256, 256, 512), (1000, 768, 768, 800, 776), (4096, 2304, 768, 768, 2304),
                                            (57, 96, 64, 64, 96)])
-def test_gemm_nt_hipblaslt_candidate(M, N, K, lda, ldc, dev, cfg_env):
+@pytest.mark.parametrize("with_bias", [False, True], ids=["plain", "bias"])
+def test_gemm_nt_hipblaslt_candidate(M, N, K, lda, ldc, with_bias, dev, cfg_env):
     """autotuner candidate -3 (plain dense bf16 NT GEMM through hipBLASLt, strided
-    operands) vs torch fp32 on the same bf16 operands"""
+    operands, optional f32 bias per output column) vs torch fp32 on the same bf16
+    operands"""
     g = torch.Generator().manual_seed(13)
     a = torch.randn(M, lda, generator=g).bfloat16()
     b = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
-    ref = a[:, :K].float() @ b.float().T
+    bias = torch.randn(N, generator=g)
+    ref = a[:, :K].float() @ b.float().T + (bias if with_bias else 0)
     c = torch.full((M, ldc), 7.0, dtype=torch.bfloat16, device=dev)
-    ad, bd = a.to(dev), b.to(dev)
+    ad, bd, biasd = a.to(dev), b.to(dev), bias.to(dev)
     _set("-3")
     _hip.call("artsbir_gemm_nt", _hip.DT_BF16, M, N, K, ad.data_ptr(), lda, bd.data_ptr(), c.data_ptr(), ldc, 0, 0,
-              None, None, _hip.stream())
+              biasd.data_ptr() if with_bias else None, None, _hip.stream())
     torch.cuda.synchronize()
     assert _hip.lib().artsbir_last_kernel().decode() == "hipblaslt_gemm_nt"
     out = c.float().cpu()
