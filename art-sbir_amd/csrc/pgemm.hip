@@ -837,7 +837,7 @@ __device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&a
 // epilogue streams while another's main loop runs
 template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false, int KS = 64,
           bool GLB = false>
-__global__ void __launch_bounds__(64 * WPX * WCH, GLB ? 3 : 1) pgemm_kernel(PgArgs a) {
+__global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3) : 1) pgemm_kernel(PgArgs a) {
   constexpr bool BNB = BK != 0;
   static_assert(!GLB || !PF, "GLB: operands from global memory, not prefetched into registers");
   static_assert(!PF || BK != 2, "PF: the bf16 mask operand of kind 2 is not prefetched");
@@ -2023,6 +2023,20 @@ static bool pg_glb_launch(const PgArgs& a, bool multi, hipStream_t st) {
   return true;
 }
 
+// candidate 18: the fused BN-backward RES dgrad with the mask as bits (kind 3,
+// one target) on a 256 x 128 tile of 8 waves, 32-k stages in a 3-stage ring
+// (72 KB), epilogue operands from global memory: two workgroups (16 waves) per
+// CU at 128 VGPRs (the other kinds spill there)
+static bool pg_glb2_launch(const PgArgs& a, bool multi, hipStream_t st) {
+  if (multi || a.bnb != 3 || a.bnb_nt != 1 || !a.res_mode) return false;
+  const long long tiles = ((a.M + 255) / 256) * ((a.Cout + 127) / 128);
+  if (tiles > 0x7fffffffLL) return false;
+  hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, false, 3, false, false, 32, true>), dim3((unsigned)tiles),
+                     dim3(512), 0, st, a);
+  set_last_kernel("pgemm_kernel<256,128,k32,glb,bnb>");
+  return true;
+}
+
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
@@ -2039,6 +2053,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (c == 14) return pstream_bnb_launch(a, multi, st);
   if (c == 15) return pstream_k32_launch(a, multi, st);
   if (c == 16) return pg_glb_launch(a, multi, st);
+  if (c == 18) return pg_glb2_launch(a, multi, st);
   if (c == 10) {
     const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
     const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);

@@ -46,6 +46,18 @@ def short(name):
     m = re.match(r"_ZN7artsbir12hconv_kernelILi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELb([01])E", name)
     if m:
         return f"hconv_kernel<{m.group(1)},{m.group(2)},{m.group(3)}x{m.group(4)}{',bnb' if m.group(5) == '1' else ''}>"
+    # BN-backward passes: <T, KIND, POOL, NT>, named by KIND as bench.py records
+    # them (bn_bwd_apply_kernel<2>); rocprofv3 prints most of these launches with
+    # a garbled demangling that keeps only the trailing arguments: ", EL, int, E,
+    # NT>" is KIND 2 (after a fused dgrad), ", int, E, 2, 1>" KIND 1 with POOL 2
+    m = re.match(r"_ZN7artsbir\d+(bn_bwd_(?:apply|reduce)_kernel)IDF16bLi(\d)E", name)  # mangled: KIND explicit
+    if m:
+        return f"{m.group(1)}<{m.group(2)}>"
+    # (the apply forms only: counted against the launches bench.py records per
+    # step — 46 of KIND 2, 4 of KIND 1 — the reduce forms are left generic)
+    m = re.match(r"(?:void )?artsbir::bn_bwd_apply_kernel<bool _Accum, int, (EL, int, E, \d|E, 2, 1)>", name)
+    if m:
+        return f"bn_bwd_apply_kernel<{'2' if m.group(1).startswith('EL') else '1'}>"
     m = re.match(r"_ZN7artsbir\d+(\w+?_kernel)", name)
     if m:
         return m.group(1)
