@@ -2037,6 +2037,19 @@ static bool pg_glb2_launch(const PgArgs& a, bool multi, hipStream_t st) {
   return true;
 }
 
+// candidate 19: the plain / statistics / bias-ReLU-residual epilogues on the
+// 256 x 128 8-wave tile with a 3-stage ring of 32-k stages and operands read
+// from global memory (72 KB of LDS): two workgroups per CU at 128 VGPRs
+static bool pg_k32w8_launch(const PgArgs& a, bool multi, hipStream_t st) {
+  if (multi || a.bnb || a.res_mode == 3) return false;
+  const long long tiles = ((a.M + 255) / 256) * ((a.Cout + 127) / 128);
+  if (tiles > 0x7fffffffLL) return false;
+  hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, false, 0, false, false, 32, true>), dim3((unsigned)tiles),
+                     dim3(512), 0, st, a);
+  set_last_kernel("pgemm_kernel<256,128,k32,glb>");
+  return true;
+}
+
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
@@ -2054,6 +2067,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (c == 15) return pstream_k32_launch(a, multi, st);
   if (c == 16) return pg_glb_launch(a, multi, st);
   if (c == 18) return pg_glb2_launch(a, multi, st);
+  if (c == 19) return pg_k32w8_launch(a, multi, st);
   if (c == 10) {
     const int bch = a.Cout <= 32 ? 32 : a.Cout <= 64 ? 64 : 128;
     const long long nt = ((a.M + 255) / 256) * ((a.Cout + bch - 1) / bch);

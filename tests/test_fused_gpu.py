@@ -14,7 +14,7 @@ import _hip
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "20", "21", "-2"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "-2"]
 
 
 @pytest.fixture

@@ -28,7 +28,7 @@ CASES = [
     (2, 32, 16, 32, 64, 3, 3, 1, 1),    # halo-tiled, 16 x 16 tiles, 32 -> 64 channels
     (3, 17, 23, 64, 32, 3, 3, 1, 1),    # halo-tiled, 8 x 16 tiles with row and column tails
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "20", "21"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21"]
 
 
 @pytest.fixture
@@ -197,7 +197,7 @@ def test_gemm_tn_strided(M, N, K, ldd, ldx, cfg, dev):
         os.environ.pop("ARTSBIR_WGRAD_CFG", None)
 
 
-@pytest.mark.parametrize("cfg", ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "21"])
+@pytest.mark.parametrize("cfg", ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "19", "21"])
 @pytest.mark.parametrize("case", CASES)
 @pytest.mark.parametrize("mode", ["bias", "bias_relu", "bias_res_relu"])
 def test_conv_fwd_act(case, cfg, mode, dev, cfg_env):
