@@ -82,10 +82,11 @@ SKIP_WGRAD = [False]
 _MASKED_STREAMS = {}
 
 
-def cu_masked_stream(device, ncu):
+def cu_masked_stream(device, ncu, invert=False):
     """a torch stream over a hipExtStreamCreateWithCUMask stream using ncu CUs
-    spread evenly over the device's CUs (cached per (device, ncu))"""
-    key = (device.index if device.index is not None else 0, ncu)
+    spread evenly over the device's CUs, or (invert) every CU but those
+    (cached per (device, ncu, invert))"""
+    key = (device.index if device.index is not None else 0, ncu, invert)
     st = _MASKED_STREAMS.get(key)
     if st is not None:
         return st
@@ -96,6 +97,10 @@ def cu_masked_stream(device, ncu):
     for i in range(ncu):
         cu = (i * total) // ncu
         mask[cu // 32] |= 1 << (cu % 32)
+    if invert:
+        for w in range(words):
+            bits = min(32, total - 32 * w)
+            mask[w] = ~mask[w] & ((1 << bits) - 1)
     handle = ctypes.c_void_p()
     with torch.cuda.device(device):
         call("artsbir_stream_create_cu_mask", mask, words, ctypes.byref(handle))

@@ -18,6 +18,9 @@ def main():
     import losses
     import models
     import optim
+    import _hip
+    if os.path.exists(bench.TUNE_CACHE):  # the committed autotuner table, as bench.py loads it
+        _hip.lib().artsbir_tune_load(bench.TUNE_CACHE.encode())
     dev = torch.device("cuda:0")
     torch.manual_seed(1234)
     model = models.ModifiedResNet(bench.LAYERS, bench.OUT_DIM, heads=bench.HEADS, input_resolution=bench.RES,
@@ -29,7 +32,8 @@ def main():
     B = int(os.environ.get("BATCH", "384"))
     g = torch.Generator(device=dev).manual_seed(100)
     batch = [torch.randn(B, 3, bench.RES, bench.RES, device=dev, generator=g) for _ in range(3)]
-    torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
+    main_default = torch.cuda.Stream(device=dev, priority=-1)
+    torch.cuda.set_stream(main_default)
 
     def step():
         loss = loss_fn(*model.forward_branches(batch))
@@ -40,8 +44,15 @@ def main():
     step()
     ks = sys.argv[1:] or ["0", "64", "96", "128", "160", "192", "0"]
     for k in ks:
+        # "xK": the side stream on K CUs and the main stream on every other CU
+        # "xKs": the main stream on every CU but those K, weight gradients skipped
+        split = k.startswith("x")
+        skip = split and k.endswith("s")
+        if split:
+            k = k[1:].rstrip("s")
+        torch.cuda.set_stream(engine.cu_masked_stream(dev, int(k), invert=True) if split else main_default)
         # "skip": no weight gradients (the main stream alone); "serial": on the main stream
-        engine.SKIP_WGRAD[0] = k == "skip"
+        engine.SKIP_WGRAD[0] = skip or k == "skip"
         engine.OVERLAP_WGRAD = k != "serial"
         engine.SIDE_CUS[0] = int(k) if k.isdigit() else 0
         step()
@@ -51,7 +62,7 @@ def main():
         for _ in range(n):
             step()
         torch.cuda.synchronize()
-        print(f"side CUs {k:>6}: {(time.perf_counter() - t0) / n * 1e3:8.2f} ms/step", flush=True)
+        print(f"side CUs {('x' if split else '') + k + ('s' if skip else ''):>6}: {(time.perf_counter() - t0) / n * 1e3:8.2f} ms/step", flush=True)
 
 
 if __name__ == "__main__":
