@@ -77,16 +77,17 @@ def set_deterministic(on: bool = True) -> bool:
 
 # ARTSBIR_SIDE_CUS=K: the weight-gradient stream is restricted to K CUs (0: all)
 SIDE_CUS = [int(os.environ.get("ARTSBIR_SIDE_CUS", "0"))]
+SIDE_CONTIGUOUS = [False]  # measurement switch: those K CUs are mask bits 0..K-1
 # measurement switch (never set in a real step): leave the weight gradients out
 SKIP_WGRAD = [False]
 _MASKED_STREAMS = {}
 
 
-def cu_masked_stream(device, ncu, invert=False):
+def cu_masked_stream(device, ncu, invert=False, contiguous=False):
     """a torch stream over a hipExtStreamCreateWithCUMask stream using ncu CUs
-    spread evenly over the device's CUs, or (invert) every CU but those
-    (cached per (device, ncu, invert))"""
-    key = (device.index if device.index is not None else 0, ncu, invert)
+    spread evenly over the device's CUs (contiguous: mask bits 0..ncu-1), or
+    (invert) every CU but those (cached per (device, ncu, invert, contiguous))"""
+    key = (device.index if device.index is not None else 0, ncu, invert, contiguous)
     st = _MASKED_STREAMS.get(key)
     if st is not None:
         return st
@@ -95,7 +96,7 @@ def cu_masked_stream(device, ncu, invert=False):
     words = (total + 31) // 32
     mask = (ctypes.c_uint * words)()
     for i in range(ncu):
-        cu = (i * total) // ncu
+        cu = i if contiguous else (i * total) // ncu
         mask[cu // 32] |= 1 << (cu % 32)
     if invert:
         for w in range(words):
@@ -796,12 +797,13 @@ class Engine:
         CUs (spread evenly over the chip), so the main stream's HBM-bound chain
         always finds free CUs while the MFMA-bound weight gradients run beside it"""
         st = getattr(self, "_side", None)
-        if st is None or st.device != device or getattr(self, "_side_cus", None) != SIDE_CUS[0]:
+        want = (SIDE_CUS[0], SIDE_CONTIGUOUS[0])
+        if st is None or st.device != device or getattr(self, "_side_cus", None) != want:
             if SIDE_CUS[0] > 0:
-                st = self._side = cu_masked_stream(device, SIDE_CUS[0])
+                st = self._side = cu_masked_stream(device, SIDE_CUS[0], contiguous=SIDE_CONTIGUOUS[0])
             else:
                 st = self._side = torch.cuda.Stream(device=device)
-            self._side_cus = SIDE_CUS[0]
+            self._side_cus = want
         return st
 
     def _wgrad(self, dy, a: Act, conv, stride, pad, grads, ci_pad=None):

@@ -46,11 +46,15 @@ def main():
     for k in ks:
         # "xK": the side stream on K CUs and the main stream on every other CU
         # "xKs": the main stream on every CU but those K, weight gradients skipped
-        split = k.startswith("x")
+        # "cK": as "xK" with the side stream on mask bits 0..K-1 instead of spread CUs
+        contig = k.startswith("c")
+        split = k.startswith("x") or contig
         skip = split and k.endswith("s")
         if split:
             k = k[1:].rstrip("s")
-        torch.cuda.set_stream(engine.cu_masked_stream(dev, int(k), invert=True) if split else main_default)
+        engine.SIDE_CONTIGUOUS[0] = contig
+        torch.cuda.set_stream(engine.cu_masked_stream(dev, int(k), invert=True, contiguous=contig) if split
+                              else main_default)
         # "skip": no weight gradients (the main stream alone); "serial": on the main stream
         engine.SKIP_WGRAD[0] = skip or k == "skip"
         engine.OVERLAP_WGRAD = k != "serial"
@@ -62,7 +66,7 @@ def main():
         for _ in range(n):
             step()
         torch.cuda.synchronize()
-        print(f"side CUs {('x' if split else '') + k + ('s' if skip else ''):>6}: {(time.perf_counter() - t0) / n * 1e3:8.2f} ms/step", flush=True)
+        print(f"side CUs {('c' if contig else 'x' if split else '') + k + ('s' if skip else ''):>6}: {(time.perf_counter() - t0) / n * 1e3:8.2f} ms/step", flush=True)
 
 
 if __name__ == "__main__":
