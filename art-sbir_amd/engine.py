@@ -78,6 +78,10 @@ def set_deterministic(on: bool = True) -> bool:
 # ARTSBIR_SIDE_CUS=K: the weight-gradient stream is restricted to K CUs (0: all)
 SIDE_CUS = [int(os.environ.get("ARTSBIR_SIDE_CUS", "0"))]
 SIDE_CONTIGUOUS = [False]  # measurement switch: those K CUs are mask bits 0..K-1
+# ARTSBIR_WGRAD_DEFER=3x3|1x1|all: the side stream starts a layer's weight gradient
+# only after that layer's data gradient has run on the main stream (instead of
+# beside it), so the two GEMMs of one layer never compete for the same CUs
+WGRAD_DEFER = [os.environ.get("ARTSBIR_WGRAD_DEFER", "")]
 # measurement switch (never set in a real step): leave the weight gradients out
 SKIP_WGRAD = [False]
 _MASKED_STREAMS = {}
@@ -850,6 +854,19 @@ class Engine:
         if target is not g:
             call("artsbir_unpack_wgrad", ptr(target), co, ci, R, S, C, ptr(g), _s())
 
+    def _wgrad_pre(self, dy, a, conv, stride, pad, grads):
+        """issue a layer's weight gradient now, or hold it (WGRAD_DEFER) until
+        _wgrad_post is called after the layer's data gradient"""
+        k = WGRAD_DEFER[0]
+        if k and (k == "all" or k == ("1x1" if conv.weight.shape[2] == 1 else "3x3")):
+            return (dy, a, conv, stride, pad, grads)
+        self._wgrad(dy, a, conv, stride, pad, grads)
+        return None
+
+    def _wgrad_post(self, held):
+        if held is not None:
+            self._wgrad(*held)
+
     def _dgrad(self, dy, dw, conv, pad, out_shape, res=None, res_mode=0, fused=None):
         B, H, W, C = out_shape
         co, _, R, S = conv.weight.shape
@@ -892,30 +909,35 @@ class Engine:
             dys = self._bn_bwd(0, dout, targets, bnmods, ws, grads, mask=out, gout=gid)
         dy3 = dys[0]
         c3in = Act(p2)
-        self._wgrad(dy3, c3in, blk.conv3, 1, 0, grads)
+        held = self._wgrad_pre(dy3, c3in, blk.conv3, 1, 0, grads)
         c3out = c3in.shape[:3] + (blk.conv3.weight.shape[1],)
         if s == 1 and _fuse_bnb():
             f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
             g2 = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out, fused=f2)
+            self._wgrad_post(held)
             dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
         else:
             dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out)
+            self._wgrad_post(held)
             dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
-        self._wgrad(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
+        held = self._wgrad_pre(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
         if _fuse_bnb():
             f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
             g1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape, fused=f1)
+            self._wgrad_post(held)
             dy1, = self._bn_finish(g1, f1, [blk.bn1], grads)
         else:
             da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
+            self._wgrad_post(held)
             dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
-        self._wgrad(dy1, Act(h), blk.conv1, 1, 0, grads)
+        held1 = self._wgrad_pre(dy1, Act(h), blk.conv1, 1, 0, grads)
         if has_ds:
             dyd = dys[1]
             din = pd if s > 1 else h
             dconv = blk.downsample[1]
-            self._wgrad(dyd, Act(din), dconv, 1, 0, grads)
+            held = self._wgrad_pre(dyd, Act(din), dconv, 1, 0, grads)
             res = self._dgrad(dyd, bp["down"][1], dconv, 0, din.shape)
+            self._wgrad_post(held)
             res_mode = 2 if s > 1 else 1
         else:
             res, res_mode = gid, 1
@@ -928,27 +950,32 @@ class Engine:
             else:
                 fprev = self._bnb_fused_desc(0, ptargets, ws, mask=pc["out"])
         dh = self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=res, res_mode=res_mode, fused=fprev)
+        self._wgrad_post(held1)
         return dh, fprev
 
     def _stem_bwd(self, m, pk, c, dh, grads, ws):
         x0, y1, y2, y3, b1, b2, b3 = (c[k] for k in ("x0", "y1", "y2", "y3", "b1", "b2", "b3"))
         (_, _), (_, dw2), (_, dw3) = pk["stem"]
         dy3, = self._bn_bwd(1, dh, [(y3, b3)], [m.bn3], ws, grads, mask_bn=b3, pool=2)
-        self._wgrad(dy3, Act(c["a2"]), m.conv3, 1, 1, grads)
+        held = self._wgrad_pre(dy3, Act(c["a2"]), m.conv3, 1, 1, grads)
         if _fuse_bnb():
             f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
             g2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape, fused=f2)
+            self._wgrad_post(held)
             dy2, = self._bn_finish(g2, f2, [m.bn2], grads)
         else:
             da2 = self._dgrad(dy3, dw3, m.conv3, 1, y2.shape)
+            self._wgrad_post(held)
             dy2, = self._bn_bwd(1, da2, [(y2, b2)], [m.bn2], ws, grads, mask_bn=b2)
-        self._wgrad(dy2, Act(c["a1"]), m.conv2, 1, 1, grads)
+        held = self._wgrad_pre(dy2, Act(c["a1"]), m.conv2, 1, 1, grads)
         if _fuse_bnb():
             f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
             g1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape, fused=f1)
+            self._wgrad_post(held)
             dy1, = self._bn_finish(g1, f1, [m.bn1], grads)
         else:
             da1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape)
+            self._wgrad_post(held)
             dy1, = self._bn_bwd(1, da1, [(y1, b1)], [m.bn1], ws, grads, mask_bn=b1)
         self._wgrad(dy1, Act(x0), m.conv1, 2, 1, grads)
 
