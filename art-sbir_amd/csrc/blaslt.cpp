@@ -74,7 +74,58 @@ BltPlan make_plan(long long M, int N, int K, long long lda, long long ldc, const
   pl.ok = pl.ws <= kBltWs;
   return pl;
 }
+// dW (f32, [Cout][K] row-major) += dY^T X over M rows: column-major
+//   dW^T (K x Cout, ld K) = X (K x M, ld ldx) * op(dY) (M x Cout), dY stored
+//   column-major Cout x M (ld ldd, transposed); beta = 1 accumulates
+using BltWKey = std::tuple<long long, int, int, long long, long long>;
+std::map<BltWKey, BltPlan> g_blt_wplans;
+
+BltPlan make_wplan(long long M, int Cout, int K, long long ldx, long long ldd) {
+  BltPlan pl;
+  const hipblasOperation_t tA = HIPBLAS_OP_N, tB = HIPBLAS_OP_T;
+  if (hipblasLtMatmulDescCreate(&pl.op, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS) return pl;
+  hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_TRANSA, &tA, sizeof(tA));
+  hipblasLtMatmulDescSetAttribute(pl.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tB, sizeof(tB));
+  if (hipblasLtMatrixLayoutCreate(&pl.la, HIP_R_16BF, (uint64_t)K, (uint64_t)M, (int64_t)ldx) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&pl.lb, HIP_R_16BF, (uint64_t)Cout, (uint64_t)M, (int64_t)ldd) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&pl.lc, HIP_R_32F, (uint64_t)K, (uint64_t)Cout, (int64_t)K) != HIPBLAS_STATUS_SUCCESS)
+    return pl;
+  hipblasLtMatmulPreference_t pref;
+  if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return pl;
+  const uint64_t wsmax = kBltWs;
+  hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsmax, sizeof(wsmax));
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int nres = 0;
+  const hipblasStatus_t hs =
+      hipblasLtMatmulAlgoGetHeuristic(g_blt, pl.op, pl.la, pl.lb, pl.lc, pl.lc, pref, 1, res, &nres);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  if (hs != HIPBLAS_STATUS_SUCCESS || nres < 1 || res[0].state != HIPBLAS_STATUS_SUCCESS) return pl;
+  pl.algo = res[0].algo;
+  pl.ws = res[0].workspaceSize;
+  pl.ok = pl.ws <= kBltWs;
+  return pl;
+}
 }  // namespace
+
+// weight gradient of a dense 1x1 convolution (Xcol = X) through hipBLASLt,
+// accumulated into the f32 dW; false (nothing launched) when no plan exists
+bool blt_wgrad_tn(const void* dy, long long ldd, const void* x, long long ldx, int Cout, int K, long long M, float* dw,
+                  hipStream_t st) {
+  if (M <= 0 || Cout <= 0 || K <= 0) return false;
+  std::lock_guard<std::mutex> lk(g_blt_mu);
+  if (!blt_init()) return false;
+  const BltWKey key{M, Cout, K, ldx, ldd};
+  auto it = g_blt_wplans.find(key);
+  if (it == g_blt_wplans.end()) it = g_blt_wplans.emplace(key, make_wplan(M, Cout, K, ldx, ldd)).first;
+  const BltPlan& pl = it->second;
+  if (!pl.ok) return false;
+  const float alpha = 1.f, beta = 1.f;
+  const hipblasStatus_t s =
+      hipblasLtMatmul(g_blt, pl.op, &alpha, x, pl.la, dy, pl.lb, &beta, dw, pl.lc, dw, pl.lc, &pl.algo, g_blt_ws, pl.ws, st);
+  if (s != HIPBLAS_STATUS_SUCCESS) return false;
+  set_last_kernel("hipblaslt_wgrad_tn");
+  return true;
+}
 
 // the dense NT GEMM of a PgArgs (H = W = 1, 1x1 "conv" over M rows) with a plain
 // bf16 output (+ an f32 bias per output column); false (nothing launched) when

@@ -1158,6 +1158,8 @@ static void launch_wgrad_old(WgradArgs& a, hipStream_t st);
 // candidate -1: register-staged wgrad_kernel; c >= 0: pipelined config c
 static bool run_wg_candidate(int c, WgradArgs& a, hipStream_t st) {
   if (c >= 0) return pwgrad_launch(to_pw(a), c, st);
+  if (c == -3)  // hipBLASLt, dense 1x1 weight gradients only
+    return a.dense && blt_wgrad_tn(a.dy, a.ldd, a.x, a.ldx, a.Cout, a.K, a.M, a.dw, st);
   launch_wgrad_old<bf16>(a, st);
   return true;
 }
@@ -1183,7 +1185,8 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   // weight gradients share the chip with the data-gradient stream, which the
   // standalone timing here cannot see)
   static const int minlevel = getenv("ARTSBIR_WGRAD_MINLEVEL") ? atoi(getenv("ARTSBIR_WGRAD_MINLEVEL")) : 0;
-  for (int c = -1; c < pwgrad_num_cfgs(); ++c) {
+  for (int c = -3; c < pwgrad_num_cfgs(); ++c) {
+    if (c == -2) continue;
     if (c >= 0 && pwgrad_level(c) >= 0 && pwgrad_level(c) < minlevel) continue;
     if (!run_wg_candidate(c, at, st)) continue;
     float ms = 1e30f;
@@ -1228,6 +1231,7 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
       ARTSBIR_CHECK_LAUNCH("pwgrad");
       return 0;
     }
+    if (choice == -3 && a.dense && blt_wgrad_tn(a.dy, a.ldd, a.x, a.ldx, a.Cout, a.K, a.M, a.dw, st)) return 0;
   }
   launch_wgrad_old<T>(a, st);
   ARTSBIR_CHECK_LAUNCH("wgrad");

@@ -141,9 +141,9 @@ WG_CASES = [
 ]
 
 
-# candidates (gemm.hip tune_wgrad): -1 register-staged kernel, c + 9 * level the
+# candidates (gemm.hip tune_wgrad): -3 hipBLASLt (dense 1x1 only), -1 register-staged kernel, c + 9 * level the
 # pipelined kernel's 9 tile shapes at 4 split levels, 36 / 37 the halo-tiled kernel variants
-@pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "16", "20", "34", "36", "37",
+@pytest.mark.parametrize("cfg", ["-3", "-1", "0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "16", "20", "34", "36", "37",
                                  "auto"])
 @pytest.mark.parametrize("case", WG_CASES)
 def test_wgrad_accumulates(case, cfg, dev):
@@ -178,7 +178,7 @@ def test_wgrad_accumulates(case, cfg, dev):
             os.environ["ARTSBIR_WGRAD_CFG"] = old
 
 
-@pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "6", "7", "8"])
+@pytest.mark.parametrize("cfg", ["-3", "-1", "0", "1", "2", "3", "6", "7", "8"])
 @pytest.mark.parametrize("M,N,K,ldd,ldx", [(100, 96, 64, 96, 64), (3000, 512, 2048, 512, 2048), (77, 40, 24, 48, 32)])
 def test_gemm_tn_strided(M, N, K, ldd, ldx, cfg, dev):
     os.environ["ARTSBIR_WGRAD_CFG"] = cfg
