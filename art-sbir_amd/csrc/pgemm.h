@@ -69,6 +69,10 @@ int pwgrad_level(int c);
 // persistent streaming kernel).  Returns false, launching nothing, when the
 // shape is outside what that kernel supports.
 bool pgemm_launch_cfg(const PgArgs& a, int cfg, hipStream_t st);
+// Candidates 22 / 23 (pp256.hip): the ping-pong 256 x 256 tile, one tile per
+// workgroup / persistent over 256 workgroups; false when the shape or epilogue
+// is outside it (C % 32 != 0, LDS-staged operands).
+bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st);
 // Heuristic candidate for a shape (-1: unsupported).
 int pgemm_default_cfg(const PgArgs& a);
 // candidate -3 (blaslt.cpp): a plain dense bf16 NT GEMM (H = W = R = S = 1, no

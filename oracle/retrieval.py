@@ -169,3 +169,40 @@ def synthetic_gallery(n: int, d: int, q: int, seed_g: int = 7, seed_q: int = 8, 
     pos = (np.arange(q, dtype=np.int64) * 7919) % n
     qs = g[pos] + noise * np.random.Generator(np.random.PCG64(seed_q)).standard_normal((q, d), dtype=np.float32)
     return g, qs.astype(np.float32), pos
+
+
+def fp32_reference_order(qs: np.ndarray, g: np.ndarray, pos, k: int, metric: str = "euclidean",
+                         rows_per_chunk: int = 131072):
+    """The reference's own float32 op sequence (inference.py:43-56 and 60-66 on
+    the CPU): utils.euclidean_distance = nn.PairwiseDistance(p=2) (or the
+    CosineLoss of utils.py:31-40) of one sketch feature against every gallery
+    row, distances.topk(k, largest=False) for the top-k list and
+    distances.topk(N, largest=False) + position of the positive for the rank.
+    Rows are evaluated in chunks (each row's norm is its own reduction, so the
+    values equal the one-call result).  Returns (topk idx [Q,k], topk dist
+    [Q,k] float32, ranks [Q], -1 without a positive, and the per-query float32
+    distance of every top-k / positive item for the tie analysis)."""
+    import torch
+    G = torch.from_numpy(np.ascontiguousarray(g))
+    if metric == "euclidean":
+        fn = torch.nn.PairwiseDistance(p=2)
+    else:
+        cs = torch.nn.CosineSimilarity(dim=1)
+        fn = lambda a, b: cs(a, b) * -1 + 1  # noqa: E731  (utils.py:37-38)
+    n = G.shape[0]
+    out_i = np.zeros((len(qs), k), np.int64)
+    out_d = np.zeros((len(qs), k), np.float32)
+    ranks = np.full(len(qs), -1, np.int64)
+    dists = []
+    with torch.no_grad():
+        for qi, q in enumerate(qs):
+            qt = torch.from_numpy(np.ascontiguousarray(q))[None, :]
+            d = torch.cat([fn(qt, G[c0:c0 + rows_per_chunk]) for c0 in range(0, n, rows_per_chunk)])
+            v, i = d.topk(k, largest=False)
+            out_i[qi], out_d[qi] = i.numpy(), v.numpy()
+            p = int(pos[qi])
+            if p >= 0:
+                _, full = d.topk(n, largest=False)
+                ranks[qi] = int((full == p).nonzero().flatten()[0])
+            dists.append(d.numpy())
+    return out_i, out_d, ranks, dists

@@ -14,7 +14,7 @@ import _hip
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "-2"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "22", "23", "-2"]
 
 
 @pytest.fixture
@@ -32,6 +32,11 @@ def _set(cfg):
         os.environ.pop("ARTSBIR_PGEMM_CFG", None)
     else:
         os.environ["ARTSBIR_PGEMM_CFG"] = cfg
+    # candidate 23 (persistent pp256): 8 workgroups, so these small shapes walk several tiles each
+    if cfg == "23":
+        os.environ["ARTSBIR_PP_GRID"] = "8"
+    else:
+        os.environ.pop("ARTSBIR_PP_GRID", None)
 
 
 def _nhwc(x):

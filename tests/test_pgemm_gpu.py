@@ -28,7 +28,7 @@ CASES = [
     (2, 32, 16, 32, 64, 3, 3, 1, 1),    # halo-tiled, 16 x 16 tiles, 32 -> 64 channels
     (3, 17, 23, 64, 32, 3, 3, 1, 1),    # halo-tiled, 8 x 16 tiles with row and column tails
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21", "22", "23"]
 
 
 @pytest.fixture
@@ -46,6 +46,11 @@ def _set(cfg):
         os.environ.pop("ARTSBIR_PGEMM_CFG", None)
     else:
         os.environ["ARTSBIR_PGEMM_CFG"] = cfg
+    # candidate 23 (persistent pp256): 8 workgroups, so these small shapes walk several tiles each
+    if cfg == "23":
+        os.environ["ARTSBIR_PP_GRID"] = "8"
+    else:
+        os.environ.pop("ARTSBIR_PP_GRID", None)
 
 
 def _nhwc(x):
