@@ -49,8 +49,8 @@ def _threads():
     return max(1, min(16, n))
 
 
-def _build_oracle(damp):
-    r = osteps.build(C2["layers"], C2["output_dim"], C2["heads"], C2["res"], C2["width"])
+def _build_oracle(damp, cfg=C2):
+    r = osteps.build(cfg["layers"], cfg["output_dim"], cfg["heads"], cfg["res"], cfg["width"])
     if damp != 1.0:
         with torch.no_grad():
             for n, p in r.named_parameters():
@@ -59,8 +59,8 @@ def _build_oracle(damp):
     return r
 
 
-def _oracle_run(damp, elements, dt, autocast=False, backward=True):
-    r = _build_oracle(damp).to(dt)
+def _oracle_run(damp, elements, dt, autocast=False, backward=True, cfg=C2):
+    r = _build_oracle(damp, cfg).to(dt)
     r.train()
     if autocast:  # PyTorch's own bf16 path: convs/linears in bf16, BN in f32
         with torch.autocast("cpu", dtype=torch.bfloat16):
@@ -74,17 +74,16 @@ def _oracle_run(damp, elements, dt, autocast=False, backward=True):
     return out
 
 
-@pytest.fixture(scope="module")
-def oracle_c2():
+def oracle_runs(cfg, batch=B):
     """oracle runs of one triplet step's forward + backward (three separate
     train-mode forwards, TripletMarginLoss(0.2)) on the damped weights: float64,
     float32 and bf16 autocast; the float64 model's running statistics and its
     eval-mode embedding of the sketch batch"""
     torch.set_num_threads(_threads())
-    elements = oenc.synthetic_triplet(B, C2["res"], seed=3)
-    o64 = _oracle_run(DAMP, elements, torch.float64)
-    o32 = _oracle_run(DAMP, elements, torch.float32)
-    oac = _oracle_run(DAMP, elements, torch.float32, autocast=True)
+    elements = oenc.synthetic_triplet(batch, cfg["res"], seed=3)
+    o64 = _oracle_run(DAMP, elements, torch.float64, cfg=cfg)
+    o32 = _oracle_run(DAMP, elements, torch.float32, cfg=cfg)
+    oac = _oracle_run(DAMP, elements, torch.float32, autocast=True, cfg=cfg)
     r = o64.pop("model")
     o64["state"] = {k: v.double() if v.dtype.is_floating_point else v
                     for k, v in r.state_dict().items() if "running" in k or "num_batches" in k}
@@ -93,14 +92,19 @@ def oracle_c2():
         o64["eval"] = r(elements[0].double()).double()
     for o in (o32, oac):
         o.pop("model")
-    return {"elements": elements, "64": o64, "32": o32, "ac": oac}
+    return {"elements": elements, "64": o64, "32": o32, "ac": oac, "cfg": cfg}
 
 
-def _mine(dev, dtype, damp=DAMP):
+@pytest.fixture(scope="module")
+def oracle_c2():
+    return oracle_runs(C2)
+
+
+def _mine(dev, dtype, damp=DAMP, cfg=C2):
     import models
-    ref = _build_oracle(damp)
-    m = models.ModifiedResNet(C2["layers"], C2["output_dim"], heads=C2["heads"], input_resolution=C2["res"],
-                              width=C2["width"])
+    ref = _build_oracle(damp, cfg)
+    m = models.ModifiedResNet(cfg["layers"], cfg["output_dim"], heads=cfg["heads"], input_resolution=cfg["res"],
+                              width=cfg["width"])
     m.load_state_dict(ref.state_dict(), strict=True)
     m.compute_dtype = dtype
     return m.to(dev)
@@ -125,13 +129,13 @@ def _rel_l2(a, b):
     return float((a - b).norm() / max(b.norm().item(), 1e-30))
 
 
-def _conditioned(damp, elements, dt, masks):
+def _conditioned(damp, elements, dt, masks, cfg=C2):
     from oracle import encoder as oe
     from _parity import MaskFeed
     feed = MaskFeed(masks)
     oe.RELU = feed
     try:
-        out = _oracle_run(damp, elements, dt)
+        out = _oracle_run(damp, elements, dt, cfg=cfg)
     finally:
         oe.RELU = None
     out.pop("model")
@@ -140,6 +144,10 @@ def _conditioned(damp, elements, dt, masks):
 
 
 def test_c2_f32_step_matches_oracle(oracle_c2, dev):
+    check_f32_step(oracle_c2, dev, "C2")
+
+
+def check_f32_step(oracle, dev, tag):
     """f32 mode, deterministic.  Unconditioned: embeddings within 1e-3 of the
     float64 oracle, loss and the whole gradient vector (relative L2) as accurate
     as PyTorch's fp32 (2x its error, floor 1e-3), BN running statistics, eval
@@ -149,15 +157,15 @@ def test_c2_f32_step_matches_oracle(oracle_c2, dev):
     oracle's error) of the float64 one, relative to its largest entry — no
     outliers; the HIP and float64 ReLU decisions differ only at |x| < 1e-5 max|x|."""
     import engine
-    elements = oracle_c2["elements"]
+    elements, cfg = oracle["elements"], oracle["cfg"]
     old = engine.set_deterministic(True)
     try:
-        m = _mine(dev, torch.float32)
+        m = _mine(dev, torch.float32, cfg=cfg)
         masks = hip_relu_masks(m, elements, dev)
         loss, embs, grads = _step(m, elements, dev)
     finally:
         engine.set_deterministic(old)
-    o64, o32 = oracle_c2["64"], oracle_c2["32"]
+    o64, o32 = oracle["64"], oracle["32"]
     for e, e64 in zip(embs, o64["emb"]):
         assert torch.allclose(e, e64, atol=1e-3, rtol=1e-3), (e - e64).abs().max().item()
     l32_err = abs(o32["loss"] - o64["loss"])
@@ -170,9 +178,9 @@ def test_c2_f32_step_matches_oracle(oracle_c2, dev):
     assert _rel_l2(flat, flat64) < max(1e-3, 2 * _rel_l2(flat32, flat64)), (_rel_l2(flat, flat64),
                                                                             _rel_l2(flat32, flat64))
     # mask-conditioned oracles
-    c64, feed = _conditioned(DAMP, elements, torch.float64, masks)
-    c32, _ = _conditioned(DAMP, elements, torch.float32, masks)
-    print(f"\nC2 f32: ReLU decisions differing from float64: {feed.flips} of {feed.total} "
+    c64, feed = _conditioned(DAMP, elements, torch.float64, masks, cfg)
+    c32, _ = _conditioned(DAMP, elements, torch.float32, masks, cfg)
+    print(f"\n{tag} f32: ReLU decisions differing from float64: {feed.flips} of {feed.total} "
           f"(max |x| there {feed.flip_mag:.2e} of the layer's max |x|)")
     assert feed.flip_mag < 1e-5, feed.flip_mag
     assert feed.flips <= 1e-5 * feed.total, feed.flips
@@ -185,7 +193,7 @@ def test_c2_f32_step_matches_oracle(oracle_c2, dev):
         worst = max(worst, e_mine)
         if e_mine > max(2e-4, 4 * e_ref):
             bad.append((k, e_mine, e_ref))
-    print(f"C2 f32 gradient vs mask-conditioned float64: worst parameter max-error {worst:.2e}")
+    print(f"{tag} f32 gradient vs mask-conditioned float64: worst parameter max-error {worst:.2e}")
     assert not bad, bad
     # BN running statistics after the three train-mode forwards (models.py BN momentum 0.1)
     sd = m.state_dict()
@@ -251,14 +259,18 @@ BF16_EMB_FLOOR, BF16_LOSS_FLOOR, BF16_GRAD_FLOOR = 2e-2, 2e-2, 1e-1
 
 @pytest.mark.parametrize("deterministic", [False, True], ids=["atomic", "det"])
 def test_c2_bf16_step_accuracy(oracle_c2, dev, deterministic):
+    check_bf16_step(oracle_c2, dev, deterministic, "C2")
+
+
+def check_bf16_step(oracle, dev, deterministic, tag):
     import engine
     old = engine.set_deterministic(deterministic)
     try:
-        m = _mine(dev, torch.bfloat16)
-        loss, embs, grads = _step(m, oracle_c2["elements"], dev)
+        m = _mine(dev, torch.bfloat16, cfg=oracle["cfg"])
+        loss, embs, grads = _step(m, oracle["elements"], dev)
     finally:
         engine.set_deterministic(old)
-    o64, oac = oracle_c2["64"], oracle_c2["ac"]
+    o64, oac = oracle["64"], oracle["ac"]
     g64 = o64["grad"]
     flat64 = torch.cat([g.flatten() for g in g64.values()])
 
@@ -269,7 +281,7 @@ def test_c2_bf16_step_accuracy(oracle_c2, dev, deterministic):
         return e, le, _rel_l2(fl, flat64), float(torch.nn.functional.cosine_similarity(fl, flat64, dim=0))
     e_err, l_err, g_err, g_cos = errs(embs, loss, grads)
     a_emb, a_loss, a_grad, a_cos = errs(oac["emb"], oac["loss"], oac["grad"])
-    print(f"\nC2 bf16 ({'det' if deterministic else 'atomic'}) vs float64: emb rel-L2 {e_err:.3e} "
+    print(f"\n{tag} bf16 ({'det' if deterministic else 'atomic'}) vs float64: emb rel-L2 {e_err:.3e} "
           f"(autocast {a_emb:.3e}), loss rel {l_err:.3e} (autocast {a_loss:.3e}), grad rel-L2 {g_err:.3e} "
           f"(autocast {a_grad:.3e}), grad cos {g_cos:.4f} (autocast {a_cos:.4f})")
     assert e_err < max(BF16_EMB_FLOOR, BF16_FACTOR * a_emb), (e_err, a_emb)
