@@ -20,10 +20,15 @@
 //    rewritten two phases after its last read, and one counted s_waitcnt vmcnt
 //    per K-tile (never 0 in the steady state) retires K-tile t+1 one phase
 //    before its first read: up to three K-tiles (96 KB) in flight per CU;
-//  * persistent form (G > 0): a workgroup walks a contiguous range of output
-//    tiles of its XCD (tiles that share an operand panel run at the same time
-//    on one L2), and the stage stream runs across tile boundaries: the next
-//    tile's first three K-tiles load while this tile's epilogue stores drain.
+//  * the loop carries almost no vector work besides the MFMAs (a wave64 VALU
+//    instruction holds the SIMD's issue port for 4 cycles, so every one of
+//    them in the K loop comes out of the MFMA budget; the first version, with
+//    a tap walk and offsets in VGPRs and 46 SGPR-spill reloads per K-tile, ran
+//    at 0.85 PF with no memory traffic at all): the per-row part of each LDS-DMA
+//    address is a VGPR fixed for the tile (for a 3x3 conv: per tap), the K-tile's
+//    part is the instruction's SGPR soffset, the LDS destination an SGPR, and
+//    the loop is unrolled by the four buffers so every LDS offset is an
+//    immediate.
 // The epilogue is pgemm's compile-time-specialised one (pg_epilogue_k), its
 // operands read from global memory (no LDS staging), so every fused form of
 // pgemm_kernel (forward BN statistics per segment, residual / average-unpool,
@@ -42,52 +47,37 @@ constexpr int PP_HALF = 256 * PP_ROWB;  // one operand of one K-tile: 16 KB
 constexpr int PP_BUF = 2 * PP_HALF;     // pixels | weights
 constexpr int PP_NBUF = 4;
 
-__device__ __forceinline__ void pp_barrier(bool skip = false) {
+__device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  if (!skip) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("" ::: "memory");
 }
 
-// retire all but the newest 4 * n LDS-DMA instructions of this wave (n = K-tiles
-// left in flight; a K-tile is 2 pixel + 2 weight instructions per wave)
-__device__ __forceinline__ void pp_wait(int n) {
-  if (n >= 2) vm_wait<8>();
-  else if (n == 1) vm_wait<4>();
-  else vm_wait<0>();
+// LDS-DMA of 16 B per lane to LDS address lds + 16 * lane (lds wave-uniform,
+// in an SGPR) from buffer offset voff (VGPR) + soff (SGPR).  Out-of-range voff
+// (>= the descriptor's size, e.g. 0x80000000) reads zeros.
+__device__ __forceinline__ void pp_glds(__amdgpu_buffer_rsrc_t r, unsigned lds, unsigned voff, unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds), "s"(r), "s"(soff)
+      : "memory");
 }
 
 }  // namespace
 
-#ifndef PP_STAMP
-#define PP_STAMP 0
-#endif
-// PP_STAMP=1: diagnostic build (never the product library) that sums the cycles
-// of each segment of a K-tile per wave (cdna_hip_programming.md §7 stamps) into
-// ts[block][wave][16]; read its shares, not its run time
-#if PP_STAMP
-#define PP_TS(k)                                                                            \
-  do {                                                                                      \
-    __builtin_amdgcn_sched_barrier(0);                                                      \
-    unsigned long long t_;                                                                  \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
-    __builtin_amdgcn_sched_barrier(0);                                                      \
-    tsum[k] += t_ - t_last;                                                                 \
-    t_last = t_;                                                                            \
-  } while (0)
-#else
-#define PP_TS(k) \
-  do {           \
-  } while (0)
-#endif
-
-template <int BK, bool TWO>
-__global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a, int G
-#if PP_STAMP
-                                                      , unsigned long long* ts
-#endif
-) {
+// TAPS: R x S > 1 (3x3 convolutions: the row offsets of a tile change with the
+// tap); otherwise every K-tile of a tile reads the same rows at a growing k.
+template <int BK, bool TWO, bool TAPS>
+__global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   constexpr int NW = PP_NW, BCH = PP_BCH;
   constexpr int WTPX = 64, WTCH = 128, NTP = WTPX / 16, MTC = WTCH / 16;
   constexpr int IPX = 2, ICH = 2;  // DMA instructions per wave per K-tile half
@@ -101,109 +91,81 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a, int G
   const int grp = wid >> 2;
   const int wpx = wid & 3, wch = wid >> 2;
   const int ntc = (a.Cout + BCH - 1) / BCH;
-  const int ntp = (int)((a.M + PP_BPX - 1) / PP_BPX);
-  const int T = ntp * ntc;  // < 2^31 (pp256_launch)
-
-  // ---- the tiles of this workgroup
-  int t_first, t_step, ntl;
-  if (G == 0) {
-    t_first = (int)pg_xcd_remap(blockIdx.x, T);
-    t_step = 0;
-    ntl = 1;
-  } else {  // XCD x = blockIdx % 8 owns tiles [x T / 8, (x + 1) T / 8); its G / 8 workgroups interleave
-    const int x = (int)(blockIdx.x & 7), l = (int)(blockIdx.x >> 3), per = G >> 3;
-    const int lo = (int)((long long)x * T / 8), hi = (int)((long long)(x + 1) * T / 8);
-    t_first = lo + l;
-    t_step = per;
-    ntl = t_first < hi ? (hi - t_first + per - 1) / per : 0;
-  }
-  if (ntl == 0) return;
-  // loop-invariant scalars, copied once: inside the loop an a.field read is a
-  // kernarg load (the asm "memory" clobbers keep it from being hoisted) with an
-  // lgkmcnt wait that also drains the LDS fragment reads
-  const int aC = a.C, aS = a.S;
-  const int nk = (a.K + PP_KS - 1) / PP_KS;
-  const int S = ntl * nk;  // K-tiles of the whole stream
-  const int stepS = (int)a.sW * 2 - aC * 2;         // tap walk: channel chunk wraps, next column tap
-  const int stepR = (int)a.sH * 2 - aS * (int)a.sW * 2;  // column taps wrap, next row tap
-
-  const int HoWo = a.Ho * a.Wo;
-  const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
+  const long long ntp = (a.M + PP_BPX - 1) / PP_BPX;
+  const long long tile = pg_xcd_remap(blockIdx.x, ntp * ntc);  // the N tiles of a pixel panel share an XCD
+  const long long bpx = (tile / ntc) * PP_BPX;
+  const int bch = (int)(tile % ntc) * BCH;
+  const int nk = a.K / PP_KS;  // K % 32 == 0 (pp256_launch)
 
   // ---- loader: this lane fills slot (lane & 3) of row (lane >> 2) of each
   // 16-row DMA instruction with k-chunk csrc = slot ^ ((row >> 2) & 2) (conflict-free
   // for the ds_read_b128 lane groups of MI355X_MICROARCH §LDS)
   const int lrow = lane >> 2, lslot = lane & 3;
   const int csrc = lslot ^ ((lrow >> 2) & 2);
+  const int HoWo = a.Ho * a.Wo;
+  const long long img0 = bpx / HoWo;
+  // the pixel descriptor starts BIAS bytes before the tile's first image, so
+  // the most negative row offset of a padded tap is still >= 0 (the per-row
+  // part is the VGPR offset, which alone decides out-of-range)
+  const int bias = (a.pad * (int)a.sH + a.pad * (int)a.sW) * 2;
+  const __amdgpu_buffer_rsrc_t xr =
+      pg_rsrc(reinterpret_cast<const char*>(a.x) + pg_uniform(img0 * a.sN * 2 - bias),
+              (a.x_elems - img0 * a.sN) * 2 + bias);
+  const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
   int rowoff[IPX];
-  unsigned rmask[IPX];
-  unsigned woff[ICH];
-  __amdgpu_buffer_rsrc_t xr = wr;
-  int l_tile = 0, l_kt = 0;  // position of the next stage to issue
-  // its tap walk (C % 32 == 0: a K-tile never straddles taps): byte offset of the
-  // K-tile in the receptive field, channel offset within the tap, tap index r*S+s
-  int u_off = 0, u_ci = 0, u_s = 0, u_rs = 0, w_off = 0;
-  auto decode = [&](int tile) {
-    const long long bpx = (long long)(tile / ntc) * PP_BPX;
-    const int bch = (tile % ntc) * BCH;
-    const long long img0 = bpx / HoWo;
-    xr = pg_rsrc(reinterpret_cast<const bf16*>(a.x) + pg_uniform(img0 * a.sN), (a.x_elems - img0 * a.sN) * 2);
+  unsigned rmask[IPX], vofs[IPX], woff[ICH];
 #pragma unroll
-    for (int u = 0; u < IPX; ++u) {
-      const int row = (u * NW + wid) * PP_RPI + lrow;
-      const long long gm = bpx + row;
-      const bool valid = gm < a.M;
-      const long long gmc = valid ? gm : bpx;
-      const long long img = gmc / HoWo;
-      const int rem = (int)(gmc - img * HoWo);
-      const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-      const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
-      rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2) + csrc * 16;
-      unsigned msk = 0;
-      for (int r = 0; r < a.R; ++r)
-        for (int s = 0; s < a.S; ++s) {
-          const bool ok = valid && ih0 + r >= 0 && ih0 + r < a.H && iw0 + s >= 0 && iw0 + s < a.W;
-          msk |= (ok ? 1u : 0u) << (r * a.S + s);
-        }
-      rmask[u] = msk;
-    }
+  for (int u = 0; u < IPX; ++u) {
+    const int row = (u * NW + wid) * PP_RPI + lrow;
+    const long long gm = bpx + row;
+    const bool valid = gm < a.M;
+    const long long gmc = valid ? gm : bpx;
+    const long long img = gmc / HoWo;
+    const int rem = (int)(gmc - img * HoWo);
+    const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+    const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
+    rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2) + bias + csrc * 16;
+    unsigned msk = 0;
+    for (int r = 0; r < a.R; ++r)
+      for (int s = 0; s < a.S; ++s) {
+        const bool ok = valid && ih0 + r >= 0 && ih0 + r < a.H && iw0 + s >= 0 && iw0 + s < a.W;
+        msk |= (ok ? 1u : 0u) << (r * a.S + s);
+      }
+    rmask[u] = msk;
+    vofs[u] = (msk & 1u) ? (unsigned)rowoff[u] : PG_OOB;
+  }
 #pragma unroll
-    for (int u = 0; u < ICH; ++u) {
-      const int ch = bch + pg_perm((u * NW + wid) * PP_RPI + lrow);
-      woff[u] = ch < a.Cout ? (unsigned)(ch * a.K * 2 + csrc * 16) : PG_OOB;
+  for (int u = 0; u < ICH; ++u) {
+    const int ch = bch + pg_perm((u * NW + wid) * PP_RPI + lrow);
+    woff[u] = ch < a.Cout ? (unsigned)(ch * a.K * 2 + csrc * 16) : PG_OOB;
+  }
+  // K-tile parts of the addresses (SGPRs): pixel offset within the receptive
+  // field (tap walk for TAPS), weight offset; LDS destination of this wave
+  const int aC = a.C, aS = a.S;
+  const int stepS = (int)a.sW * 2 - aC * 2, stepR = (int)a.sH * 2 - aS * (int)a.sW * 2;
+  unsigned px_soff = 0, w_soff = 0;
+  int u_ci = 0, u_s = 0, u_rs = 0;
+  const unsigned lds0 = (unsigned)(unsigned long long)(pg_lds_t)smem + (unsigned)wid * 1024u;
+  auto issue_px = [&](int slot) {
+#pragma unroll
+    for (int u = 0; u < IPX; ++u) pp_glds(xr, lds0 + slot * PP_BUF + u * NW * 1024, vofs[u], px_soff);
+    px_soff += PP_KS * 2;
+    if constexpr (TAPS) {
+      u_ci += PP_KS;
+      if (u_ci == aC) {  // next tap: its row validity
+        u_ci = 0;
+        px_soff += stepS;
+        ++u_rs;
+        if (++u_s == aS) { u_s = 0; px_soff += stepR; }
+#pragma unroll
+        for (int u = 0; u < IPX; ++u) vofs[u] = ((rmask[u] >> u_rs) & 1u) ? (unsigned)rowoff[u] : PG_OOB;
+      }
     }
   };
-  // pixel half of the next stage (advances the tap walk); decodes a new tile first
-  auto issue_px = [&](int s) {
-    if (l_kt == 0) decode(t_first + l_tile * t_step);
-    char* pxs = smem + (s & 3) * PP_BUF;
-    const int rs = u_rs, toff = u_off;
-    u_off += PP_KS * 2;
-    u_ci += PP_KS;
-    if (u_ci == aC) {
-      u_ci = 0;
-      u_off += stepS;
-      ++u_rs;
-      if (++u_s == aS) { u_s = 0; u_off += stepR; }
-    }
+  auto issue_ch = [&](int slot) {
 #pragma unroll
-    for (int u = 0; u < IPX; ++u) {
-      const bool ok = (rmask[u] >> rs) & 1u;
-      glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + toff) : PG_OOB);
-    }
-  };
-  // weight half of the same stage (K % 32 == 0: no k tail); moves the loader to the next K-tile
-  auto issue_ch = [&](int s) {
-    char* chs = smem + (s & 3) * PP_BUF + PP_HALF;
-#pragma unroll
-    for (int u = 0; u < ICH; ++u)
-      glds16(wr, chs + (u * NW + wid) * 1024, woff[u] != PG_OOB ? woff[u] + w_off : PG_OOB);
-    w_off += PP_ROWB;
-    if (++l_kt == nk) {
-      l_kt = 0;
-      ++l_tile;
-      u_off = 0; u_ci = 0; u_s = 0; u_rs = 0; w_off = 0;
-    }
+    for (int u = 0; u < ICH; ++u) pp_glds(wr, lds0 + slot * PP_BUF + PP_HALF + u * NW * 1024, woff[u], w_soff);
+    w_soff += PP_ROWB;
   };
 
   const bool sums = (BK != 0) || a.stats != nullptr;
@@ -219,44 +181,33 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a, int G
     for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ---- prologue: K-tiles 0..2 in flight, K-tile 0 retired
-  const int npro = S < 3 ? S : 3;
-  for (int s = 0; s < npro; ++s) {
-    issue_px(s);
-    issue_ch(s);
-  }
-  pp_wait(npro - 1);
+  issue_px(0);
+  issue_ch(0);
+  if (nk > 1) { issue_px(1); issue_ch(1); }
+  if (nk > 2) { issue_px(2); issue_ch(2); }
+  if (nk > 2) vm_wait<8>();
+  else if (nk > 1) vm_wait<4>();
+  else vm_wait<0>();
   pp_barrier();
   if (grp == 1) pp_barrier();  // the stagger: group 1 runs one barrier behind
 
   const int fr = lane & 15, fq = lane >> 4;
   const int so = (fq ^ ((fr >> 2) & 2)) << 4;
-  const int brow = (wpx * WTPX + fr) * PP_ROWB + so;            // pixel fragment j: + j * 16 rows
-  const int arow = PP_HALF + (wch * WTCH + fr) * PP_ROWB + so;  // channel fragment i: + i * 16 rows
-  int kt = 0, n = 0;
-  bool after_epi = false;
-  // timing ablations (ARTSBIR_PG_DBG, wrong results): 8 no stage loads in the
-  // loop, 16 no fragment reads, 32 no barriers in the loop
-  const int dbg = a.dbg;
-  uint4 bv[NTP], af[MTC];  // fragments (declared outside the loop: the ablations reuse stale ones)
-#if PP_STAMP
-  unsigned long long tsum[16] = {}, t_last;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_last)::"memory");
-#endif
-  for (int s = 0; s < S; ++s) {
-    const char* buf = smem + (s & 3) * PP_BUF;
-    PP_TS(0);  // loop overhead / previous tail
-    // ---- phase a: pixel fragments + channel fragments 0..3
-    if (s + 3 < S && !(dbg & 8)) issue_px(s + 3);
-    PP_TS(1);  // pixel stage issue
-    if (!(dbg & 16) || s < 2) {
+  const char* bbase = smem + (wpx * WTPX + fr) * PP_ROWB + so;            // pixel fragment j: + j * 16 rows
+  const char* abase = smem + PP_HALF + (wch * WTCH + fr) * PP_ROWB + so;  // channel fragment i: + i * 16 rows
+  uint4 bv[NTP], af[MTC];
+  // one K-tile in buffer SL (compile-time: every LDS offset an immediate)
+  auto ktile = [&](int s, auto slc) {
+    constexpr int SL = decltype(slc)::value;
+    const char* bb = bbase + SL * PP_BUF;
+    const char* ab = abase + SL * PP_BUF;
+    // ---- phase a: pixel fragments + channel fragments 0..3; pixel half of K-tile s+3
+    if (s + 3 < nk) issue_px((SL + 3) & 3);
 #pragma unroll
-      for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(buf + brow + j * 16 * PP_ROWB);
+    for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(bb + j * 16 * PP_ROWB);
 #pragma unroll
-      for (int i = 0; i < MTC / 2; ++i) af[i] = *reinterpret_cast<const uint4*>(buf + arow + i * 16 * PP_ROWB);
-    }
-    PP_TS(2);  // fragment reads a (issue + latency in this build)
-    pp_barrier(dbg & 32);
-    PP_TS(3);  // barrier 1
+    for (int i = 0; i < MTC / 2; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
+    pp_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     PG_PRIO_ON();
@@ -267,26 +218,19 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a, int G
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
                                                             *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j], 0, 0, 0);
     PG_PRIO_OFF();
-    PP_TS(4);  // MFMA issue a
-    pp_barrier(dbg & 32);
-    PP_TS(5);  // barrier 2
-    // ---- phase b: channel fragments 4..7; K-tile s+1 retired for the next phase a
-    if (s + 3 < S && !(dbg & 8)) issue_ch(s + 3);
-    PP_TS(6);  // weight stage issue
-    if (s + 1 < S) {
-      int left = (s + 3 < S ? s + 3 : S - 1) - (s + 1);
-      if (after_epi && left > 1) left = 1;  // the epilogue's stores sit between the stages: retire them too
-      pp_wait(left);
+    pp_barrier();
+    // ---- phase b: channel fragments 4..7; weight half of K-tile s+3; K-tile s+1 retired
+    if (s + 3 < nk) {
+      issue_ch((SL + 3) & 3);
+      vm_wait<8>();
+    } else if (s + 2 < nk) {
+      vm_wait<4>();
+    } else if (s + 1 < nk) {
+      vm_wait<0>();
     }
-    after_epi = false;
-    PP_TS(7);  // vmcnt wait for K-tile s+1
-    if (!(dbg & 16) || s < 2) {
 #pragma unroll
-      for (int i = MTC / 2; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(buf + arow + i * 16 * PP_ROWB);
-    }
-    PP_TS(8);  // fragment reads b
-    pp_barrier(dbg & 32);
-    PP_TS(9);  // barrier 3
+    for (int i = MTC / 2; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
+    pp_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     PG_PRIO_ON();
@@ -297,52 +241,31 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a, int G
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&af[i]),
                                                             *reinterpret_cast<const bf16x8*>(&bv[j]), acc[i][j], 0, 0, 0);
     PG_PRIO_OFF();
-    PP_TS(10);  // MFMA issue b
-    if (!(s == S - 1 && grp == 1)) pp_barrier(dbg & 32);  // group 1 drops its last one: equal barrier counts
-    PP_TS(11);  // barrier 4
-    if (++kt == nk) {
-      kt = 0;
-      const int tile = t_first + n * t_step;
-      const long long bpx = (long long)(tile / ntc) * PP_BPX;
-      const int bch = (tile % ntc) * BCH;
-      const long long seg0 = a.seg_m > 0 ? bpx / a.seg_m : 0;
-      EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
-      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 2, true>(a, acc, bpx, bch, wpx, wch,
-                                                                                            fr, fq, red, sgg);
-      if (sums) stats_flush<BCH>(red, red_cnt, (n + 1) * NW - 1, a, bch, (int)(blockIdx.x % ARTSBIR_NSLOT), lane, bpx,
-                                 PP_BPX);
-      ++n;
-      // the compiler's own count of the epilogue's global loads: tell it they are
-      // retired (vmcnt 0, the other counters at their maximum), or its waitcnt pass
-      // carries them round the loop and drains vmcnt(0) before every K-tile's
-      // first fragment read, i.e. the whole LDS-DMA pipeline
-      __builtin_amdgcn_s_waitcnt(0x0f70);
-#pragma unroll
-      for (int i = 0; i < MTC; ++i)
-#pragma unroll
-        for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      after_epi = true;
-      PP_TS(12);  // epilogue
-    }
+    if (!(s == nk - 1 && grp == 1)) pp_barrier();  // group 1 drops its last one: equal barrier counts
+  };
+  for (int s = 0; s < nk; s += 4) {
+    ktile(s, std::integral_constant<int, 0>{});
+    if (s + 1 < nk) ktile(s + 1, std::integral_constant<int, 1>{});
+    if (s + 2 < nk) ktile(s + 2, std::integral_constant<int, 2>{});
+    if (s + 3 < nk) ktile(s + 3, std::integral_constant<int, 3>{});
   }
-#if PP_STAMP
-  if (lane == 0) {
-    unsigned long long* o = ts + ((long long)blockIdx.x * NW + wid) * 16;
-    for (int k = 0; k < 13; ++k) o[k] = tsum[k];
-    o[13] = S;
-  }
-#endif
+
+  const long long seg0 = a.seg_m > 0 ? bpx / a.seg_m : 0;
+  EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
+  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 2, true>(a, acc, bpx, bch, wpx, wch, fr,
+                                                                                        fq, red, sgg);
+  if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, (int)(blockIdx.x % ARTSBIR_NSLOT), lane, bpx, PP_BPX);
 }
 
-// Candidate 22 (one tile per workgroup) / 23 (persistent, 256 workgroups):
-// C % 32 == 0 (uniform taps), every epilogue of pgemm_launch_cfg except the
-// LDS-staged BN-backward forms.
+// Candidate 22: C % 32 == 0 (uniform taps), every epilogue of pgemm_launch_cfg
+// except the LDS-staged BN-backward forms.
 bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st) {
+  if (persistent) return false;  // candidate 23 (persistent form) retired: no gain over one tile per workgroup
   if (a.C % 32 != 0 || a.Cout % 32 != 0 || a.M <= 0) return false;
   if (a.R * a.S > 32 || a.K != a.R * a.S * a.C) return false;
   if ((long long)a.Cout * a.K * 2 > 0x7fffffffLL) return false;
   const long long HoWo = (long long)a.Ho * a.Wo;
-  if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 > 0x7fffffffLL) return false;
+  if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 + 2LL * (a.pad * a.sH + a.pad * a.sW) > 0x7fffffffLL) return false;
   if (a.M > (1LL << 40)) return false;
   if (a.seg_m > 0 && (a.seg_m % 64 != 0 || a.seg_m < 256 || a.M % a.seg_m != 0)) return false;
   const bool act = a.bias != nullptr || a.relu != 0;
@@ -352,36 +275,22 @@ bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st) {
   if ((a.bnb == 2 || a.bnb == 3) && !a.res_mode) return false;
   if (a.res_mode == 3 && (a.bnb || a.R * a.S != 1)) return false;
   const long long T = ((a.M + PP_BPX - 1) / PP_BPX) * ((a.Cout + PP_BCH - 1) / PP_BCH);
-  if (T > 0x3fffffffLL) return false;
-  int G = 0;
-  unsigned grid = (unsigned)T;
-  if (persistent) {
-    // ARTSBIR_PP_GRID (tests): a smaller persistent grid (multiple of 8), so that
-    // small shapes also walk several tiles per workgroup
-    const char* eg = getenv("ARTSBIR_PP_GRID");
-    G = eg ? atoi(eg) : 256;
-    if (G < 8 || G % 8 || G > 4096) return false;
-    if (!eg && T < 2LL * G) return false;  // fewer than two tiles per workgroup: the one-tile form
-    grid = (unsigned)G;
-  }
-  const dim3 g(grid), b(512);
-#if PP_STAMP
-  unsigned long long* ts = reinterpret_cast<unsigned long long*>(strtoull(getenv("ARTSBIR_PP_TS"), nullptr, 0));
-  if (!a.bnb) hipLaunchKernelGGL((pp256_kernel<0, false>), g, b, 0, st, a, G, ts);
-  set_last_kernel(persistent ? "pp256_kernel<persistent,stamp>" : "pp256_kernel<stamp>");
+  if (T > 0x7fffffffLL) return false;
+  const dim3 g((unsigned)T), b(512);
+#define PP_GO(BKV, TWOV)                                                              \
+  do {                                                                                \
+    if (a.R * a.S > 1) hipLaunchKernelGGL((pp256_kernel<BKV, TWOV, true>), g, b, 0, st, a); \
+    else hipLaunchKernelGGL((pp256_kernel<BKV, TWOV, false>), g, b, 0, st, a);       \
+  } while (0)
+  if (a.bnb == 1) PP_GO(1, false);
+  else if (a.bnb == 2 && a.bnb_nt == 2) PP_GO(2, true);
+  else if (a.bnb == 2) PP_GO(2, false);
+  else if (a.bnb == 3 && a.bnb_nt == 2) PP_GO(3, true);
+  else if (a.bnb == 3) PP_GO(3, false);
+  else PP_GO(0, false);
+#undef PP_GO
+  set_last_kernel(a.bnb ? "pp256_kernel<bnb>" : "pp256_kernel");
   return true;
-#else
-  if (a.bnb == 1) hipLaunchKernelGGL((pp256_kernel<1, false>), g, b, 0, st, a, G);
-  else if (a.bnb == 2 && a.bnb_nt == 2) hipLaunchKernelGGL((pp256_kernel<2, true>), g, b, 0, st, a, G);
-  else if (a.bnb == 2) hipLaunchKernelGGL((pp256_kernel<2, false>), g, b, 0, st, a, G);
-  else if (a.bnb == 3 && a.bnb_nt == 2) hipLaunchKernelGGL((pp256_kernel<3, true>), g, b, 0, st, a, G);
-  else if (a.bnb == 3) hipLaunchKernelGGL((pp256_kernel<3, false>), g, b, 0, st, a, G);
-  else hipLaunchKernelGGL((pp256_kernel<0, false>), g, b, 0, st, a, G);
-  static const char* names[2][2] = {{"pp256_kernel", "pp256_kernel<bnb>"},
-                                    {"pp256_kernel<persistent>", "pp256_kernel<bnb,persistent>"}};
-  set_last_kernel(names[persistent ? 1 : 0][a.bnb ? 1 : 0]);
-  return true;
-#endif
 }
 
 }  // namespace artsbir
