@@ -775,7 +775,6 @@ static int run_old(const ConvArgs& a, hipStream_t st) {
 
 static bool run_candidate(int c, const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   if (c == -2) return a.res_mode != 3 && run_old<bf16>(a, st) == 0;
-  if (c == -3) return blt_gemm_nt(p, st);
   return pgemm_launch_cfg(p, c, st);
 }
 
@@ -807,7 +806,7 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   // caller's overlapped weight gradients) would otherwise share the chip with
   // some trials and not others and make the choice noisy
   (void)hipDeviceSynchronize();
-  static const int cands[] = {-2, -3, 0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 18, 19, 20, 21};
+  static const int cands[] = {-2, 0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 18, 19, 20, 21, 22};
   int best = -2;
   float best_ms = 1e30f;
   for (int c : cands) {
@@ -888,7 +887,6 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
         g_conv_choice[key] = choice;
       }
     }
-    if (choice == -3 && blt_gemm_nt(p, st)) return 0;
     if ((choice != -2 && pgemm_launch_cfg(p, choice, st)) || (bd && force_bnb && pgemm_launch_cfg(p, 0, st))) {
       ARTSBIR_CHECK_LAUNCH("pgemm");
       return 0;
@@ -1158,8 +1156,6 @@ static void launch_wgrad_old(WgradArgs& a, hipStream_t st);
 // candidate -1: register-staged wgrad_kernel; c >= 0: pipelined config c
 static bool run_wg_candidate(int c, WgradArgs& a, hipStream_t st) {
   if (c >= 0) return pwgrad_launch(to_pw(a), c, st);
-  if (c == -3)  // hipBLASLt, dense 1x1 weight gradients only
-    return a.dense && blt_wgrad_tn(a.dy, a.ldd, a.x, a.ldx, a.Cout, a.K, a.M, a.dw, st);
   launch_wgrad_old<bf16>(a, st);
   return true;
 }
@@ -1185,8 +1181,7 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   // weight gradients share the chip with the data-gradient stream, which the
   // standalone timing here cannot see)
   static const int minlevel = getenv("ARTSBIR_WGRAD_MINLEVEL") ? atoi(getenv("ARTSBIR_WGRAD_MINLEVEL")) : 0;
-  for (int c = -3; c < pwgrad_num_cfgs(); ++c) {
-    if (c == -2) continue;
+  for (int c = -1; c < pwgrad_num_cfgs(); ++c) {
     if (c >= 0 && pwgrad_level(c) >= 0 && pwgrad_level(c) < minlevel) continue;
     if (!run_wg_candidate(c, at, st)) continue;
     float ms = 1e30f;
@@ -1231,7 +1226,6 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
       ARTSBIR_CHECK_LAUNCH("pwgrad");
       return 0;
     }
-    if (choice == -3 && a.dense && blt_wgrad_tn(a.dy, a.ldd, a.x, a.ldx, a.Cout, a.K, a.M, a.dw, st)) return 0;
   }
   launch_wgrad_old<T>(a, st);
   ARTSBIR_CHECK_LAUNCH("wgrad");
@@ -1312,12 +1306,14 @@ extern "C" int artsbir_tune_load(const char* path) {
       if (fscanf(f, "%lld %d %d %d %d %d %d %d %d %d %d %d %d %d %d %d", &k.M, &k.H, &k.W, &k.C, &k.Cout, &k.R, &k.S,
                  &k.stride, &k.pad, &k.Ho, &k.Wo, &k.res_mode, &k.stats, &k.nseg, &k.bnb, &choice) != 16)
         break;
+      if (choice < -2 || choice == 23) continue;  // retired candidates (hipBLASLt -3, persistent pp256): re-tune
       g_conv_choice[k] = choice;
     } else if (tag[0] == 'w') {
       WgKey k;
       if (fscanf(f, "%lld %d %d %d %d %d %d %d %d %d %d %lld %lld %d", &k.M, &k.H, &k.W, &k.C, &k.Cout, &k.R, &k.S,
                  &k.stride, &k.pad, &k.dense, &k.K, &k.ldd, &k.ldx, &choice) != 14)
         break;
+      if (choice < -1) continue;  // the retired hipBLASLt candidate: re-tune
       g_wg_choice[k] = choice;
     } else {
       break;

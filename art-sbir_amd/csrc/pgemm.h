@@ -75,11 +75,5 @@ bool pgemm_launch_cfg(const PgArgs& a, int cfg, hipStream_t st);
 bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st);
 // Heuristic candidate for a shape (-1: unsupported).
 int pgemm_default_cfg(const PgArgs& a);
-// candidate -3 (blaslt.cpp): a plain dense bf16 NT GEMM (H = W = R = S = 1, no
-// fused epilogue) through hipBLASLt; false, launching nothing, otherwise
-bool blt_gemm_nt(const PgArgs& a, hipStream_t st);
-// dW (f32 [Cout][K]) += dY^T X for a dense 1x1 weight gradient through hipBLASLt
-bool blt_wgrad_tn(const void* dy, long long ldd, const void* x, long long ldx, int Cout, int K, long long M, float* dw,
-                  hipStream_t st);
 
 }  // namespace artsbir

@@ -43,10 +43,11 @@ def init_distributed() -> None:
         return
     backend = os.environ.get("ARTSBIR_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = local % torch.cuda.device_count() if torch.cuda.is_available() else 0  # one index for both uses
     if torch.cuda.is_available():
-        torch.cuda.set_device(local % torch.cuda.device_count())
+        torch.cuda.set_device(gpu)
     if backend == "nccl":
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
     else:
         dist.init_process_group(backend)
 

@@ -304,8 +304,8 @@ def run_inference(model, dataset, folder_name: str = None, loss_type='euclidean'
     start_time = timer()
     with_classification = 'with_classification' in type(model).__name__
     import ddp
-    if ddp.is_distributed() and not folder_name:
-        return run_inference_sharded(model, dataset, loss_type, start_time)
+    if ddp.is_distributed():
+        return run_inference_sharded(model, dataset, loss_type, start_time, folder_name=folder_name)
     if folder_name:
         image_paths, image_features = utils.load_image_features(folder_name)
         inference_dataset = data_preparation.InferenceDataset(image_paths, getattr(model, "transform", None))
@@ -324,10 +324,14 @@ def run_inference(model, dataset, folder_name: str = None, loss_type='euclidean'
     return {'image_features': feature_folder, 'drawing_stats': inference_dict, 'sketch_stats': inference_dict2}
 
 
-def run_inference_sharded(model, dataset, loss_type='euclidean', start_time=None, **search) -> Dict:
+def run_inference_sharded(model, dataset, loss_type='euclidean', start_time=None, folder_name: str = None,
+                          **search) -> Dict:
     """run_inference with one process per GPU: sharded gallery embedding and
     shard-parallel retrieval; every rank returns the same dictionary, rank 0
-    wrote the feature file (its path is broadcast)."""
+    wrote the feature file (its path is broadcast).  With a feature folder
+    (--feature_folder) every rank reads the file and keeps only its contiguous
+    row shard, so the retrieval stays sharded instead of every rank scanning
+    the whole gallery."""
     import torch.distributed as dist
     import ddp
     start_time = timer() if start_time is None else start_time
@@ -335,11 +339,21 @@ def run_inference_sharded(model, dataset, loss_type='euclidean', start_time=None
     # every rank embeds its shard with the same eval model: rank 0's BatchNorm
     # running statistics (each rank's own came from its own minibatches)
     ddp.broadcast_buffers(model)
-    inference_dataset, shard, g_base, feature_path = compute_image_features_sharded(model, dataset,
-                                                                                    with_classification)
-    box = [str(feature_path) if feature_path is not None else None]
-    dist.broadcast_object_list(box, src=0)
-    feature_folder = box[0]
+    if folder_name:
+        image_paths, image_features = utils.load_image_features(folder_name)
+        inference_dataset = data_preparation.InferenceDataset(image_paths, getattr(model, "transform", None))
+        b = shard_bounds(len(inference_dataset), dist.get_world_size())
+        r = dist.get_rank()
+        shard = torch.as_tensor(image_features)[b[r]:b[r + 1]].to(device)
+        g_base = b[r]
+        feature_folder = folder_name
+        print("Image features loaded from file")
+    else:
+        inference_dataset, shard, g_base, feature_path = compute_image_features_sharded(model, dataset,
+                                                                                        with_classification)
+        box = [str(feature_path) if feature_path is not None else None]
+        dist.broadcast_object_list(box, src=0)
+        feature_folder = box[0]
     first = process_inference_sharded(model, dataset, inference_dataset, _Sketches(dataset), shard, g_base,
                                       start_time, with_classification, loss_type, **search)
     if not _needs_second_pass(dataset):
