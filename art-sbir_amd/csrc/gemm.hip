@@ -1155,6 +1155,7 @@ static void launch_wgrad_old(WgradArgs& a, hipStream_t st);
 
 // candidate -1: register-staged wgrad_kernel; c >= 0: pipelined config c
 static bool run_wg_candidate(int c, WgradArgs& a, hipStream_t st) {
+  if (c >= 100) return pw256_launch(to_pw(a), c - 100, st);
   if (c >= 0) return pwgrad_launch(to_pw(a), c, st);
   launch_wgrad_old<bf16>(a, st);
   return true;
@@ -1181,7 +1182,8 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   // weight gradients share the chip with the data-gradient stream, which the
   // standalone timing here cannot see)
   static const int minlevel = getenv("ARTSBIR_WGRAD_MINLEVEL") ? atoi(getenv("ARTSBIR_WGRAD_MINLEVEL")) : 0;
-  for (int c = -1; c < pwgrad_num_cfgs(); ++c) {
+  for (int ci = -1; ci < pwgrad_num_cfgs() + 3; ++ci) {
+    const int c = ci < pwgrad_num_cfgs() ? ci : 100 + ci - pwgrad_num_cfgs();  // then pw256 at 3 split levels
     if (c >= 0 && pwgrad_level(c) >= 0 && pwgrad_level(c) < minlevel) continue;
     if (!run_wg_candidate(c, at, st)) continue;
     float ms = 1e30f;
@@ -1222,7 +1224,11 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
         g_wg_choice[key] = choice;
       }
     }
-    if (choice >= 0 && pwgrad_launch(to_pw(a), choice, st)) {
+    if (choice >= 100 && pw256_launch(to_pw(a), choice - 100, st)) {
+      ARTSBIR_CHECK_LAUNCH("pw256");
+      return 0;
+    }
+    if (choice >= 0 && choice < 100 && pwgrad_launch(to_pw(a), choice, st)) {
       ARTSBIR_CHECK_LAUNCH("pwgrad");
       return 0;
     }

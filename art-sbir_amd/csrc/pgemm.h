@@ -62,6 +62,9 @@ struct PwArgs {
 // candidate c (0 .. pwgrad_num_cfgs()-1) of the pipelined wgrad kernel;
 // false, launching nothing, if it does not apply to the shape
 bool pwgrad_launch(PwArgs a, int c, hipStream_t st);
+// wgrad candidates 100 + level (pw256.hip): the ping-pong 256 x 256 weight-gradient
+// tile, m-split over 256 << level workgroups; false outside its range
+bool pw256_launch(PwArgs a, int level, hipStream_t st);
 int pwgrad_num_cfgs();
 int pwgrad_level(int c);
 

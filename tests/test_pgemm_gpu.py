@@ -285,3 +285,68 @@ def test_gemm_nt_pp256_candidate(M, N, K, lda, ldc, with_bias, dev, cfg_env):
     out = c.float().cpu()
     assert torch.allclose(out[:, :N], ref, atol=3e-2, rtol=1e-2), (out[:, :N] - ref).abs().max()
     assert torch.all(out[:, N:] == 7.0)  # the row padding beyond N is untouched
+
+
+PW256_CASES = [
+    # N, H, W, C, Cout, R, S, stride, pad
+    (2, 14, 14, 128, 256, 3, 3, 1, 1),   # 3x3, a 256-k tile spans two taps
+    (16, 28, 28, 128, 256, 3, 3, 1, 1),  # many m-splits
+    (2, 7, 7, 512, 512, 3, 3, 1, 1),     # 7x7 images (49 pixels): a K-tile of 32 rows crosses images
+    (3, 10, 9, 256, 512, 1, 1, 1, 0),    # dense 1x1
+    (3, 12, 12, 512, 256, 1, 1, 2, 0),   # strided 1x1 (implicit im2col)
+    (2, 9, 11, 64, 200, 3, 3, 1, 1),     # Cout and K tails (200 co, 576 k)
+]
+
+
+@pytest.mark.parametrize("cfg", ["100", "101", "102"])
+@pytest.mark.parametrize("case", PW256_CASES)
+def test_wgrad_pw256(case, cfg, dev):
+    """wgrad candidates 100-102 (pw256.hip, the ping-pong 256x256 weight-gradient
+    tile at three m-split levels): dW accumulated onto an existing gradient vs
+    torch fp32 autograd on the same bf16 operands"""
+    os.environ["ARTSBIR_WGRAD_CFG"] = cfg
+    try:
+        N, H, W, C, Co, R, S, st, pd = case
+        g = torch.Generator().manual_seed(21)
+        x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+        w = torch.randn(Co, C, R, S, generator=g)
+        Ho = (H + 2 * pd - R) // st + 1
+        Wo = (W + 2 * pd - S) // st + 1
+        dy = torch.randn(N, Co, Ho, Wo, generator=g).bfloat16().float()
+        wr = w.clone().requires_grad_(True)
+        F.conv2d(x, wr, stride=st, padding=pd).backward(dy)
+        init = torch.randn(Co, R, S, C, generator=g)
+        ref = init + wr.grad.permute(0, 2, 3, 1)
+        dw = init.clone().to(dev)
+        d = _hip.conv_desc(torch.bfloat16, N, H, W, C, Co, R, S, st, pd)
+        dyd, xd = _nhwc(dy).to(dev, torch.bfloat16), _nhwc(x).to(dev, torch.bfloat16)
+        _hip.call("artsbir_conv2d_wgrad", d, dyd.data_ptr(), xd.data_ptr(), None, None, 0, dw.data_ptr(),
+                  _hip.stream())
+        torch.cuda.synchronize()
+        assert _hip.lib().artsbir_last_kernel().decode().startswith("pw256_kernel")
+        assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
+    finally:
+        os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+
+
+@pytest.mark.parametrize("cfg", ["100", "102"])
+@pytest.mark.parametrize("M,N,K,ldd,ldx", [(3000, 512, 2048, 512, 2048), (5001, 768, 2304, 776, 2304),
+                                           (40000, 256, 768, 256, 800)])
+def test_gemm_tn_pw256(M, N, K, ldd, ldx, cfg, dev):
+    """artsbir_gemm_tn (the dense weight gradients of the attention pool and the
+    ViT projections) on pw256, strided rows, vs torch fp32"""
+    os.environ["ARTSBIR_WGRAD_CFG"] = cfg
+    try:
+        g = torch.Generator().manual_seed(22)
+        dy = torch.randn(M, ldd, generator=g).bfloat16().float()
+        x = torch.randn(M, ldx, generator=g).bfloat16().float()
+        ref = dy[:, :N].t() @ x[:, :K]
+        dw = torch.zeros(N, K, device=dev)
+        dyd, xd = dy.to(dev, torch.bfloat16), x.to(dev, torch.bfloat16)
+        _hip.call("artsbir_gemm_tn", _hip.DT_BF16, M, N, K, dyd.data_ptr(), ldd, xd.data_ptr(), ldx, dw.data_ptr(),
+                  _hip.stream())
+        torch.cuda.synchronize()
+        assert _hip.lib().artsbir_last_kernel().decode() == "pw256_kernel<dense>"
+        assert torch.allclose(dw.cpu(), ref, atol=5e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
+    finally:
+        os.environ.pop("ARTSBIR_WGRAD_CFG", None)
