@@ -218,7 +218,7 @@ class HipError(RuntimeError):
 
 # Optional live per-launch timing (bench.py): when PROFILE is a list, every call
 # that declares its algorithmic work is bracketed by two timing events on the
-# current stream and (kernel, flops, bytes, start, end, tag) is appended.
+# current stream and (kernel, flops, bytes, start, end, tag, stream) is appended.
 PROFILE = None
 
 
@@ -234,7 +234,7 @@ def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes
         e1.record()
         if kernel == "auto":  # the variant the library chose for this call
             kernel = lib().artsbir_last_kernel().decode()
-        prof.append((kernel, flops, nbytes, e0, e1, tag))
+        prof.append((kernel, flops, nbytes, e0, e1, tag, torch.cuda.current_stream().cuda_stream))
     else:
         rc = getattr(lib(), name)(*args)
     if rc != 0:

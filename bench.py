@@ -121,6 +121,20 @@ def roofline(prof, peak_of, traffic_file=None):
         a[2] += 1
         a[3] += nb
         a[4] += max(nb / (HBM_PEAK_GBS * 1e9), fl / (peak_of(kname) * 1e12))
+    # per family (by the launch's tag) and per stream: kernel time per step would
+    # otherwise hinge on which tile variant of a family happens to be the largest
+    fam, streams = {}, {}
+    for kname, fl, nb, e0, e1, *rest in prof:
+        tag = rest[0] if rest else None
+        f = launch_family(kname, tag)
+        ms = e0.elapsed_time(e1)
+        v = fam.setdefault(f, [0.0, 0, 0.0, 0.0])
+        v[0] += ms
+        v[1] += 1
+        v[2] += fl
+        v[3] += nb
+        if len(rest) > 1:
+            streams[rest[1]] = streams.get(rest[1], 0.0) + ms
     dom = max(agg, key=lambda k: agg[k][1])
     fl, secs, cnt, nb, rt = agg[dom]
     peak_fl = peak_of(dom)
@@ -146,8 +160,34 @@ def roofline(prof, peak_of, traffic_file=None):
                                     "tflops": round(v[0] / v[1] / 1e12, 1),
                                     "gbs": round(v[3] / v[1] / 1e9, 1), "share_s": round(v[1], 4),
                                     "roof_frac": round(v[4] / v[1], 4)}
-                                for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])}})
+                                for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])},
+                 # kernel ms summed over the profiled launches (divide by the steps for ms/step)
+                 "families": {f: {"kernel_ms": round(v[0], 3), "launches": v[1],
+                                  "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 1) if v[0] else None,
+                                  "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1) if v[0] else None}
+                              for f, v in sorted(fam.items(), key=lambda kv: -kv[1][0])},
+                 "streams_kernel_ms": {("main" if i == 0 else f"side{i}"): round(ms, 3) for i, (sid, ms) in
+                                       enumerate(sorted(streams.items(), key=lambda kv: -kv[1]))}})
     return roof
+
+
+def launch_family(kernel, tag):
+    """the step's kernel families: forward convolutions / GEMMs, fused BN-backward
+    data gradients, plain data gradients, weight gradients (the overlapped side
+    stream), the elementwise BatchNorm / ReLU / pool passes, everything else"""
+    t = (tag or "").split(" ")[0]
+    if t.startswith("dgrad+bn"):
+        return "bn_backward_dgrad"
+    if t == "dgrad":
+        return "dgrad"
+    if t in ("wgrad", "gemm_tn"):
+        return "weight_gradient"
+    if t in ("fwd", "fwd_act", "gemm_nt"):
+        return "forward_gemm"
+    if t.startswith(("act_pool", "block_out", "bn_")):
+        return "elementwise_bn"
+    return "other"
+
 
 
 def preprocess_leg(dev, rank, world, n_triplets=384, reps=5):

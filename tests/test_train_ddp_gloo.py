@@ -160,3 +160,55 @@ def test_sharded_inference_uses_rank0_bn_statistics(tmp_path):
     for rank, ok, rm in res:
         assert ok, rank
         assert rm == 0.0  # rank 1's running statistics were replaced by rank 0's
+
+
+def _ff_entry(rank, port, tmp, q):
+    """--feature_folder under two ranks: each rank reads the file, keeps its own
+    row shard and the retrieval stays sharded (before, every rank ran the whole
+    unsharded retrieval); results equal the run that wrote the features"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(WORLD), RANK=str(rank),
+                      LOCAL_RANK=str(rank), ARTSBIR_DIST_BACKEND="gloo")
+    os.chdir(tmp)
+    _patch_cpu(16)
+    import knn
+    import train
+    seen = []
+    inner = knn.knn_sharded
+
+    def spy(queries, shard, g_base, *a, **k):
+        seen.append((int(shard.shape[0]), int(g_base)))
+        return inner(queries, shard, g_base, *a, **k)
+    knn.knn_sharded = spy
+    try:
+        args = ["--resolution", "16", "--output_dim", "8", "-b", "4", "--synthetic_n", "60", "-e", "1"]
+        # both runs untrained (the seeded stand-in), so the queries are embedded by the same model
+        _, inf = train.main(args + ["--inference", "--no_training", "--no_save"])
+        folder = inf["image_features"]
+        n_first = len(seen)
+        _, inf2 = train.main(args + ["--inference", "--no_training", "--feature_folder", folder, "--no_save"])
+        q.put((rank, json.dumps(_strip(inf), sort_keys=True), json.dumps(_strip(inf2), sort_keys=True),
+               seen[n_first:]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_feature_folder_inference_stays_sharded(tmp_path):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ff_entry, args=(r, port, str(tmp_path), q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert [p.exitcode for p in procs] == [0, 0]
+    res = sorted(q.get(timeout=5) for _ in range(WORLD))
+    (_, a0, b0, s0), (_, a1, b1, s1) = res
+    assert b0 == b1  # same statistics on both ranks
+    d_a, d_b = json.loads(a0), json.loads(b0)
+    d_a.pop("image_features"), d_b.pop("image_features")
+    assert d_a == d_b  # the file's features give the statistics the embedding run gave
+    # each rank searched only its own contiguous shard of the gallery
+    assert len(s0) == len(s1) == 1
+    (n0, base0), (n1, base1) = s0[0], s1[0]
+    assert base0 == 0 and base1 == n0 and n0 > 0 and n1 > 0
