@@ -68,7 +68,7 @@ def main():
     el = (time.perf_counter() - t0) / args.steps
     _hip.PROFILE = None
     agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
-    for kname, fl, nb, e0, e1, tag in prof:
+    for kname, fl, nb, e0, e1, tag, *_ in prof:
         a = agg[(kname, tag)]
         a[0] += 1
         a[1] += e0.elapsed_time(e1) / 1e3

@@ -15,6 +15,7 @@ import _hip  # noqa: E402
 CONV = [  # N, H, W, C, Cout, R (stride 1, pad R//2): C2's 3x3 convs and big 1x1 at 1152 images
     (1152, 56, 56, 64, 64, 3), (1152, 28, 28, 128, 128, 3), (1152, 14, 14, 256, 256, 3), (1152, 7, 7, 512, 512, 3),
     (1152, 56, 56, 128, 128, 3), (1152, 28, 28, 256, 256, 3), (1152, 14, 14, 1024, 256, 1), (1152, 56, 56, 64, 256, 1),
+    (1152, 56, 56, 256, 64, 1), (1152, 56, 56, 256, 128, 1), (1152, 28, 28, 512, 128, 1), (1152, 28, 28, 128, 512, 1),
 ]
 TN = [(302592, 768, 2304), (302592, 768, 768), (302592, 3072, 768), (302592, 768, 3072), (57600, 4096, 2048)]
 
