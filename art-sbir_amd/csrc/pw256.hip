@@ -279,7 +279,10 @@ __global__ void __launch_bounds__(512, 1) pw256_kernel(PwArgs a, int ntiles) {
 // the kernel's range
 bool pw256_launch(PwArgs a, int level, hipStream_t st) {
   if (level < 0 || level > 2) return false;
-  if (a.Cout < 192 || a.K < 192 || a.Cout % 8 || a.K % 8 || a.M <= 0) return false;
+  // small Cout or K leave most of the 256 x 256 tile idle; the tuner still
+  // takes it where the weight gradient is bound by its HBM reads (1x1 convs of
+  // 64-channel layers), not by the MFMAs
+  if (a.Cout < 64 || a.K < 64 || a.Cout % 8 || a.K % 8 || a.M <= 0) return false;
   if (a.ldd % 8 || (a.dense && a.ldx % 8)) return false;
   if (!a.dense && (a.C % 8 || a.R * a.S > 32 || (long long)a.Ho * a.Wo < PW_KS)) return false;
   const int ntiles = ((a.Cout + PW_BT - 1) / PW_BT) * ((a.K + PW_BT - 1) / PW_BT);

@@ -802,8 +802,10 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
         }
       }
     }
-    if (a.kb && (t & (KB_SYNC - 1)) == KB_SYNC - 1 && t + 1 < ntiles) {
-      // every KB_SYNC tiles, the query's bound shared by every chunk (one
+    if (a.kb && (((t & (KB_SYNC - 1)) == KB_SYNC - 1) || t + 1 == ntiles)) {
+      // every KB_SYNC tiles and once more at the chunk's end (a chunk of at most
+      // KB_SYNC tiles, and the ragged last one, still publish what they found),
+      // the query's bound shared by every chunk (one
       // returning atomicMin per row): publish this chunk's kq-th smallest so far
       // and take the best any chunk has published.  The pipeline drains here
       // once (the atomic's value is used at once), instead of at every list

@@ -234,9 +234,10 @@ class Engine:
         ONE batched launch (artsbir_pack_weights) instead of ~120 small ones."""
         key = self._params_key()
         if self._packed_key != key:
-            plan_key = (self.dtype, tuple((p.data_ptr(), tuple(p.shape)) for p in self.model.parameters()))
+            plan_key = (self.dtype, self.dt,
+                        tuple((p.data_ptr(), tuple(p.shape), p.dtype) for p in self.model.parameters()))
             plan = getattr(self, "_plan", None)
-            if plan is not None and plan[0] == plan_key:
+            if plan is not None and plan[0] == plan_key and plan[4] == self._packed_ranges():
                 call("artsbir_pack_weights", self.dt, ptr(plan[1]), plan[2], plan[3], _s(),
                      kernel="pack_weights_kernel", tag=f"pack_weights x{plan[2]}")
             else:
@@ -247,9 +248,37 @@ class Engine:
             self._packed_key = key
         return self._packed
 
+    def _packed_ranges(self):
+        """(data_ptr, nbytes) of every packed buffer the replay writes into"""
+        out = []
+
+        def walk(v):
+            if isinstance(v, torch.Tensor):
+                out.append((v.data_ptr(), v.numel() * v.element_size()))
+            elif isinstance(v, (list, tuple)):
+                for x in v:
+                    walk(x)
+            elif isinstance(v, dict):
+                for x in v.values():
+                    walk(x)
+        walk(getattr(self, "_packed", None))
+        return tuple(sorted(out))
+
     def _make_plan(self, plan_key, recs):
         if not recs:
             return None
+        # the replay rewrites exactly the buffers _pack_all filled: every recorded
+        # destination lies in a packed buffer, and every packed buffer was written
+        # through a recorded pack (a pack added without recording would go stale)
+        ranges = self._packed_ranges()
+        hit = [False] * len(ranges)
+        for rec in recs:
+            dst = rec[1]
+            inside = [i for i, (b, n) in enumerate(ranges) if b <= dst < b + n]
+            assert inside, "re-pack plan: a recorded destination outside the packed buffers"
+            for i in inside:
+                hit[i] = True
+        assert all(hit), "re-pack plan: a packed buffer written without a recorded pack"
         dev = next(self.model.parameters()).device
         descs = (_hip.PackDesc * len(recs))()
         blk = 0
@@ -261,7 +290,7 @@ class Engine:
             else:
                 blk += -(-(co * r * s * ci_pad if mode == 0 else co) // PACK_EPB)
         raw = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8)
-        return (plan_key, raw.to(dev), len(recs), blk)
+        return (plan_key, raw.to(dev), len(recs), blk, ranges)
 
     def _pack_one(self, src, co, ci, r, s, ci_pad, mode, ldo, dst):
         call("artsbir_pack_weight", self.dt, ptr(src), co, ci, r, s, ci_pad, mode, ldo, ptr(dst), _s())
