@@ -202,11 +202,16 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
     const char* bb = bbase + SL * PP_BUF;
     const char* ab = abase + SL * PP_BUF;
     // ---- phase a: pixel fragments + channel fragments 0..3; pixel half of K-tile s+3
-    if (s + 3 < nk) issue_px((SL + 3) & 3);
+#ifndef PP_ABL
+#define PP_ABL 0  // timing ablations of a diagnostic build only (1: no stage loads in the loop, 2: no fragment reads)
+#endif
+    if (!(PP_ABL & 1) && s + 3 < nk) issue_px((SL + 3) & 3);
+    if (!(PP_ABL & 2) || s < 1) {
 #pragma unroll
-    for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(bb + j * 16 * PP_ROWB);
+      for (int j = 0; j < NTP; ++j) bv[j] = *reinterpret_cast<const uint4*>(bb + j * 16 * PP_ROWB);
 #pragma unroll
-    for (int i = 0; i < MTC / 2; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
+      for (int i = 0; i < MTC / 2; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
+    }
     pp_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -221,15 +226,17 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
     pp_barrier();
     // ---- phase b: channel fragments 4..7; weight half of K-tile s+3; K-tile s+1 retired
     if (s + 3 < nk) {
-      issue_ch((SL + 3) & 3);
+      if (!(PP_ABL & 1)) issue_ch((SL + 3) & 3);
       vm_wait<8>();
     } else if (s + 2 < nk) {
       vm_wait<4>();
     } else if (s + 1 < nk) {
       vm_wait<0>();
     }
+    if (!(PP_ABL & 2) || s < 1) {
 #pragma unroll
-    for (int i = MTC / 2; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
+      for (int i = MTC / 2; i < MTC; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
+    }
     pp_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);

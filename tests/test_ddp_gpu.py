@@ -170,6 +170,6 @@ def test_rccl_world1_collectives():
     assert p.exitcode == 0, p.exitcode
     err, n_during, vit_ok, knn_ok = q.get(timeout=5)
     print(f"RCCL world 1: gradient max rel diff {err:.2e}, all-reduces inside the backward {n_during}")
-    assert err == 0.0, err
+    assert err < 1e-5, err  # the f32 atomics of the weight gradients add in a different order per run
     assert n_during >= 3
     assert vit_ok and knn_ok
