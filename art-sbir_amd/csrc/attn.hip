@@ -23,6 +23,9 @@
 //                                  dV^T += dO^T P, dK^T += Q^T dS
 // P is recomputed from the forward's per-row log-sum-exp; nothing of size
 // L x L leaves the registers.
+#include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 namespace artsbir {
@@ -34,6 +37,9 @@ typedef __attribute__((address_space(3))) at_v4s* at_lds_v4s;
 
 constexpr int AT_MAXB = 8;                  // 32-row blocks: L <= 256
 constexpr int AT_IMG = AT_MAXB * 32 * 128;  // one [256][64] bf16 image
+
+constexpr float AT_LOG2E = 1.4426950408889634f, AT_LN2 = 0.6931471805599453f;
+constexpr float AT_SC2 = 0.125f * AT_LOG2E;  // the 1 / sqrt(64) score scale, log2 domain
 
 __device__ __forceinline__ int at_sw(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
 __device__ __forceinline__ int at_off(int row, int chunk) { return row * 128 + ((chunk ^ at_sw(row)) << 4); }
@@ -145,9 +151,14 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(const bf16* __restrict__ 
   for (int s = 0; s < 4; ++s) qf[s] = at_ld16(base + q * rs + 16 * s + 8 * hh, q < L);
   __syncthreads();
 
+  // softmax in the log2 domain: v = s / 8 * log2(e) in one multiply, p = 2^(v - m)
+  // on v_exp_f32 directly (mask values, natural-log units, scaled alike)
   f32x16 o0 = at_zero(), o1 = at_zero();
   float m = -INFINITY, l = 0.f;
-  for (int kb = 0; kb < nb; ++kb) {
+  // one key block; CHK: the last block when L % 32 != 0 (keys >= L get -inf:
+  // their K rows are zero, so without it they would enter the normaliser)
+  auto kblock = [&](int kb, auto chk) {
+    constexpr bool CHK = decltype(chk)::value;
     f32x16 st = at_zero();
 #pragma unroll
     for (int s = 0; s < 4; ++s) st = at_mfma(at_row(kimg, 32 * kb + r, s, hh), qf[s], st);
@@ -155,21 +166,21 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(const bf16* __restrict__ 
 #pragma unroll
     for (int rho = 0; rho < 16; ++rho) {
       const int key = 32 * kb + at_crow(rho, hh);
-      float v = st[rho] * 0.125f;
-      if (MASK && key < L && q < L) v += mask[(long long)q * L + key];
-      if (key >= L) v = -INFINITY;
+      float v = st[rho] * AT_SC2;
+      if (MASK && key < L && q < L) v += mask[(long long)q * L + key] * AT_LOG2E;
+      if ((CHK || MASK) && key >= L) v = -INFINITY;
       st[rho] = v;
       mx = fmaxf(mx, v);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m, mx);
     const float mu = mn == -INFINITY ? 0.f : mn;
-    const float alpha = __expf(m - mu);
+    const float alpha = __builtin_amdgcn_exp2f(m - mu);
     float sum = 0.f;
     bf16x8 pf0, pf1;
 #pragma unroll
     for (int rho = 0; rho < 16; ++rho) {
-      const float p = __expf(st[rho] - mu);
+      const float p = __builtin_amdgcn_exp2f(st[rho] - mu);
       sum += p;
       if (rho < 8) pf0[rho] = (bf16)p;
       else pf1[rho - 8] = (bf16)p;
@@ -183,11 +194,14 @@ __global__ void __launch_bounds__(512) attn_fwd_kernel(const bf16* __restrict__ 
     o0 = at_mfma(at_trfrag(vimg, 32 * kb + 16, 0, lane), pf1, o0);
     o1 = at_mfma(at_trfrag(vimg, 32 * kb, 32, lane), pf0, o1);
     o1 = at_mfma(at_trfrag(vimg, 32 * kb + 16, 32, lane), pf1, o1);
-  }
+  };
+  const int nfull = (L & 31) ? nb - 1 : nb;
+  for (int kb = 0; kb < nfull; ++kb) kblock(kb, std::false_type{});
+  if (nfull < nb) kblock(nb - 1, std::true_type{});
   float am = 0.f;
   if (q < L) {
     at_store_t(out + ((long long)q * N + n) * E + h * 64, o0, o1, 1.f / l, hh);
-    if (lse && hh == 0) lse[((long long)q * N + n) * heads + h] = m + __logf(l);
+    if (lse && hh == 0) lse[((long long)q * N + n) * heads + h] = (m + __log2f(l)) * AT_LN2;
     if (pmax) {
       const float il = 1.f / l;
 #pragma unroll
@@ -346,6 +360,161 @@ __global__ void __launch_bounds__(512) attn_bwd_kv_kernel(const bf16* __restrict
   }
 }
 
+// The backward in ONE workgroup per (batch n, head h): the four (L x 64)
+// slices Q, K, V, dO are staged into LDS once (128 KB) and wave w runs the query
+// side of block w (dQ) and then the key side of block w (dK, dV) on them.  The
+// two-kernel form above read Q, K, V and dO twice from HBM (once per side) and
+// passed D = rowsum(dO o O) through global memory: 6.2 GB per ViT-B/16 layer
+// at 512 triplets (profiles/r4_c5_pmc_traffic.json) where this one needs
+// 3.7 GB (Q K V dO O once, dQ dK dV once).  The q side's own operands come from
+// the images (at_row of image row q is the layout at_ld16 loads).  Softmax in
+// the log2 domain (one FMA and v_exp_f32 per element) and, without a mask, no
+// validity tests (see the comments in the loops).
+template <bool MASK>
+__global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
+                                                       const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                       int L, int N, int heads, const float* __restrict__ mask,
+                                                       bf16* __restrict__ dqkv) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * AT_IMG];
+  __shared__ __attribute__((aligned(16))) float ls[AT_MAXB * 32], ds_[AT_MAXB * 32];
+  char* kimg = smem;
+  char* vimg = smem + AT_IMG;
+  char* qimg = smem + 2 * AT_IMG;
+  char* gimg = smem + 3 * AT_IMG;
+  const int nb = (L + 31) >> 5;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int h = (int)(blockIdx.x % heads), n = (int)(blockIdx.x / heads);
+  const int E = heads * 64;
+  const long long ld = 3LL * E, rs = (long long)N * ld, ors = (long long)N * E;
+  const bf16* base = qkv + (long long)n * ld + h * 64;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q = 32 * w + r;  // the q side's row and the key side's key
+  const bool qok = q < L;
+  const long long orow = (long long)q * ors + (long long)n * E + h * 64;
+  // O and dO of this wave's query rows for D (issued ahead of the staging)
+  bf16x8 of[4], gd[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    of[s] = at_ld16(o + orow + 16 * s + 8 * hh, qok);
+    gd[s] = at_ld16(dout + orow + 16 * s + 8 * hh, qok);
+  }
+  const long long item = ((long long)q * N + n) * heads + h;
+  const float lq = qok ? lse[item] : 0.f;
+  at_stage2(base + E, rs, base + 2 * E, rs, L, kimg, vimg, tid, nb * 64);
+  at_stage2(base, rs, dout + (long long)n * E + h * 64, ors, L, qimg, gimg, tid, nb * 64);
+  float D = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) D += (float)gd[s][j] * (float)of[s][j];
+  D += __shfl_xor(D, 32, 64);
+  const float lq2 = lq * AT_LOG2E;  // log-sum-exp in the log2 domain
+  if (hh == 0) {
+    ls[q] = lq2;
+    ds_[q] = qok ? D : 0.f;
+  }
+  __syncthreads();
+
+  {  // ---- query side of block w: S^T = K Q^T, dP^T = V dO^T, dQ^T += K^T dS^T
+    bf16x8 qf[4], gf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      qf[s] = at_row(qimg, q, s, hh);
+      gf[s] = at_row(gimg, q, s, hh);
+    }
+    f32x16 dq0 = at_zero(), dq1 = at_zero();
+    for (int kb = 0; kb < nb; ++kb) {
+      f32x16 st = at_zero(), dpt = at_zero();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        st = at_mfma(at_row(kimg, 32 * kb + r, s, hh), qf[s], st);
+        dpt = at_mfma(at_row(vimg, 32 * kb + r, s, hh), gf[s], dpt);
+      }
+      bf16x8 df0, df1;
+#pragma unroll
+      for (int rho = 0; rho < 16; ++rho) {
+        // no validity test without a mask: a key >= L has zero K and V rows, so
+        // its dS (finite) meets a zero row of K in dQ; rows q >= L are not stored
+        float p;
+        if (MASK) {
+          const int key = 32 * kb + at_crow(rho, hh);
+          float v = st[rho] * AT_SC2;
+          if (key < L && qok) v += mask[(long long)q * L + key] * AT_LOG2E;
+          p = (key < L && qok) ? __builtin_amdgcn_exp2f(v - lq2) : 0.f;
+        } else {
+          p = __builtin_amdgcn_exp2f(fmaf(st[rho], AT_SC2, -lq2));
+        }
+        const float ds = p * (dpt[rho] - D);
+        if (rho < 8) df0[rho] = (bf16)ds;
+        else df1[rho - 8] = (bf16)ds;
+      }
+      dq0 = at_mfma(at_trfrag(kimg, 32 * kb, 0, lane), df0, dq0);
+      dq0 = at_mfma(at_trfrag(kimg, 32 * kb + 16, 0, lane), df1, dq0);
+      dq1 = at_mfma(at_trfrag(kimg, 32 * kb, 32, lane), df0, dq1);
+      dq1 = at_mfma(at_trfrag(kimg, 32 * kb + 16, 32, lane), df1, dq1);
+    }
+    if (qok) at_store_t(dqkv + (long long)q * rs + (long long)n * ld + h * 64, dq0, dq1, 0.125f, hh);
+  }
+
+  // ---- key side of block w: S = Q K^T, dP = dO V^T, dS = P (dP - D),
+  // dV^T += dO^T P, dK^T += Q^T dS
+  const int key = q;
+  const bool kok = qok;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = at_row(kimg, key, s, hh);
+    vf[s] = at_row(vimg, key, s, hh);
+  }
+  f32x16 dk0 = at_zero(), dk1 = at_zero(), dv0 = at_zero(), dv1 = at_zero();
+  for (int qb = 0; qb < nb; ++qb) {
+    f32x16 sc = at_zero(), dp = at_zero();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      sc = at_mfma(at_row(qimg, 32 * qb + r, s, hh), kf[s], sc);
+      dp = at_mfma(at_row(gimg, 32 * qb + r, s, hh), vf[s], dp);
+    }
+    bf16x8 pf0, pf1, df0, df1;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int q0 = 32 * qb + 8 * g + 4 * hh;
+      const float4 l4 = *reinterpret_cast<const float4*>(&ls[q0]);
+      const float4 d4 = *reinterpret_cast<const float4*>(&ds_[q0]);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rho = 4 * g + e, qi = q0 + e;
+        // no validity test without a mask: a query row >= L has zero Q and dO
+        // rows and ls = ds_ = 0, so p = 1 meets dP = 0 and a zero row of dO
+        float p;
+        if (MASK) {
+          float v = sc[rho] * AT_SC2;
+          if (qi < L && kok) v += mask[(long long)qi * L + key] * AT_LOG2E;
+          p = (qi < L && kok) ? __builtin_amdgcn_exp2f(v - lv[e]) : 0.f;
+        } else {
+          p = __builtin_amdgcn_exp2f(fmaf(sc[rho], AT_SC2, -lv[e]));
+        }
+        const float d = p * (dp[rho] - dv[e]);
+        if (rho < 8) { pf0[rho] = (bf16)p; df0[rho] = (bf16)d; }
+        else { pf1[rho - 8] = (bf16)p; df1[rho - 8] = (bf16)d; }
+      }
+    }
+    dv0 = at_mfma(at_trfrag(gimg, 32 * qb, 0, lane), pf0, dv0);
+    dv0 = at_mfma(at_trfrag(gimg, 32 * qb + 16, 0, lane), pf1, dv0);
+    dv1 = at_mfma(at_trfrag(gimg, 32 * qb, 32, lane), pf0, dv1);
+    dv1 = at_mfma(at_trfrag(gimg, 32 * qb + 16, 32, lane), pf1, dv1);
+    dk0 = at_mfma(at_trfrag(qimg, 32 * qb, 0, lane), df0, dk0);
+    dk0 = at_mfma(at_trfrag(qimg, 32 * qb + 16, 0, lane), df1, dk0);
+    dk1 = at_mfma(at_trfrag(qimg, 32 * qb, 32, lane), df0, dk1);
+    dk1 = at_mfma(at_trfrag(qimg, 32 * qb + 16, 32, lane), df1, dk1);
+  }
+  if (kok) {
+    bf16* dst = dqkv + (long long)key * rs + (long long)n * ld + h * 64;
+    at_store_t(dst + E, dk0, dk1, 0.125f, hh);
+    at_store_t(dst + 2 * E, dv0, dv1, 1.f, hh);
+  }
+}
+
 // launchers (vit.hip's entry points route bf16 here): false if not applicable
 bool attn_fwd_mfma(const bf16* qkv, int L, int N, int heads, const float* mask, bf16* out, float* lse,
                    unsigned* pmax, hipStream_t st) {
@@ -368,6 +537,18 @@ bool attn_bwd_mfma(const bf16* qkv, const bf16* o, const bf16* dout, const float
   const long long grid = (long long)N * heads;
   if (grid > 0x7fffffffLL) return false;
   const int nthr = ((L + 31) / 32) * 64;
+  // ARTSBIR_ATTN_BWD2=1: the two-kernel form (timing comparison)
+  static const bool two = [] { const char* e = getenv("ARTSBIR_ATTN_BWD2"); return e && atoi(e) != 0; }();
+  // the one-workgroup form addresses rows by 32-bit buffer offsets
+  if (!two) {
+    if (mask)
+      hipLaunchKernelGGL(attn_bwd_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, o, dout, lse, L, N, heads,
+                         mask, dqkv);
+    else
+      hipLaunchKernelGGL(attn_bwd_kernel<false>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, o, dout, lse, L, N,
+                         heads, mask, dqkv);
+    return true;
+  }
   if (mask) {
     hipLaunchKernelGGL(attn_bwd_q_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, o, dout, lse, L, N,
                        heads, mask, dqkv, dscratch);

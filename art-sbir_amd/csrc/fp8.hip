@@ -605,7 +605,12 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
 // measured slower on every C5 shape (qkv 1.09 vs 0.93 ms, c_fc 1.29 vs 1.13,
 // out_proj 0.62 vs 0.58, c_proj 0.94 vs 0.83 ms; profiles/r3_fp8_tile_ab.txt):
 // the doubled A re-reads and LDS bytes per MAC cost more than the deeper ring
-// saves, so the wait per k-step is not what bounds the 256-wide tile
+// saves, so the wait per k-step is not what bounds the 256-wide tile.  Nor is
+// the ring depth (round 4): pp256.hip's ping-pong schedule rebuilt for fp8
+// (32x32x64 block-scaled MFMAs on 64-k LDS rows, four buffers, three K-tiles
+// in flight, epilogue from the registers by buffer stores) ran 12-29 % slower
+// on all four shapes (qkv 1.06 vs 0.93, out_proj 0.76 vs 0.59, c_fc 1.34 vs
+// 1.14, c_proj 0.96 vs 0.83 ms; profiles/r4_fp8_attn.txt) and was dropped
 static int fp8_bn(int N) {
   static const int forced = [] { const char* e = getenv("ARTSBIR_FP8_BN"); return e ? atoi(e) : 0; }();
   return forced == 128 ? 128 : 256;

@@ -255,10 +255,12 @@ def test_vit_backward_kernels_individually(dev):
 @pytest.mark.gpu
 @pytest.mark.parametrize("L,N,heads,masked", [(1, 2, 1, False), (9, 3, 2, True), (32, 2, 2, False),
                                               (33, 2, 3, True), (197, 4, 12, False), (197, 2, 2, True),
-                                              (256, 2, 2, False)])
+                                              (256, 2, 2, False), (100, 3, 4, False), (160, 2, 2, True),
+                                              (64, 5, 1, False)])
 def test_mfma_attention_bf16(L, N, heads, masked, dev):
-    """the bf16 attention core (attn.hip: MFMA forward with online softmax, query-
-    and key-side MFMA backward) against float64 autograd on the same bf16 inputs:
+    """the bf16 attention core (attn.hip: MFMA forward with online softmax, the
+    one-workgroup query- and key-side MFMA backward, both LDS-DMA staged, one
+    instantiation per count of 32-row blocks) against float64 autograd on the same bf16 inputs:
     output and gradients within 2e-2 relative L2 (bf16 P / dS operands and bf16
     outputs), log-sum-exp within 1e-4"""
     import _hip
