@@ -112,35 +112,69 @@ __global__ void __launch_bounds__(256) layernorm_v_kernel(const T* __restrict__ 
   if (pmax) vt_block_amax(am, pmax);
 }
 
+typedef __attribute__((ext_vector_type(4))) unsigned vt_u32x4;
+// raw 8-element chunks of a row (bf16: one 16-B load, f32: two), converted to
+// f32 only when used, so that the next row's loads can be in flight meanwhile
+template <typename T>
+struct VtRaw {
+  uint4 v[sizeof(T) == 2 ? 1 : 2];
+};
+__device__ __forceinline__ void vt_raw_load(const bf16* p, VtRaw<bf16>& r) { r.v[0] = *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ void vt_raw_load(const float* p, VtRaw<float>& r) {
+  r.v[0] = reinterpret_cast<const uint4*>(p)[0];
+  r.v[1] = reinterpret_cast<const uint4*>(p)[1];
+}
+__device__ __forceinline__ void vt_raw_cvt(const VtRaw<bf16>& r, float (&v)[8]) {
+  const bf16x8 b = __builtin_bit_cast(bf16x8, r.v[0]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)b[i];
+}
+__device__ __forceinline__ void vt_raw_cvt(const VtRaw<float>& r, float (&v)[8]) {
+  v[0] = __uint_as_float(r.v[0].x); v[1] = __uint_as_float(r.v[0].y); v[2] = __uint_as_float(r.v[0].z);
+  v[3] = __uint_as_float(r.v[0].w); v[4] = __uint_as_float(r.v[1].x); v[5] = __uint_as_float(r.v[1].y);
+  v[6] = __uint_as_float(r.v[1].z); v[7] = __uint_as_float(r.v[1].w);
+}
+// x, dy (and dres) of one row, every lane's chunks loaded unconditionally
+// (chunks past C repeat the last one and are masked at use): no branch around
+// the loads, so the compiler counts them across the row loop
+template <typename T, int NCH>
+struct LnRow {
+  VtRaw<T> x[NCH], g[NCH], r[NCH];
+};
+template <typename T, int NCH, bool RES>
+__device__ __forceinline__ void ln_fetch(const T* __restrict__ x, const T* __restrict__ dy, const T* dres, long long row,
+                                         int C, int lane, LnRow<T, NCH>& R) {
+  const int nch = C >> 3;
+#pragma unroll
+  for (int u = 0; u < NCH; ++u) {
+    const int ch = min(lane + 64 * u, nch - 1);
+    vt_raw_load(x + row * C + ch * 8, R.x[u]);
+    vt_raw_load(dy + row * C + ch * 8, R.g[u]);
+    if (RES) vt_raw_load(dres + row * C + ch * 8, R.r[u]);
+  }
+}
+
 // LayerNorm backward with 8-column chunks per lane; each block's 4 waves reduce
 // their dgamma / dbeta partials in LDS and add them with one atomic per column
-template <typename T, int NCH, bool SUMS>
-__device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __restrict__ dy, const T* dres, T* dx,
-                                           long long row, int C, float eps, int lane, const float (&gm)[NCH][8],
-                                           float (&pg)[NCH][8], float (&pb)[NCH][8], float (&pr)[NCH][8],
-                                           float (&po)[NCH][8]) {
+template <typename T, int NCH, bool SUMS, bool RES>
+__device__ __forceinline__ void ln_bwd_row(const LnRow<T, NCH>& R, T* dx, long long row, int C, float eps, int lane,
+                                           const float (&gm)[NCH][8], float (&pg)[NCH][8], float (&pb)[NCH][8],
+                                           float (&pr)[NCH][8], float (&po)[NCH][8]) {
   const int nch = C >> 3;
-  const T* xr = x + row * C;
-  const T* gr = dy + row * C;
-  const T* rr = dres ? dres + row * C : nullptr;
   float xv[NCH][8], gv[NCH][8], res[NCH][8];
   float s = 0.f;
 #pragma unroll
-  for (int u = 0; u < NCH; ++u) {  // all three operands of the row requested together
-    const int ch = lane + 64 * u;
-    if (ch < nch) {
-      vt_load8(xr + ch * 8, xv[u]);
-      vt_load8(gr + ch * 8, gv[u]);
-      if (rr) vt_load8(rr + ch * 8, res[u]);
-    } else {
+  for (int u = 0; u < NCH; ++u) {
+    const bool ok = lane + 64 * u < nch;
+    vt_raw_cvt(R.x[u], xv[u]);
+    vt_raw_cvt(R.g[u], gv[u]);
+    if (RES) vt_raw_cvt(R.r[u], res[u]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { xv[u][e] = 0.f; gv[u][e] = 0.f; }
+    for (int e = 0; e < 8; ++e) {
+      if (!ok) { xv[u][e] = 0.f; gv[u][e] = 0.f; }
+      if (!RES || !ok) res[u][e] = 0.f;
+      s += xv[u][e];
     }
-    if (!rr || ch >= nch)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) res[u][e] = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += xv[u][e];
   }
   const float mean = warp_sum(s) / (float)C;
   float q = 0.f;
@@ -166,19 +200,35 @@ __device__ __forceinline__ void ln_bwd_row(const T* __restrict__ x, const T* __r
     }
   a = warp_sum(a) / (float)C;
   b = warp_sum(b) / (float)C;
-  T* o = dx + row * C;
+  // the row's dx by buffer stores: a chunk past C goes past the descriptor's
+  // end and is dropped (no branch around the stores either)
+  const __amdgpu_buffer_rsrc_t orow =
+      __builtin_amdgcn_make_buffer_rsrc(dx + row * C, (short)0, C * (int)sizeof(T), 0x00020000);
 #pragma unroll
   for (int u = 0; u < NCH; ++u) {
     const int ch = lane + 64 * u;
-    if (ch < nch) {
-      float out[8];
+    const unsigned off = ch < nch ? (unsigned)(ch * 8 * (int)sizeof(T)) : 0x80000000u;
+    float out[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[u][e];
-      vt_store8(o + ch * 8, out);
-      if constexpr (SUMS) {  // column sums of the residual gradient and of dx (bias gradients)
+    for (int e = 0; e < 8; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[u][e];
+    if constexpr (sizeof(T) == 2) {
+      uint4 h;
+      unsigned* hp = &h.x;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) { pr[u][e] += res[u][e]; po[u][e] += out[e]; }
-      }
+      for (int k = 0; k < 4; ++k)
+        hp[k] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)out[2 * k]) |
+                ((unsigned)__builtin_bit_cast(unsigned short, (bf16)out[2 * k + 1]) << 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(vt_u32x4, h), orow, off, 0, 0);
+    } else {
+      vt_u32x4 f0, f1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { f0[k] = __float_as_uint(out[k]); f1[k] = __float_as_uint(out[4 + k]); }
+      __builtin_amdgcn_raw_buffer_store_b128(f0, orow, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(f1, orow, off == 0x80000000u ? off : off + 16, 0, 0);
+    }
+    if constexpr (SUMS) {  // column sums of the residual gradient and of dx (bias gradients; chunks past C unused)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { pr[u][e] += res[u][e]; po[u][e] += out[e]; }
     }
   }
 }
@@ -195,7 +245,7 @@ __global__ void __launch_bounds__(256) layernorm_bwd_v_kernel(const T* __restric
                                                               float* __restrict__ dx_sum) {
   constexpr int NR = SUMS ? 4 : 2;
   __shared__ float red[NR][3][64 * NCH * 8];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nch = C >> 3;
   float pg[NCH][8], pb[NCH][8], gm[NCH][8], pr[NCH][8], po[NCH][8];
 #pragma unroll
@@ -205,8 +255,27 @@ __global__ void __launch_bounds__(256) layernorm_bwd_v_kernel(const T* __restric
     for (int e = 0; e < 8; ++e) { pg[u][e] = 0.f; pb[u][e] = 0.f; gm[u][e] = 0.f; pr[u][e] = 0.f; po[u][e] = 0.f; }
     if (ch < nch) vt_load8(gamma + ch * 8, gm[u]);
   }
-  for (long long row = blockIdx.x * 4LL + w; row < rows; row += gridDim.x * 4LL)
-    ln_bwd_row<T, NCH, SUMS>(x, dy, dres, dx, row, C, eps, lane, gm, pg, pb, pr, po);
+  // rows in a stride of the grid, the next row's operands loaded before this
+  // row's arithmetic and store (one wave per row, two waves per SIMD: without
+  // the prefetch each row's loads wait out a full memory latency)
+  const long long stride = gridDim.x * 4LL;
+  long long row = blockIdx.x * 4LL + w;
+  if (row < rows) {
+    LnRow<T, NCH> cur, nxt;
+    if (dres) ln_fetch<T, NCH, true>(x, dy, dres, row, C, lane, cur);
+    else ln_fetch<T, NCH, false>(x, dy, dres, row, C, lane, cur);
+    for (; row < rows; row += stride) {
+      const long long rn = min(row + stride, rows - 1);  // the last row re-fetched: no branch around the loads
+      if (dres) {
+        ln_fetch<T, NCH, true>(x, dy, dres, rn, C, lane, nxt);
+        ln_bwd_row<T, NCH, SUMS, true>(cur, dx, row, C, eps, lane, gm, pg, pb, pr, po);
+      } else {
+        ln_fetch<T, NCH, false>(x, dy, dres, rn, C, lane, nxt);
+        ln_bwd_row<T, NCH, SUMS, false>(cur, dx, row, C, eps, lane, gm, pg, pb, pr, po);
+      }
+      cur = nxt;
+    }
+  }
   if (w > 0) {
 #pragma unroll
     for (int u = 0; u < NCH; ++u)
