@@ -692,13 +692,19 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     constexpr int PF = KB < 6 ? KB : 6;
     f32x16 acc = {};
     uint4 bq[KB];
+#ifndef KNN_ABL
+#define KNN_ABL 0  // timing ablations of a diagnostic build only (1: no list work, 2: no MFMAs; tools/gpu/r4_knn_abl.sh)
+#endif
 #pragma unroll
     for (int j = 0; j < PF; ++j) bq[j] = *reinterpret_cast<const uint4*>(bp + j * 32);
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
       if (kb + PF < KB) bq[kb + PF] = *reinterpret_cast<const uint4*>(bp + (kb + PF) * 32);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[kb]),
-                                                    *reinterpret_cast<const bf16x8*>(&bq[kb]), acc, 0, 0, 0);
+      if (KNN_ABL & 2)
+        acc[kb & 15] += __uint_as_float(bq[kb].x & 0x80000000u);
+      else
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[kb]),
+                                                      *reinterpret_cast<const bf16x8*>(&bq[kb]), acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     const int bn = g0 + t * V2_ROWS;
@@ -722,6 +728,10 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     bool any = false;
 #pragma unroll
     for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[e], gsq) <= critp[e];
+    if (KNN_ABL & 1) {
+      st_entries += __builtin_amdgcn_ballot_w64(any) ? 1u : 0u;
+      any = false;
+    }
     if (__builtin_amdgcn_ballot_w64(any)) {
       ++st_entries;
       // stage the raw dot products of every row with a prefilter hit; the owner
