@@ -42,13 +42,19 @@ __global__ void __launch_bounds__(512, 1) fill_kernel(const char* __restrict__ s
 #pragma unroll
       for (int u = 0; u < 4; ++u) {  // 32 KB = 32 pieces of 1 KB, 4 per wave
         const int piece = u * 8 + w;
-        const unsigned off = (unsigned)(blk * 32768 + piece * 1024 + lane * 16);
+        unsigned off = (unsigned)(blk * 32768 + piece * 1024 + lane * 16);
+        asm volatile("" : "+v"(off));  // opaque: no hoisting of the loads out of the iteration loop
         if (MODE == 0) {
           dma16(r, (unsigned)(unsigned long long)(lds_t)(&smem[slot][piece * 1024]), off);
         } else {
-          const uint4 v = *reinterpret_cast<const uint4*>(src + off);
-          if (MODE == 1) *reinterpret_cast<uint4*>(&smem[slot][piece * 1024 + lane * 16]) = v;
-          else { accv.x ^= v.x; accv.y ^= v.y; accv.z ^= v.z; accv.w ^= v.w; }
+          typedef __attribute__((ext_vector_type(4))) unsigned u4;
+          const u4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+          if (MODE == 1) {
+            unsigned lo = (unsigned)(unsigned long long)(lds_t)(&smem[slot][piece * 1024 + lane * 16]);
+            asm volatile("ds_write_b128 %0, %1" ::"v"(lo), "v"(v) : "memory");
+          } else {
+            accv.x ^= v.x; accv.y ^= v.y; accv.z ^= v.z; accv.w ^= v.w;
+          }
         }
       }
       if (MODE == 0 && slot == 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // two blocks in flight
