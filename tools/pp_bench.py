@@ -5,7 +5,7 @@ interleaved over rounds in one process (guide §5.4 rule 24), with the max error
 against torch.matmul / conv2d on the same bf16 operands.  torch is the checker
 and a scale reference only; the product path never calls it.
 
-usage: python tools/pp_bench.py [--cands 0,5,19,22,23] [--rounds 3] [--only nt|conv]"""
+usage: python tools/pp_bench.py [--cands 0,5,19,22] [--rounds 3] [--only nt|conv]"""
 import argparse
 import os
 import sys
@@ -25,6 +25,7 @@ NT = [  # M, N, K: C5 projection data gradients (302592 tokens) and forwards, at
 CONV = [  # N, H, W, C, Cout, R (3x3 stride 1 pad 1 forwards of C2 at 1152 images)
     (1152, 56, 56, 64, 64, 3), (1152, 28, 28, 128, 128, 3), (1152, 14, 14, 256, 256, 3), (1152, 7, 7, 512, 512, 3),
     (1152, 56, 56, 64, 256, 1), (1152, 28, 28, 512, 128, 1),
+    (1152, 112, 112, 32, 64, 3), (1152, 112, 112, 32, 32, 3), (1152, 112, 112, 64, 32, 3),  # stem (and its dgrads)
 ]
 
 
@@ -53,7 +54,7 @@ def set_cfg(c):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cands", default="0,5,19,22,23")
+    ap.add_argument("--cands", default="0,5,19,22")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="")
     args = ap.parse_args()
