@@ -115,17 +115,35 @@ __device__ __forceinline__ bf16x8 at_ld16(const bf16* p, bool ok) {
 // accumulator row of register rho for lane half hh
 __device__ __forceinline__ int at_crow(int rho, int hh) { return (rho & 3) + 8 * (rho >> 2) + 4 * hh; }
 
-// rows of C^T (d = 32 dt + at_crow) of column `col` (lane) -> dst[d], 8-byte stores
+// rows of C^T (d = 32 dt + at_crow) of column `col` (lane) -> dst[d] with
+// 16-byte stores: lane half hh holds d = 32 dt + 8 g + 4 hh + (0..3), so each
+// 8-element group is split over lanes l and l + 32; v_permlane32_swap hands
+// lane l the upper halves of groups 0 and 2 and lane l + 32 the lower halves of
+// groups 1 and 3, and every lane stores two whole groups (four dwordx4 stores
+// per call instead of eight dwordx2: the epilogue store tail is issue-bound,
+// MI355X_MICROARCH's attention-epilogue row)
+__device__ __forceinline__ unsigned at_pack2(float a, float b) {
+  return (unsigned)__builtin_bit_cast(unsigned short, (bf16)a) |
+         ((unsigned)__builtin_bit_cast(unsigned short, (bf16)b) << 16);
+}
 __device__ __forceinline__ void at_store_t(bf16* dst, const f32x16& c0, const f32x16& c1, float scale, int hh) {
 #pragma unroll
   for (int dt = 0; dt < 2; ++dt) {
     const f32x16& c = dt ? c1 : c0;
+    unsigned x[4][2];  // group g: elements 4 hh + (0, 1) | (2, 3) of d = 32 dt + 8 g
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      __attribute__((ext_vector_type(4))) bf16 v;
+      x[g][0] = at_pack2(c[4 * g] * scale, c[4 * g + 1] * scale);
+      x[g][1] = at_pack2(c[4 * g + 2] * scale, c[4 * g + 3] * scale);
+    }
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (bf16)(c[4 * g + e] * scale);
-      *reinterpret_cast<decltype(v)*>(dst + 32 * dt + 8 * g + 4 * hh) = v;
+    for (int gp = 0; gp < 2; ++gp) {  // groups (0, 1) then (2, 3)
+      uint4 o;
+      const auto s0 = __builtin_amdgcn_permlane32_swap(x[2 * gp][0], x[2 * gp + 1][0], false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(x[2 * gp][1], x[2 * gp + 1][1], false, false);
+      // lane l: group 2 gp = (own lower half, lane l + 32's upper half); lane l + 32: group 2 gp + 1
+      o.x = s0[0]; o.y = s1[0]; o.z = s0[1]; o.w = s1[1];
+      *reinterpret_cast<uint4*>(dst + 32 * dt + 8 * (2 * gp + hh)) = o;
     }
   }
 }
