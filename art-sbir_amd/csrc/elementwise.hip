@@ -23,11 +23,21 @@ template <> __device__ __forceinline__ void load8<float>(const float* p, float (
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8]);
+#ifndef ARTSBIR_NT_STORES
+// 1: streaming (non-temporal) stores of the elementwise passes too — measured
+// slower than plain stores on top of the GEMM epilogues' (profiles/r4_nt_stores.txt)
+#define ARTSBIR_NT_STORES 0
+#endif
 template <> __device__ __forceinline__ void store8<bf16>(bf16* p, const float (&v)[8]) {
   Vec16<bf16> r;
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.v[i] = (bf16)v[i];
-  st16<bf16>(p, r);
+  if constexpr (ARTSBIR_NT_STORES) {
+    typedef unsigned st_u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(*reinterpret_cast<const st_u32x4*>(&r), reinterpret_cast<st_u32x4*>(p));
+  } else {
+    st16<bf16>(p, r);
+  }
 }
 template <> __device__ __forceinline__ void store8<float>(float* p, const float (&v)[8]) {
   *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);

@@ -698,7 +698,19 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
           Vec16<bf16> o;
 #pragma unroll
           for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
-          st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
+#ifndef PG_NT_STORE
+// the global-operand (GLB) epilogues store their output non-temporally: the
+// lines are not allocated in L2, so the residual / BN-target operand lines the
+// next channel pair reads stay resident (read bytes -15 %, C2 step -0.6 to
+// -0.8 ms; tools/gpu/r4_ntst.sh, r4_ntst_step.sh, profiles/r4_nt_stores.txt)
+#define PG_NT_STORE 1
+#endif
+          if (PG_NT_STORE && GLB) {
+            typedef __attribute__((ext_vector_type(4))) unsigned pg_u4;
+            __builtin_nontemporal_store(*reinterpret_cast<const pg_u4*>(&o),
+                                        reinterpret_cast<pg_u4*>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0));
+          } else
+            st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
         }
       }
     }

@@ -57,6 +57,18 @@ def pmc_traffic(kernel, path=None):
     return None if k is None else round(k["hbm_bytes_per_launch"])
 
 
+def pmc_traffic_by_size(kernel, path=None):
+    """the same kernel's bytes with the reads counted by request size (None
+    when the traffic file has no request-size pass)"""
+    try:
+        with open(path or PMC_TRAFFIC) as f:
+            ks = json.load(f)["kernels"]
+        k = ks.get(kernel) or ks.get(kernel.split("<")[0])
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if k is None or "hbm_bytes_by_size_per_launch" not in k else round(k["hbm_bytes_by_size_per_launch"])
+
+
 def encoder_flops_per_image(layers=LAYERS, out_dim=OUT_DIM, res=RES, width=WIDTH):
     """Algorithmic forward FLOPs of one image (2 x MACs of every conv/linear +
     the attention core), from the models.py:275-360 geometry."""
@@ -151,6 +163,8 @@ def roofline(prof, peak_of, traffic_file=None):
     traffic = pmc_traffic(dom, tf)
     roof.update({"traffic": traffic, "traffic_source": os.path.relpath(tf, ROOT) if traffic is not None else None,
                  "traffic_over_algorithmic": round(traffic / (nb / cnt), 3) if traffic and nb else None,
+                 # reads by request size (FETCH_SIZE x 2 over-counts 64-B requests 2x)
+                 "traffic_by_request_size": pmc_traffic_by_size(dom, tf),
                  "kernel": dom, "launches": cnt, "avg_launch_us": round(secs / cnt * 1e6, 2),
                  "avg_launch_flops": fl / cnt, "avg_launch_bytes": nb / cnt,
                  "intensity_flop_per_byte": round(fl / nb, 1) if nb else None,

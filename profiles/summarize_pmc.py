@@ -6,7 +6,11 @@
     python profiles/summarize_pmc.py gpurun_out/pmc_train gpurun_out/pmc_retr profiles/r2_pmc_traffic.json
 
 Counter values are KiB.  gfx950 correction (MI355X_MICROARCH.md §HBM):
-FETCH_SIZE reports half the bytes of a wide coalesced stream -> doubled;
+FETCH_SIZE reports half the bytes of a wide coalesced stream -> doubled (exact
+for 128-B requests only: a kernel whose loads make 64-B requests, such as
+16 B x 4 lanes per row segment, is over-counted 2x by it; an optional third
+pass pmc_req/ with TCC_EA0_RDREQ_32B/_64B/_128B and TCC_EA0_RDREQ gives the
+read bytes by request size);
 WRITE_SIZE is exact for 16-B-per-lane stores and float atomics.  Kernels are
 keyed by the short names bench.py uses (template variants of one tile shape
 are pooled, weighted by launch count).
@@ -100,9 +104,33 @@ def load(path, counter):
     return agg
 
 
+def load_req(path):
+    """read bytes by request size from a pass with TCC_EA0_RDREQ_{32B,64B,128B}
+    and TCC_EA0_RDREQ: per kernel [dispatches, bytes = 32 n32 + 64 n64 + 128 n128,
+    requests, RDREQ] (values summed over the counter's instances per dispatch)"""
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for r in csv.DictReader(open(path)):
+        d = r["Dispatch_Id"]
+        names[d] = short(r["Kernel_Name"])
+        per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    agg = collections.defaultdict(lambda: [0, 0.0, 0.0, 0.0])
+    for d, c in per.items():
+        a = agg[names[d]]
+        a[0] += 1
+        a[1] += 32 * c["TCC_EA0_RDREQ_32B"] + 64 * c["TCC_EA0_RDREQ_64B"] + 128 * c["TCC_EA0_RDREQ_128B"]
+        a[2] += c["TCC_EA0_RDREQ_32B"] + c["TCC_EA0_RDREQ_64B"] + c["TCC_EA0_RDREQ_128B"]
+        a[3] += c["TCC_EA0_RDREQ"]
+    return agg
+
+
 def summarize(src):
     fetch = load(f"{src}/pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
     write = load(f"{src}/pmc_write/run_counter_collection.csv", "WRITE_SIZE")
+    try:
+        req = load_req(f"{src}/pmc_req/run_counter_collection.csv")
+    except OSError:
+        req = {}
     out = {}
     for k in fetch:
         if k not in write:
@@ -111,6 +139,13 @@ def summarize(src):
         nw, bw = write[k]
         out[k] = {"launches": nf, "fetch_bytes_per_launch": 2.0 * bf / nf, "write_bytes_per_launch": bw / nw,
                   "hbm_bytes_per_launch": 2.0 * bf / nf + bw / nw}
+        if k in req and req[k][0]:
+            n, b, nreq, rd = req[k]
+            # FETCH_SIZE x 2 is exact only for 128-B requests; the request-size
+            # counters give the read bytes whatever the access width
+            out[k]["read_bytes_by_size_per_launch"] = b / n
+            out[k]["hbm_bytes_by_size_per_launch"] = b / n + bw / nw
+            out[k]["sized_requests_over_rdreq"] = round(nreq / rd, 4) if rd else None
     return out
 
 
@@ -122,7 +157,9 @@ def main(dst, *srcs):
         for k, v in summarize(src).items():
             out.setdefault(k, v)
     out = dict(sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"]))
-    json.dump({"note": "FETCH_SIZE doubled (gfx950 correction), WRITE_SIZE as reported; bytes per launch, "
+    json.dump({"note": "FETCH_SIZE doubled (gfx950 correction), WRITE_SIZE as reported; with a third pass, "
+                       "read bytes by request size (32/64/128-B TCC_EA0_RDREQ counters): hbm_bytes_by_size; "
+                       "bytes per launch, "
                        "averaged over every launch of the kernel in the profiled runs (the training leg with "
                        "the autotune cache loaded: warmup + timed steps, no tuning trials)",
                "kernels": out}, open(dst, "w"), indent=1)

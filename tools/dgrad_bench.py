@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Microbenchmark of the conv GEMM variants on C2 shapes: forward, plain data
 gradient and the fused BN-backward data gradient (kind 1 ACT, kind 3 RES with
-residual), per forced tile configuration (ARTSBIR_PGEMM_CFG)."""
+residual), per forced tile configuration (ARTSBIR_PGEMM_CFG).  Env: CFGS (candidates),
+SHAPES (indices into SHAPES)."""
 import os
 import sys
 
@@ -41,7 +42,9 @@ def timeit(fn, reps=5):
 def main():
     dev = torch.device("cuda:0")
     st = _hip.stream()
-    for (N, H, W, C, Co, R, kind, rm) in SHAPES:
+    only = os.environ.get("SHAPES")  # comma-separated indices into SHAPES (default: all)
+    sel = [SHAPES[int(i)] for i in only.split(",")] if only else SHAPES
+    for (N, H, W, C, Co, R, kind, rm) in sel:
         pad = R // 2
         G = 3
         x = torch.randn(N, H, W, Co, device=dev).bfloat16()      # dy (dgrad input, Co channels)

@@ -2,7 +2,8 @@
 # round-4 traffic measurement with the committed autotune table
 # (profiles/tune_r4.txt, loaded so a kernel name stands for the same launches
 # as in the bench): rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate
-# runs) of each leg on its own launches -> one traffic file per leg
+# runs, and a third with the read requests by size) of each leg on its own
+# launches -> one traffic file per leg
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
@@ -10,8 +11,9 @@ TC=$R/profiles/tune_r4.txt
 cd /tmp && export TMPDIR=/tmp
 for leg in train retr embed c5; do
   mkdir -p $R/gpurun_out/pmc_$leg
-  for c in FETCH_SIZE WRITE_SIZE; do
-    d=$R/gpurun_out/pmc_$leg/pmc_$( [ $c = FETCH_SIZE ] && echo fetch || echo write )
+  for c in FETCH_SIZE WRITE_SIZE REQ; do
+    d=$R/gpurun_out/pmc_$leg/pmc_$( [ $c = FETCH_SIZE ] && echo fetch || { [ $c = WRITE_SIZE ] && echo write || echo req; } )
+    [ $c = REQ ] && c="TCC_EA0_RDREQ_32B TCC_EA0_RDREQ_64B TCC_EA0_RDREQ_128B TCC_EA0_RDREQ"
     rm -rf $d
     case $leg in
       train) timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $c --output-format csv -d $d -o run -- python3 $R/bench.py --no-cpu-baseline --no-retrieval --no-embed --no-c5 --no-preprocess --no-profile --no-loss-check --steps 2 --warmup 1 --tune-cache $TC > $d.log 2>&1 ;;
