@@ -92,7 +92,8 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   const int wpx = wid & 3, wch = wid >> 2;
   const int ntc = (a.Cout + BCH - 1) / BCH;
   const long long ntp = (a.M + PP_BPX - 1) / PP_BPX;
-  const long long tile = pg_xcd_remap(blockIdx.x, ntp * ntc);  // the N tiles of a pixel panel share an XCD
+  // the N tiles of a pixel panel share an XCD (ARTSBIR_PG_DBG bit 4: dispatch order, a measurement)
+  const long long tile = (a.dbg & 4) ? (long long)blockIdx.x : pg_xcd_remap(blockIdx.x, ntp * ntc);
   const long long bpx = (tile / ntc) * PP_BPX;
   const int bch = (int)(tile % ntc) * BCH;
   const int nk = a.K / PP_KS;  // K % 32 == 0 (pp256_launch)
