@@ -284,6 +284,25 @@ __device__ __forceinline__ i32x8 f8_frag(const char* img, int row, int kq) {
 
 typedef __attribute__((ext_vector_type(4))) unsigned f8_u32x4;
 
+// epilogue stores of the fp8 GEMM: non-temporal (not allocated in L2, which
+// keeps the A panels and B slices the other column tiles re-read): the four
+// projection GEMMs 3.51 -> 3.29 ms per block, C5 forward -2.3 ms per step
+// (tools/gpu/r4_f8nt.sh, profiles/r4_nt_stores.txt)
+#ifndef F8_NT_STORE
+#define F8_NT_STORE 1
+#endif
+template <typename V>
+__device__ __forceinline__ void f8_st(V* p, const V& v) {
+  if constexpr (F8_NT_STORE) {
+    typedef unsigned f8_u2 __attribute__((ext_vector_type(2)));
+    typedef unsigned f8_u4 __attribute__((ext_vector_type(4)));
+    if constexpr (sizeof(V) == 8) __builtin_nontemporal_store(*reinterpret_cast<const f8_u2*>(&v), reinterpret_cast<f8_u2*>(p));
+    else __builtin_nontemporal_store(*reinterpret_cast<const f8_u4*>(&v), reinterpret_cast<f8_u4*>(p));
+  } else {
+    *p = v;
+  }
+}
+
 // the epilogue of four adjacent outputs of row m (offset ro, column n):
 // (+ C if accumulate) (+ res) -> C unless skip_c, and a bf16 copy to out2
 template <typename T>
@@ -309,19 +328,19 @@ __device__ __forceinline__ void f8_store_row4(T* __restrict__ C, const bf16* __r
     }
     if (!skip_c) {
       if constexpr (sizeof(T) == 4) {
-        *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+        f8_st(reinterpret_cast<float4*>(p), make_float4(v[0], v[1], v[2], v[3]));
       } else {
         bf16x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-        *reinterpret_cast<bf16x4*>(p) = o;
+        f8_st(reinterpret_cast<bf16x4*>(p), o);
       }
     }
     if (out2) {  // a bf16 copy of the result (the next LayerNorm's input / the block output)
       bf16x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-      *reinterpret_cast<bf16x4*>(out2 + ro) = o;
+      f8_st(reinterpret_cast<bf16x4*>(out2 + ro), o);
     }
   } else {
 #pragma unroll
@@ -351,8 +370,8 @@ __device__ __forceinline__ void f8_gelu_row4(T* __restrict__ C, bf16* __restrict
       go[e] = (bf16)f8_quickgelu((float)fo[e]);
       am = fmaxf(am, fabsf((float)go[e]));
     }
-    *reinterpret_cast<bf16x4*>(C + ro) = fo;
-    *reinterpret_cast<bf16x4*>(out2 + ro) = go;
+    f8_st(reinterpret_cast<bf16x4*>(C + ro), fo);
+    f8_st(reinterpret_cast<bf16x4*>(out2 + ro), go);
     return;
   }
 #pragma unroll
