@@ -76,6 +76,22 @@ __device__ __forceinline__ void pp_glds(__amdgpu_buffer_rsrc_t r, unsigned lds, 
 
 // TAPS: R x S > 1 (3x3 convolutions: the row offsets of a tile change with the
 // tap); otherwise every K-tile of a tile reads the same rows at a growing k.
+#ifndef PP_NOL
+#define PP_NOL 0  // 1: normalize-on-load cost probe of a diagnostic build only (see pp_nol2)
+#endif
+// Cost probe for a consumer-side BatchNorm + ReLU (+ padded-tap mask) on the
+// pixel fragments: relu(s * x + b) per input channel in f32, repacked to bf16,
+// with coefficients read from LDS per K-tile.  Wrong results by design (the
+// coefficients are scratch); only the kernel time is of interest.
+__device__ __forceinline__ unsigned pp_nol2(unsigned w, float s0, float s1, float b0, float b1, bool keep) {
+  float lo = __uint_as_float(w << 16), hi = __uint_as_float(w & 0xffff0000u);
+  lo = fmaxf(fmaf(lo, s0, b0), 0.f);
+  hi = fmaxf(fmaf(hi, s1, b1), 0.f);
+  const unsigned r = (unsigned)__builtin_bit_cast(unsigned short, (bf16)lo) |
+                     ((unsigned)__builtin_bit_cast(unsigned short, (bf16)hi) << 16);
+  return keep ? r : 0u;
+}
+
 template <int BK, bool TWO, bool TAPS>
 __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   constexpr int NW = PP_NW, BCH = PP_BCH;
@@ -197,6 +213,11 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   const char* bbase = smem + (wpx * WTPX + fr) * PP_ROWB + so;            // pixel fragment j: + j * 16 rows
   const char* abase = smem + PP_HALF + (wch * WTCH + fr) * PP_ROWB + so;  // channel fragment i: + i * 16 rows
   uint4 bv[NTP], af[MTC];
+#if PP_NOL
+  const char* cbase = reinterpret_cast<const char*>(red) + fq * 32;
+  unsigned nol_m = (unsigned)lane * 0x9e3779b9u;
+  asm volatile("" : "+v"(nol_m));  // opaque per-lane row-validity bits
+#endif
   // one K-tile in buffer SL (compile-time: every LDS offset an immediate)
   auto ktile = [&](int s, auto slc) {
     constexpr int SL = decltype(slc)::value;
@@ -213,9 +234,23 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
 #pragma unroll
       for (int i = 0; i < MTC / 2; ++i) af[i] = *reinterpret_cast<const uint4*>(ab + i * 16 * PP_ROWB);
     }
+#if PP_NOL
+    const f32x4 cs0 = *reinterpret_cast<const f32x4*>(cbase), cs1 = *reinterpret_cast<const f32x4*>(cbase + 16);
+    const f32x4 cb0 = *reinterpret_cast<const f32x4*>(cbase + 128), cb1 = *reinterpret_cast<const f32x4*>(cbase + 144);
+#endif
     pp_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+#if PP_NOL
+#pragma unroll
+    for (int j = 0; j < NTP; ++j) {
+      const bool keep = !TAPS || ((nol_m >> (j + 4 * SL)) & 1u);
+      bv[j].x = pp_nol2(bv[j].x, cs0[0], cs0[1], cb0[0], cb0[1], keep);
+      bv[j].y = pp_nol2(bv[j].y, cs0[2], cs0[3], cb0[2], cb0[3], keep);
+      bv[j].z = pp_nol2(bv[j].z, cs1[0], cs1[1], cb1[0], cb1[1], keep);
+      bv[j].w = pp_nol2(bv[j].w, cs1[2], cs1[3], cb1[2], cb1[3], keep);
+    }
+#endif
     PG_PRIO_ON();
 #pragma unroll
     for (int i = 0; i < MTC / 2; ++i)

@@ -25,6 +25,7 @@ NT = [  # M, N, K: C5 projection data gradients (302592 tokens) and forwards, at
 CONV = [  # N, H, W, C, Cout, R (3x3 stride 1 pad 1 forwards of C2 at 1152 images)
     (1152, 56, 56, 64, 64, 3), (1152, 28, 28, 128, 128, 3), (1152, 14, 14, 256, 256, 3), (1152, 7, 7, 512, 512, 3),
     (1152, 56, 56, 64, 256, 1), (1152, 28, 28, 512, 128, 1),
+    (1152, 28, 28, 128, 512, 1), (1152, 14, 14, 256, 1024, 1), (1152, 7, 7, 512, 2048, 1),  # bottleneck conv3
     (1152, 112, 112, 32, 64, 3), (1152, 112, 112, 32, 32, 3), (1152, 112, 112, 64, 32, 3),  # stem (and its dgrads)
 ]
 

@@ -23,6 +23,7 @@ CONV = [  # H, W (input), C, Cout, R, stride
     (28, 28, 128, 128, 3, 1),    # layer2 conv2
     (14, 14, 256, 256, 3, 1),    # layer3 conv2
     (7, 7, 512, 512, 3, 1),      # layer4 conv2
+    (56, 56, 128, 128, 3, 1),    # layer2 block-0 conv2 (before the 2x2 pool)
 ]
 DENSE = [(75648, 2304, 768), (75648, 768, 768), (75648, 3072, 768), (75648, 768, 3072)]  # M, N(out), K(in)
 
@@ -46,7 +47,7 @@ def sweep(label, fl, run, ncand):
     t = timeit(run)
     kn = _hip.lib().artsbir_last_kernel().decode()
     res = [(t, "tuned:" + kn)]
-    for c in range(ncand):
+    for c in list(range(ncand)) + [100, 101, 102]:  # then pw256 at its 3 split levels
         os.environ["ARTSBIR_WGRAD_CFG"] = str(c)
         try:
             t = timeit(run)
@@ -64,10 +65,13 @@ def sweep(label, fl, run, ncand):
 def main():
     dev = torch.device("cuda:0")
     st = _hip.stream()
-    ncand = 38  # pwgrad tile configs x split levels + the two halo kernel variants (gemm.hip tune_wgrad)
+    ncand = int(os.environ.get("NCAND", "38"))  # pwgrad tile configs x split levels + the two halo kernel variants (gemm.hip tune_wgrad)
     which = os.environ.get("WHICH", "conv,dense")
     if "conv" in which:
-        for (H, W, C, Co, R, s) in CONV:
+        only = os.environ.get("SHAPES")
+        for ci, (H, W, C, Co, R, s) in enumerate(CONV):
+            if only and str(ci) not in only.split(","):
+                continue
             pad = R // 2
             Ho, Wo = H // s, W // s
             x = torch.randn(B, H, W, C, device=dev).bfloat16()
