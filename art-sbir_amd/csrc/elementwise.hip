@@ -124,9 +124,31 @@ __global__ void bn_finalize_kernel(const float* __restrict__ stats, int C, doubl
 // Slot sums of a BN site: 4 lanes per channel add 8 of the ARTSBIR_NSLOT
 // replica slots each (16 independent loads in flight per lane instead of a
 // 32-long dependent chain per channel), the quarters combined in fixed order
-// through LDS; segments FIN_SEGS at a time.  grid ceil(C / 64), 256 threads.
-constexpr int FIN_CPB = 64, FIN_Q = 4, FIN_SEGS = 8;
+// by lane shuffles; segments FIN_SEGS at a time.  grid ceil(C / 64), 256
+// threads: lanes 4i..4i+3 of wave w hold the quarters of channel 16w + i.
+// No LDS, so the kernel co-resides with the LDS-heavy weight-gradient
+// workgroups of the side stream instead of waiting for a CU to drain (the
+// backward's finalizes took ~60 us each behind them, the forward's 6 us).
+constexpr int FIN_CPB = 64, FIN_Q = 4, FIN_SEGS = 4;
 static_assert(ARTSBIR_NSLOT % FIN_Q == 0, "slot quarters");
+
+__device__ __forceinline__ int fin_channel() {
+  return blockIdx.x * FIN_CPB + (threadIdx.x >> 6) * 16 + ((threadIdx.x & 63) >> 2);
+}
+
+// the four quarters of this lane's channel, added in quarter order (the same
+// f64 order as a sequential sum over the quarters); every lane must call it
+__device__ __forceinline__ void fin_combine(double& s1, double& s2) {
+  const int b = (threadIdx.x & 63) & ~3;
+  double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+  for (int u = 0; u < FIN_Q; ++u) {
+    t1 += __shfl(s1, b + u, 64);
+    t2 += __shfl(s2, b + u, 64);
+  }
+  s1 = t1;
+  s2 = t2;
+}
 
 __device__ __forceinline__ void fin_quarter(const float* __restrict__ st, long long C, int c, int q, double& s1,
                                             double& s2) {
@@ -156,33 +178,27 @@ __global__ void __launch_bounds__(256) bn_finalize_seg_kernel(const float* __res
                                                               const float* gamma, const float* beta, float* rmean,
                                                               float* rvar, long long* nbt, float momentum, float eps,
                                                               int train, float* __restrict__ out) {
-  __shared__ double red[FIN_SEGS][FIN_Q][2][FIN_CPB];
-  const int cl = threadIdx.x & (FIN_CPB - 1), q = threadIdx.x / FIN_CPB;
-  const int c = blockIdx.x * FIN_CPB + cl;
+  const int c = fin_channel(), q = threadIdx.x & 3;
   if (blockIdx.x == 0 && threadIdx.x == 0 && train && nbt) nbt[0] += nseg;
   for (int s0 = 0; s0 < nseg; s0 += FIN_SEGS) {
     const int ns = nseg - s0 < FIN_SEGS ? nseg - s0 : FIN_SEGS;
-    if (train && c < C) {
-      for (int s = 0; s < ns; ++s) {
-        double a, b;
-        fin_quarter(stats + (long long)(s0 + s) * seg_stride, C, c, q, a, b);
-        red[s][q][0][cl] = a;
-        red[s][q][1][cl] = b;
-      }
+    double r1[FIN_SEGS], r2[FIN_SEGS];
+#pragma unroll
+    for (int s = 0; s < FIN_SEGS; ++s) {
+      r1[s] = 0.0;
+      r2[s] = 0.0;
+      if (train && s < ns && c < C) fin_quarter(stats + (long long)(s0 + s) * seg_stride, C, c, q, r1[s], r2[s]);
     }
-    __syncthreads();
+    if (train) {
+#pragma unroll
+      for (int s = 0; s < FIN_SEGS; ++s) fin_combine(r1[s], r2[s]);
+    }
     if (q == 0 && c < C) {
       for (int s = 0; s < ns; ++s) {
         double mean, var;
         if (train) {
-          double s1 = 0, s2 = 0;
-#pragma unroll
-          for (int u = 0; u < FIN_Q; ++u) {
-            s1 += red[s][u][0][cl];
-            s2 += red[s][u][1][cl];
-          }
-          mean = s1 / count;
-          var = s2 / count - mean * mean;
+          mean = r1[s] / count;
+          var = r2[s] / count - mean * mean;
           if (var < 0) var = 0;
           if (rmean) rmean[c] = (float)((1.0 - momentum) * rmean[c] + momentum * mean);
           if (rvar) rvar[c] = (float)((1.0 - momentum) * rvar[c] + momentum * var * count / (count > 1 ? count - 1 : 1));
@@ -199,7 +215,6 @@ __global__ void __launch_bounds__(256) bn_finalize_seg_kernel(const float* __res
         o[3 * C + c] = beta[c];
       }
     }
-    __syncthreads();
   }
 }
 
@@ -767,37 +782,28 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_seg_kernel(const float* _
                                                                   const float* gamma, const float* istd,
                                                                   long long istd_stride, float* dgamma, float* dbeta,
                                                                   float* coef) {
-  __shared__ double red[FIN_SEGS][FIN_Q][2][FIN_CPB];
-  const int cl = threadIdx.x & (FIN_CPB - 1), q = threadIdx.x / FIN_CPB;
-  const int c = blockIdx.x * FIN_CPB + cl;
+  const int c = fin_channel(), q = threadIdx.x & 3;
   for (int s0 = 0; s0 < nseg; s0 += FIN_SEGS) {
     const int ns = nseg - s0 < FIN_SEGS ? nseg - s0 : FIN_SEGS;
-    if (c < C) {
-      for (int s = 0; s < ns; ++s) {
-        double a, b;
-        fin_quarter(slots + (long long)(s0 + s) * seg_stride, C, c, q, a, b);
-        red[s][q][0][cl] = a;
-        red[s][q][1][cl] = b;
-      }
+    double r1[FIN_SEGS], r2[FIN_SEGS];
+#pragma unroll
+    for (int s = 0; s < FIN_SEGS; ++s) {
+      r1[s] = 0.0;
+      r2[s] = 0.0;
+      if (s < ns && c < C) fin_quarter(slots + (long long)(s0 + s) * seg_stride, C, c, q, r1[s], r2[s]);
     }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < FIN_SEGS; ++s) fin_combine(r1[s], r2[s]);
     if (q == 0 && c < C) {
       for (int s = 0; s < ns; ++s) {
-        double s1 = 0, s2 = 0;
-#pragma unroll
-        for (int u = 0; u < FIN_Q; ++u) {
-          s1 += red[s][u][0][cl];
-          s2 += red[s][u][1][cl];
-        }
-        if (dbeta) dbeta[c] += (float)s1;
-        if (dgamma) dgamma[c] += (float)s2;
+        if (dbeta) dbeta[c] += (float)r1[s];
+        if (dgamma) dgamma[c] += (float)r2[s];
         float* co = coef + (long long)(s0 + s) * 3 * C;
         co[c] = gamma[c] * istd[(long long)(s0 + s) * istd_stride + c];
-        co[C + c] = (float)(s1 / count);
-        co[2 * C + c] = (float)(s2 / count);
+        co[C + c] = (float)(r1[s] / count);
+        co[2 * C + c] = (float)(r2[s] / count);
       }
     }
-    __syncthreads();
   }
 }
 

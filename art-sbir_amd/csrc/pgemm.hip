@@ -742,10 +742,18 @@ struct HcGeom {
                                 (160 * 1024) / (FIX + 2 * HB) && NB <= 31;
   static constexpr int NBUF = THREE ? 3 : 2;
   static constexpr int LDS = WB + NBUF * HB + PRM + pg_red_bytes<COUT>();
+  // waves per SIMD the registers must allow for every workgroup the LDS admits
+  // to fit on a CU (5 waves each: 4 compute + the loader), at most 3 (168
+  // VGPRs: below that the tiles spill).  Without it the 32 -> 32 stem tile
+  // (216 VGPRs, LDS for two workgroups) ran one workgroup per CU: one compute
+  // wave per SIMD.
+  static constexpr int WPB = (160 * 1024) / LDS > 4 ? 4 : (160 * 1024) / LDS;
+  static constexpr int WPE = (5 * WPB + 3) / 4 > 3 ? 3 : (5 * WPB + 3) / 4;
 };
 
 template <int C, int COUT, int TR, int TC, bool BNB>
-__global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
+__global__ void __launch_bounds__(320) __attribute__((amdgpu_waves_per_eu(HcGeom<C, COUT, TR, TC>::WPE)))
+hconv_kernel(PgArgs a, int ntiles) {
   using Gm = HcGeom<C, COUT, TR, TC>;
   constexpr int NWC = Gm::NWC, PB = Gm::PB, NKK = Gm::NKK, MTC = Gm::MTC, NP = Gm::NP;
   constexpr int TCB = Gm::TCB, NTP = Gm::NTP, HW = Gm::HW, NQ = Gm::NQ, NB = Gm::NB, HB = Gm::HB;
@@ -882,7 +890,8 @@ __global__ void __launch_bounds__(320) hconv_kernel(PgArgs a, int ntiles) {
       for (int j = 0; j < NTP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     constexpr int KPT = C / 32;  // 32-k steps per tap
     // taps fully unrolled where the registers allow (no spills), else by rows
-    constexpr int TUN = (NTP <= 2 || (C == 32 && MTC * NTP <= 8)) ? 9 : 3;
+    // (by rows also where the waves-per-SIMD bound leaves too few registers)
+    constexpr int TUN = ((NTP <= 2 || (C == 32 && MTC * NTP <= 8)) && !(Gm::WPE >= 3 && NTP > 2)) ? 9 : 3;
 #pragma unroll TUN
     for (int t = 0; t < 9; ++t) {
       const int toff = (t / 3) * HW + (t % 3);

@@ -350,8 +350,8 @@ __device__ __forceinline__ pw_v4s hw_tr(const char* base, int off) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((pw_lds_v4s)(pw_lds_t)(base + off));
 }
 
-template <int CT, int OT, int TR, int NWC>
-__global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int ntiles, int npc) {
+template <int CT, int OT, int TR, int NWC, bool DL>
+__global__ void __launch_bounds__(64 * (NWC + (DL ? 1 : 0))) hwgrad_kernel(PwArgs a, int ntiles, int npc) {
   using Gm = HwGeom<CT, OT, TR, NWC>;
   constexpr int TC = Gm::TC, NPX = Gm::NPX, HW = Gm::HW, NQ = Gm::NQ;
   constexpr int SX = Gm::SX, SD = Gm::SD, XI = Gm::XI, DI = Gm::DI, XB = Gm::XB, STAGE = Gm::STAGE;
@@ -371,6 +371,10 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int nt
 
   // operands of tile t -> stage buf (loader wave): lane l of DMA instruction
   // g moves bytes g * 1024 + 16 l .. + 15 of the row-major image
+  // DL: the loader wave issues every piece; otherwise compute wave w issues
+  // pieces w, w + NWC, ... of each image
+  constexpr int LS = DL ? 1 : NWC;
+  const int l0 = DL ? 0 : wid;
   auto issue = [&](int t, int buf) {
     const int img = t / (nth * ntw), rem = t - img * (nth * ntw);
     const int h0 = (rem / ntw) * TR, w0 = (rem - (rem / ntw) * ntw) * TC;
@@ -379,7 +383,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int nt
     const __amdgpu_buffer_rsrc_t xr =
         pw_rsrc(reinterpret_cast<const bf16*>(a.x) + (long long)img * a.sN, (a.x_elems - (long long)img * a.sN) * 2);
 #pragma unroll 4
-    for (int g = 0; g < XI; ++g) {
+    for (int g = l0; g < XI; g += LS) {
       const int b = g * 1024 + lane * 16;
       const int q = b / SX, ci = (b - (b / SX) * SX) >> 1;
       const int hr = q / HW, hc = q - (q / HW) * HW;
@@ -391,7 +395,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int nt
     const __amdgpu_buffer_rsrc_t dr =
         pw_rsrc(reinterpret_cast<const bf16*>(a.dy) + pimg * a.ldd, (a.dy_elems - pimg * a.ldd) * 2);
 #pragma unroll 4
-    for (int g = 0; g < DI; ++g) {
+    for (int g = l0; g < DI; g += LS) {
       const int b = g * 1024 + lane * 16;
       const int m = b / SD, co = (b - (b / SD) * SD) >> 1;
       const int oh = h0 + m / TC, ow = w0 + m % TC;
@@ -423,7 +427,7 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int nt
   // the two roles run separate loops with one barrier per tile each (one loop
   // with a role branch would merge the accumulators of both paths and copy
   // them every tile)
-  if (wid == NWC) {
+  if (DL && wid == NWC) {
     if (grp < ntiles) issue(grp, 0);
     int k = 0;
     for (int tile = grp; tile < ntiles; tile += G, ++k) {
@@ -435,11 +439,16 @@ __global__ void __launch_bounds__(64 * (NWC + 1)) hwgrad_kernel(PwArgs a, int nt
     pw_vm_wait<0>();
     return;
   }
+  if (!DL && grp < ntiles) issue(grp, 0);
   int k = 0;
   for (int tile = grp; tile < ntiles; tile += G, ++k) {
+    if constexpr (!DL) pw_vm_wait<0>();  // this wave's pieces of tile k have landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // tile k visible; the other buffer is free
     asm volatile("" ::: "memory");
+    if constexpr (!DL) {
+      if (tile + G < ntiles) issue(tile + G, (k + 1) & 1);
+    }
     const char* xs = smem + (k & 1) * STAGE;
     const char* ds = xs + XB;
 #pragma unroll 1
@@ -498,7 +507,7 @@ static bool hwgrad_ok(const PwArgs& a) {
   return nt < 0x7fffffffLL;
 }
 
-template <int CT, int OT, int TR, int NWC>
+template <int CT, int OT, int TR, int NWC, bool DL>
 static void hwgrad_go(const PwArgs& a, hipStream_t st) {
   using Gm = HwGeom<CT, OT, TR, NWC>;
   const int ntiles = (int)((a.M / ((long long)a.Ho * a.Wo)) * ((a.Ho + TR - 1) / TR) * ((a.Wo + 15) / 16));
@@ -510,22 +519,50 @@ static void hwgrad_go(const PwArgs& a, hipStream_t st) {
   if (groups < 8) groups = 8;
   const int need = (ntiles + 7) / 8 * 8;
   if (groups > need) groups = need;
-  hipLaunchKernelGGL((hwgrad_kernel<CT, OT, TR, NWC>), dim3(groups * npc), dim3(64 * (NWC + 1)), 0, st, a, ntiles,
-                     npc);
+  hipLaunchKernelGGL((hwgrad_kernel<CT, OT, TR, NWC, DL>), dim3(groups * npc), dim3(64 * (NWC + (DL ? 1 : 0))), 0, st,
+                     a, ntiles, npc);
 }
 
-template <int CT, int OT, int NWC>
+template <int CT, int OT, int NWC, bool DL = true>
 static void hwgrad_tiles(const PwArgs& a, hipStream_t st) {
-  if (a.Ho % 16 == 0 && a.Wo % 16 == 0) hwgrad_go<CT, OT, 16, NWC>(a, st);
-  else hwgrad_go<CT, OT, 8, NWC>(a, st);
+  if (a.Ho % 16 == 0 && a.Wo % 16 == 0) hwgrad_go<CT, OT, 16, NWC, DL>(a, st);
+  else hwgrad_go<CT, OT, 8, NWC, DL>(a, st);
 }
 
 // variant 0: the kernel below per channel class; variant 1 (64-channel tiled
 // shapes only): 4 compute waves of 9 (channel tile, tap) pairs each instead of
 // 8 waves of 4.5 (0.72 transposing LDS reads per MFMA instead of 0.9, no
-// repeated pairs; 144 accumulator registers per lane)
+// repeated pairs; 144 accumulator registers per lane).  Variants 2 / 3: the
+// same two 64-channel forms (and variant 2 for every channel class) without
+// the loader wave, the compute waves issuing the LDS-DMA pieces themselves.
+// A loader wave is allocated the compute waves' registers: at 192 VGPRs (two
+// waves per SIMD) the 4 + 1 waves of a workgroup leave no room for a second
+// workgroup on the CU, so one compute wave per SIMD hides no LDS latency;
+// without it two workgroups (two compute waves per SIMD) fit.
 static bool hwgrad_launch(const PwArgs& a, int variant, hipStream_t st) {
   if (!hwgrad_ok(a)) return false;
+  if (variant == 3) {
+    if (a.C % 64 || a.Cout % 64) return false;
+    set_last_kernel("hwgrad_kernel<64,64,nl>");
+    hwgrad_tiles<64, 64, 8, false>(a, st);
+    return true;
+  }
+  if (variant == 2) {
+    if (a.C == 32 && a.Cout == 32) {
+      set_last_kernel("hwgrad_kernel<32,32,nl>");
+      hwgrad_tiles<32, 32, 4, false>(a, st);
+    } else if (a.C == 32) {
+      set_last_kernel("hwgrad_kernel<32,64,nl>");
+      hwgrad_tiles<32, 64, 4, false>(a, st);
+    } else if (a.Cout == 32) {
+      set_last_kernel("hwgrad_kernel<64,32,nl>");
+      hwgrad_tiles<64, 32, 4, false>(a, st);
+    } else {
+      set_last_kernel("hwgrad_kernel<64,64,w4,nl>");
+      hwgrad_tiles<64, 64, 4, false>(a, st);
+    }
+    return true;
+  }
   if (variant != 0) {
     if (variant != 1 || a.C % 64 || a.Cout % 64) return false;
     set_last_kernel("hwgrad_kernel<64,64,w4>");
@@ -594,8 +631,8 @@ static const int kSplitMinSteps[] = {8, 16, 24, 64};
 constexpr int kNumLevels = 4;
 
 // candidates: kNumPw tile configurations x kNumLevels split levels, then the
-// halo-tiled kernel (two variants, see hwgrad_launch)
-int pwgrad_num_cfgs() { return kNumPw * kNumLevels + 2; }
+// halo-tiled kernel (four variants, see hwgrad_launch)
+int pwgrad_num_cfgs() { return kNumPw * kNumLevels + 4; }
 
 // split level of candidate c of the pipelined wgrad (-1: the halo kernel)
 int pwgrad_level(int c) { return c >= 0 && c < kNumPw * kNumLevels ? c / kNumPw : -1; }

@@ -147,9 +147,9 @@ WG_CASES = [
 
 
 # candidates (gemm.hip tune_wgrad): -1 register-staged kernel, c + 9 * level the
-# pipelined kernel's 9 tile shapes at 4 split levels, 36 / 37 the halo-tiled kernel variants
+# pipelined kernel's 9 tile shapes at 4 split levels, 36-39 the halo-tiled kernel variants
 @pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "16", "20", "34", "36", "37",
-                                 "auto"])
+                                 "38", "39", "auto"])
 @pytest.mark.parametrize("case", WG_CASES)
 def test_wgrad_accumulates(case, cfg, dev):
     old = os.environ.get("ARTSBIR_WGRAD_CFG")

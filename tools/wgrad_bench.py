@@ -24,6 +24,8 @@ CONV = [  # H, W (input), C, Cout, R, stride
     (14, 14, 256, 256, 3, 1),    # layer3 conv2
     (7, 7, 512, 512, 3, 1),      # layer4 conv2
     (56, 56, 128, 128, 3, 1),    # layer2 block-0 conv2 (before the 2x2 pool)
+    (112, 112, 32, 32, 3, 1),    # stem conv2
+    (112, 112, 32, 64, 3, 1),    # stem conv3
 ]
 DENSE = [(75648, 2304, 768), (75648, 768, 768), (75648, 3072, 768), (75648, 768, 3072)]  # M, N(out), K(in)
 
@@ -65,7 +67,7 @@ def sweep(label, fl, run, ncand):
 def main():
     dev = torch.device("cuda:0")
     st = _hip.stream()
-    ncand = int(os.environ.get("NCAND", "38"))  # pwgrad tile configs x split levels + the two halo kernel variants (gemm.hip tune_wgrad)
+    ncand = int(os.environ.get("NCAND", "40"))  # pwgrad tile configs x split levels + the four halo kernel variants (gemm.hip tune_wgrad)
     which = os.environ.get("WHICH", "conv,dense")
     if "conv" in which:
         only = os.environ.get("SHAPES")
