@@ -295,7 +295,10 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
 
   const long long seg0 = a.seg_m > 0 ? bpx / a.seg_m : 0;
   EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
-  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 2, true>(a, acc, bpx, bch, wpx, wch, fr,
+#ifndef PP_EJB
+#define PP_EJB 4  // pixel tiles whose epilogue operands are loaded together (2: 1-4 % slower fused dgrads, tools/gpu/r4_ej.sh)
+#endif
+  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, PP_EJB, true>(a, acc, bpx, bch, wpx, wch, fr,
                                                                                         fq, red, sgg);
   if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, (int)(blockIdx.x % ARTSBIR_NSLOT), lane, bpx, PP_BPX);
 }
