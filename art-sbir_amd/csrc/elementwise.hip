@@ -457,9 +457,15 @@ __global__ void __launch_bounds__(256) block_out_cg_kernel(const T* __restrict__
 }
 
 // units per workgroup so that a launch has ~2048 workgroups over all segments
+// the same workgroup sizing as the BN-backward apply (launch_bnb): ~16384
+// workgroups, at least 8 unit rows each (ARTSBIR_CG_WGS / ARTSBIR_CG_MINROWS:
+// other targets, measurement knobs; round 3 used 2048 and 1)
 static int cg_units_per_block(long long units, int nseg, int C) {
+  static const int wgs = getenv("ARTSBIR_CG_WGS") ? atoi(getenv("ARTSBIR_CG_WGS")) : 16384;
+  static const int min_rows = getenv("ARTSBIR_CG_MINROWS") ? atoi(getenv("ARTSBIR_CG_MINROWS")) : 8;
   const int RL = 256 / (C / 8);
-  long long upb = (units * nseg + 2047) / 2048;
+  long long upb = (units * nseg + wgs - 1) / wgs;
+  if (upb < (long long)min_rows * RL) upb = (long long)min_rows * RL;
   if (upb < RL) upb = RL;
   return (int)upb;
 }
@@ -1224,9 +1230,18 @@ static void launch_bnb(const BnBwdArgs& a, int nseg, bool reduce, hipStream_t st
   }
   const int units = a.B * (a.H / P) * (a.W / P);
   const int RL = 256 / (a.C / 8);
-  // ~2048 workgroups over all segments, each walking a contiguous range of units
-  int upb = (units * nseg + 2047) / 2048;
+  // workgroups over all segments, each walking a contiguous range of units.
+  // The reduction: ~2048 (each adds one atomic per channel).  The apply: ~16384
+  // but at least 8 unit rows per workgroup, so small shapes keep whole trips
+  // (tools/apply_bench.py: the large shapes stream 5.0 TB/s at 2048 workgroups
+  // and 5.1-5.6 at 16384, the 7^2 ones lose half their rate with one trip
+  // each).  ARTSBIR_BNB_WGS / ARTSBIR_BNB_MINROWS: other targets, measurement knobs.
+  static const int wgs_apply = getenv("ARTSBIR_BNB_WGS") ? atoi(getenv("ARTSBIR_BNB_WGS")) : 16384;
+  static const int min_rows = getenv("ARTSBIR_BNB_MINROWS") ? atoi(getenv("ARTSBIR_BNB_MINROWS")) : 8;
+  const int wgs = reduce ? 2048 : wgs_apply;
+  int upb = (units * nseg + wgs - 1) / wgs;
   if (upb < RL) upb = RL;
+  if (!reduce && upb < min_rows * RL) upb = min_rows * RL;
   const unsigned grid = (unsigned)((units + upb - 1) / upb);
 #define BNB_LAUNCH(K, PP)                                                                                     \
   do {                                                                                                       \
