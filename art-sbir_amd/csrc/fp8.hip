@@ -112,7 +112,27 @@ __global__ void __launch_bounds__(256) fp8_quant_kernel(const T* __restrict__ x,
   const float sc = amax > 0.f ? amax / 448.f : 1.f;  // x / s, correctly rounded (as the documented formula)
   const float rs = 1.f / sc;
   const long long n8 = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(q)) & 15) ? 0 : n / 8;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n8; i += gridDim.x * 256LL) {
+  const long long G = gridDim.x * 256LL;
+  long long i = blockIdx.x * 256LL + threadIdx.x;
+  // QU chunks per trip, every load of the trip issued before the first
+  // conversion: one 16-B load in flight per lane left the pass latency-bound
+  constexpr int QU = 4;
+  for (; i + (QU - 1) * G < n8; i += QU * G) {
+    float v[QU][8];
+#pragma unroll
+    for (int u = 0; u < QU; ++u) fp8_load8(x + (i + u * G) * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < QU; ++u) {
+      unsigned lo = 0, hi = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        lo |= fp8_e4m3_rne(fp8_div(v[u][e], sc, rs)) << (8 * e);
+        hi |= fp8_e4m3_rne(fp8_div(v[u][4 + e], sc, rs)) << (8 * e);
+      }
+      *reinterpret_cast<uint2*>(q + (i + u * G) * 8) = make_uint2(lo, hi);
+    }
+  }
+  for (; i < n8; i += G) {
     float v[8];
     fp8_load8(x + i * 8, v);
     unsigned lo = 0, hi = 0;
