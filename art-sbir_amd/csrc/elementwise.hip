@@ -456,8 +456,7 @@ __global__ void __launch_bounds__(256) block_out_cg_kernel(const T* __restrict__
   }
 }
 
-// units per workgroup so that a launch has ~2048 workgroups over all segments
-// the same workgroup sizing as the BN-backward apply (launch_bnb): ~16384
+// units per workgroup: the same workgroup sizing as the BN-backward apply (launch_bnb): ~16384
 // workgroups, at least 8 unit rows each (ARTSBIR_CG_WGS / ARTSBIR_CG_MINROWS:
 // other targets, measurement knobs; round 3 used 2048 and 1)
 static int cg_units_per_block(long long units, int nseg, int C) {
