@@ -646,13 +646,23 @@ static bool sconv_ok(const PgArgs& a) {
   return (a.M + 255) / 256 <= 0x7fffffffLL / 256;
 }
 
-// persistent grid: as many blocks as fit on the 256 CUs at once (LDS-bound)
-template <int C, int COUT>
+// persistent grid: as many blocks as fit on the 256 CUs at once — by LDS and
+// by registers (the runtime's occupancy of the kernel): an LDS-only count put
+// 4 blocks per CU where the 150-220-register forms hold 2-3, so the last
+// blocks ran their whole tile share after the others had finished
+template <int C, int COUT, int ST, bool BNB>
 static int sconv_grid(int ntiles) {
   constexpr int K = 9 * C, NKK = (K + 31) / 32;
   constexpr int lds = NKK * COUT * 64 + 2 * 3 * COUT * 4 + 16;
-  int per_cu = (160 * 1024) / lds;
-  if (per_cu > 4) per_cu = 4;  // 4 x 256 threads: 16 waves per CU
+  static const int per_cu = [] {
+    int n = (160 * 1024) / lds;
+    if (n > 4) n = 4;  // 4 x 256 threads: 16 waves per CU
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, sconv_kernel<C, COUT, ST, BNB>, 256, 0) == hipSuccess &&
+        occ >= 1 && occ < n)
+      n = occ;
+    return n;
+  }();
   const int g = 256 * per_cu;
   return ntiles < g ? ntiles : g;
 }
@@ -661,19 +671,19 @@ template <bool BNB>
 static bool sconv_dispatch(const PgArgs& a, int ntiles, hipStream_t st) {
   if (a.stride == 1 && a.C == 32 && a.Cout == 32) {
     set_last_kernel(BNB ? "sconv_kernel<32,32,bnb>" : "sconv_kernel<32,32>");
-    hipLaunchKernelGGL((sconv_kernel<32, 32, 1, BNB>), dim3(sconv_grid<32, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
+    hipLaunchKernelGGL((sconv_kernel<32, 32, 1, BNB>), dim3(sconv_grid<32, 32, 1, BNB>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 1 && a.C == 32 && a.Cout == 64) {
     set_last_kernel(BNB ? "sconv_kernel<32,64,bnb>" : "sconv_kernel<32,64>");
-    hipLaunchKernelGGL((sconv_kernel<32, 64, 1, BNB>), dim3(sconv_grid<32, 64>(ntiles)), dim3(256), 0, st, a, ntiles);
+    hipLaunchKernelGGL((sconv_kernel<32, 64, 1, BNB>), dim3(sconv_grid<32, 64, 1, BNB>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 1 && a.C == 64 && a.Cout == 32) {
     set_last_kernel(BNB ? "sconv_kernel<64,32,bnb>" : "sconv_kernel<64,32>");
-    hipLaunchKernelGGL((sconv_kernel<64, 32, 1, BNB>), dim3(sconv_grid<64, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
+    hipLaunchKernelGGL((sconv_kernel<64, 32, 1, BNB>), dim3(sconv_grid<64, 32, 1, BNB>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 1 && a.C == 64 && a.Cout == 64) {
     set_last_kernel(BNB ? "sconv_kernel<64,64,bnb>" : "sconv_kernel<64,64>");
-    hipLaunchKernelGGL((sconv_kernel<64, 64, 1, BNB>), dim3(sconv_grid<64, 64>(ntiles)), dim3(256), 0, st, a, ntiles);
+    hipLaunchKernelGGL((sconv_kernel<64, 64, 1, BNB>), dim3(sconv_grid<64, 64, 1, BNB>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else if (a.stride == 2 && a.C == 8 && a.Cout == 32) {
     set_last_kernel(BNB ? "sconv_kernel<8,32,s2,bnb>" : "sconv_kernel<8,32,s2>");
-    hipLaunchKernelGGL((sconv_kernel<8, 32, 2, BNB>), dim3(sconv_grid<8, 32>(ntiles)), dim3(256), 0, st, a, ntiles);
+    hipLaunchKernelGGL((sconv_kernel<8, 32, 2, BNB>), dim3(sconv_grid<8, 32, 2, BNB>(ntiles)), dim3(256), 0, st, a, ntiles);
   } else {
     return false;
   }
