@@ -133,6 +133,12 @@ struct ConvArgs {
   int nseg;                 // BN segments (separate reference forward calls) of equal size
   const void* bnb_desc;     // artsbir_bn_bwd_desc of a fused BN-backward reduction (dgrad)
   long long bnb_pstride;    // floats between the BN parameters of consecutive segments
+  // the folded BatchNorm backward of artsbir_conv1x1_dgrad_fold (PgArgs: same
+  // fields); only the pipelined bf16 kernels take it
+  const void* x2 = nullptr;
+  long long x2_elems = 0, sN2 = 0, sH2 = 0, sW2 = 0;
+  int C1 = 0;
+  long long w_sstride = 0, bias_sstride = 0;
 };
 
 template <typename T, int BM, int BN, bool UNIFORM_TAP, bool AFFINE>
@@ -774,7 +780,7 @@ static int run_old(const ConvArgs& a, hipStream_t st) {
 }
 
 static bool run_candidate(int c, const ConvArgs& a, const PgArgs& p, hipStream_t st) {
-  if (c == -2) return a.res_mode != 3 && run_old<bf16>(a, st) == 0;
+  if (c == -2) return a.res_mode != 3 && !a.x2 && run_old<bf16>(a, st) == 0;
   return pgemm_launch_cfg(p, c, st);
 }
 
@@ -843,6 +849,8 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     p.Ho = a.Ho; p.Wo = a.Wo; p.w = a.w; p.Cout = a.Cout; p.K = a.K; p.M = a.M;
     p.y = a.y; p.ldy = a.ldy; p.stats = a.stats; p.res = a.res; p.res_mode = a.res_mode;
     p.bias = a.bias; p.relu = a.relu;
+    p.x2 = a.x2; p.x2_elems = a.x2_elems; p.sN2 = a.sN2; p.sH2 = a.sH2; p.sW2 = a.sW2; p.C1 = a.C1;
+    p.w_sstride = a.w_sstride; p.bias_sstride = a.bias_sstride;
     {
       static const int dbg = getenv("ARTSBIR_PG_DBG") ? atoi(getenv("ARTSBIR_PG_DBG")) : 0;
       p.dbg = dbg;
@@ -868,7 +876,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
       choice = atoi(force ? force : force_bnb);
     } else {
       const ConvKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.Ho, a.Wo, a.res_mode,
-                        (a.stats ? 1 : 0) | (a.bias ? 2 : 0) | (a.relu ? 4 : 0), a.nseg,
+                        (a.stats ? 1 : 0) | (a.bias ? 2 : 0) | (a.relu ? 4 : 0) | (a.x2 ? 8 : 0), a.nseg,
                         bd ? p.bnb * 4 + p.bnb_nt : 0};
       std::lock_guard<std::mutex> lk(g_tune_mu);
       auto it = g_conv_choice.find(key);
@@ -893,6 +901,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     }
   }
   if (a.res_mode == 3) { set_error("gemm_nt_gate: no kernel for this shape"); return -1; }
+  if (a.x2) return 1;  // a two-operand fold no pipelined kernel took: the caller's fallback
   return run_old<T>(a, st);
 }
 
@@ -1040,6 +1049,140 @@ static int dgrad_common(const artsbir_conv_desc* d, const void* dy, const void* 
   a.nseg = nseg; a.bnb_desc = bnb; a.bnb_pstride = pstride;
   hipStream_t st = (hipStream_t)stream;
   return d->dtype == ARTSBIR_DT_BF16 ? launch_conv<bf16>(a, st) : launch_conv<float>(a, st);
+}
+
+// ---------------------------------------------------------------------------
+// Data gradient of a 1x1 convolution with the BatchNorm backward of its output
+// folded in (artsbir.h: artsbir_conv1x1_dgrad_fold).  The reference's chain
+// conv -> BatchNorm2d (models.py:219-220 conv3 -> bn3, 227-229 downsample conv ->
+// BN) is differentiated by autograd as dy = c1 (g - c2 - xhat c3) followed by
+// dx = dy W; since y = x W^T the whole chain is linear in (g, x):
+//   dx = g (diag(c1) W) + x (W^T diag(b') W) + e,  b' = -c1 c3 istd,
+//   e = (-c1 (c2 - c3 istd mean)) W
+// per BN segment, so it runs as ONE GEMM over the concatenated reduction
+// [g | x] (K = Co + Ci) with per-segment weights (artsbir_bn_fold_bwd_prep) and
+// bias — no dy tensor is written or read.
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) fold_concat_kernel(const T* __restrict__ g, const T* __restrict__ x, T* out,
+                                                          long long M, int Co, int Ci) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int cg = (Co + Ci) / EPC;  // 16-B chunks per output row
+  const long long n = M * cg;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long m = i / cg;
+    const int c = (int)(i - m * cg) * EPC;
+    const uint4 v = c < Co ? *reinterpret_cast<const uint4*>(g + m * Co + c)
+                           : *reinterpret_cast<const uint4*>(x + m * Ci + (c - Co));
+    *reinterpret_cast<uint4*>(out + m * (Co + Ci) + c) = v;
+  }
+}
+
+static void* g_fold_ws = nullptr;  // the concatenated operand of the fallback path
+static size_t g_fold_ws_n = 0;
+
+// the segment s slice of a fused BN-backward descriptor (kind 1: the BN before the ReLU)
+static artsbir_bn_bwd_desc bnb_segment(const artsbir_bn_bwd_desc* bd, int s, long long seg_m, int C, long long pstride) {
+  artsbir_bn_bwd_desc d = *bd;
+  const long long es = bd->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+  d.nseg = 1;
+  if (bd->mask_bn) d.mask_bn = bd->mask_bn + s * pstride;
+  for (int t = 0; t < bd->ntarget; ++t) {
+    d.y[t] = reinterpret_cast<const char*>(bd->y[t]) + s * seg_m * C * es;
+    d.mean[t] = bd->mean[t] + s * pstride;
+    d.istd[t] = bd->istd[t] + s * pstride;
+    d.slots[t] = bd->slots[t] + (long long)s * ARTSBIR_NSLOT * 2 * C;
+  }
+  return d;
+}
+
+extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                                          const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                                          long long param_stride, void* stream) {
+  if (check_conv(d)) return -1;
+  if (d->R != 1 || d->S != 1 || d->stride != 1 || d->pad != 0) { set_error("conv1x1_dgrad_fold: 1x1 stride-1 convolutions only"); return -1; }
+  if (!g || !x || !w || !bias || !dx) { set_error("conv1x1_dgrad_fold: null operand"); return -1; }
+  if (d->Cout % 8 || d->C % 8) { set_error("conv1x1_dgrad_fold: channels must be multiples of 8"); return -1; }
+  if (nseg < 1 || d->N % nseg) { set_error("conv1x1_dgrad_fold: %d segments do not divide batch %d", nseg, d->N); return -1; }
+  if (bnb && (bnb->kind != 1 || bnb->ntarget != 1 || !bnb->mask_bn || bnb->pool > 1 || bnb->dtype != d->dtype)) {
+    set_error("conv1x1_dgrad_fold: the fused BN backward must be kind 1 with one target");
+    return -1;
+  }
+  const int Co = d->Cout, Ci = d->C, K = Co + Ci;
+  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
+  const bool bf = d->dtype == ARTSBIR_DT_BF16;
+  const long long es = bf ? 2 : 4;
+  hipStream_t st = (hipStream_t)stream;
+  ConvArgs a;
+  a.x = g; a.sW = Co; a.sH = (long long)d->W * Co; a.sN = (long long)d->H * d->W * Co; a.x_elems = M * Co;
+  a.x2 = x; a.sW2 = Ci; a.sH2 = (long long)d->W * Ci; a.sN2 = (long long)d->H * d->W * Ci; a.x2_elems = M * Ci;
+  a.C1 = Co;
+  a.H = d->H; a.W = d->W; a.C = K;
+  a.R = 1; a.S = 1; a.stride = 1; a.pad = 0; a.Ho = d->H; a.Wo = d->W;
+  a.in_scale = nullptr; a.in_shift = nullptr; a.in_relu = 0;
+  a.w = w; a.Cout = Ci; a.K = K; a.M = M;
+  a.y = dx; a.ldy = Ci;
+  a.out_f32 = 0; a.accumulate = 0; a.bias = bias; a.stats = nullptr;
+  a.res = nullptr; a.res_mode = 0; a.relu = 0;
+  a.nseg = nseg; a.bnb_desc = bnb; a.bnb_pstride = param_stride;
+  a.w_sstride = (long long)Ci * K; a.bias_sstride = Ci;
+  // one launch over every segment, else one per segment (the tiles of a
+  // launch then never straddle two), on the two-operand pipelined kernels
+  if (bf) {
+    int rc = launch_conv<bf16>(a, st);
+    if (rc <= 0) return rc;
+    for (int s = 0; s < nseg && rc == 0; ++s) {
+      ConvArgs p = a;
+      artsbir_bn_bwd_desc bs;
+      if (bnb) { bs = bnb_segment(bnb, s, seg_m, Ci, param_stride); p.bnb_desc = &bs; }
+      p.nseg = 1; p.M = seg_m;
+      p.x = reinterpret_cast<const bf16*>(g) + s * seg_m * Co; p.x_elems = seg_m * Co;
+      p.x2 = reinterpret_cast<const bf16*>(x) + s * seg_m * Ci; p.x2_elems = seg_m * Ci;
+      p.w = reinterpret_cast<const bf16*>(w) + s * a.w_sstride;
+      p.bias = bias + s * Ci;
+      p.y = reinterpret_cast<bf16*>(dx) + s * seg_m * Ci;
+      rc = launch_conv<bf16>(p, st);
+      if (rc < 0) return rc;
+      if (rc > 0 && s > 0) { set_error("conv1x1_dgrad_fold: segment %d has no kernel", s); return -1; }
+    }
+    if (rc == 0) return 0;
+  }
+  // f32 (the parity mode) and shapes the pipelined kernels do not take: the two
+  // operands concatenated per pixel, then one plain GEMM per segment
+  const size_t need = (size_t)(M * K * es);
+  if (need > g_fold_ws_n) {
+    if (g_fold_ws) (void)hipFree(g_fold_ws);
+    g_fold_ws = nullptr;
+    g_fold_ws_n = 0;
+    if (hipMalloc(&g_fold_ws, need) != hipSuccess) { set_error("conv1x1_dgrad_fold: workspace of %zu bytes", need); return -1; }
+    g_fold_ws_n = need;
+  }
+  {
+    const long long n = M * (K * es / 16);
+    const unsigned grid = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+    if (bf)
+      hipLaunchKernelGGL(fold_concat_kernel<bf16>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const bf16*>(g),
+                         reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(g_fold_ws), M, Co, Ci);
+    else
+      hipLaunchKernelGGL(fold_concat_kernel<float>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(g),
+                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(g_fold_ws), M, Co, Ci);
+    ARTSBIR_CHECK_LAUNCH("fold_concat");
+  }
+  for (int s = 0; s < nseg; ++s) {
+    ConvArgs p = a;
+    artsbir_bn_bwd_desc bs;
+    if (bnb) { bs = bnb_segment(bnb, s, seg_m, Ci, param_stride); p.bnb_desc = &bs; }
+    p.x2 = nullptr; p.C1 = 0; p.w_sstride = 0; p.bias_sstride = 0;
+    p.nseg = 1; p.M = seg_m;
+    p.x = reinterpret_cast<const char*>(g_fold_ws) + s * seg_m * K * es; p.x_elems = seg_m * K;
+    p.sW = K; p.sH = (long long)d->W * K; p.sN = (long long)d->H * d->W * K;
+    p.w = reinterpret_cast<const char*>(w) + s * a.w_sstride * es;
+    p.bias = bias + s * Ci;
+    p.y = reinterpret_cast<char*>(dx) + s * seg_m * Ci * es;
+    const int rc = bf ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
+    if (rc) return -1;
+  }
+  return 0;
 }
 
 extern "C" int artsbir_gemm_nt(int dtype, long long M, int N, int K, const void* a, long long lda,

@@ -38,6 +38,18 @@ struct PgArgs {
   const void* bnb_mask;   // bnb 2: the ReLU output (block output)
   float* bnb_slots[2];
   long long bnb_pstride;  // floats between the per-channel parameters of consecutive segments
+  // BatchNorm backward folded into a 1x1 data gradient (artsbir_conv1x1_dgrad_fold):
+  // the reduction operand is two tensors, k < C1 from x (C1 channels, strides
+  // sN/sH/sW) and k >= C1 from x2 (C - C1 channels, strides sN2/sH2/sW2); the
+  // weights and the bias differ per BN segment (w + seg * w_sstride elements,
+  // bias + seg * bias_sstride floats) — kernels taking it never let a tile
+  // straddle two segments
+  const void* x2 = nullptr;  // nullptr: one operand
+  long long x2_elems = 0;
+  long long sN2 = 0, sH2 = 0, sW2 = 0;
+  int C1 = 0;
+  long long w_sstride = 0;
+  long long bias_sstride = 0;
 };
 
 // Weight gradient dW[co][k] += sum_m dY[m][co] * Xcol[m][k] (pwgrad.hip).
@@ -76,6 +88,16 @@ bool pgemm_launch_cfg(const PgArgs& a, int cfg, hipStream_t st);
 // workgroup / persistent over 256 workgroups; false when the shape or epilogue
 // is outside it (C % 32 != 0, LDS-staged operands).
 bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st);
+// whether a launch with a two-operand reduction / per-segment weights can be
+// taken by a tile of BPX pixels (1x1 only, C1 a whole number of KS-k stages,
+// segments a whole number of tiles)
+inline bool pg_fold_ok(const PgArgs& a, int bpx, int ks) {
+  if (!a.x2 && !a.w_sstride) return true;
+  if (a.R != 1 || a.S != 1 || a.stride != 1 || a.pad != 0) return false;
+  if (a.x2 && (a.C1 <= 0 || a.C1 % ks != 0 || a.C1 >= a.C || (a.C - a.C1) % 8 != 0)) return false;
+  if ((a.w_sstride || a.bias_sstride) && a.seg_m > 0 && a.seg_m % bpx != 0) return false;
+  return true;
+}
 // Heuristic candidate for a shape (-1: unsupported).
 int pgemm_default_cfg(const PgArgs& a);
 

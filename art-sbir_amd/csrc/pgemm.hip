@@ -46,8 +46,11 @@ namespace artsbir {
 // constants straight from global memory (no LDS staging, no parameter table),
 // so the LDS is the stage ring alone and several workgroups share a CU: one's
 // epilogue streams while another's main loop runs
+// X2 (1x1 only): the BatchNorm-backward fold of artsbir_conv1x1_dgrad_fold — the
+// reduction runs over two operands (k < C1 from x, the rest from x2), the
+// weights and the bias are those of the tile's BN segment
 template <int BPX, int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, int BK, bool TWO, bool PF = false, int KS = 64,
-          bool GLB = false>
+          bool GLB = false, bool X2 = false>
 __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3) : 1) pgemm_kernel(PgArgs a) {
   constexpr bool BNB = BK != 0;
   static_assert(!GLB || !PF, "GLB: operands from global memory, not prefetched into registers");
@@ -88,13 +91,16 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
   const long long img0 = bpx / HoWo;
   const __amdgpu_buffer_rsrc_t xr =
       pg_rsrc(reinterpret_cast<const bf16*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * 2);
-  const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
+  const __amdgpu_buffer_rsrc_t xr2 =
+      X2 ? pg_rsrc(reinterpret_cast<const bf16*>(a.x2) + img0 * a.sN2, (a.x2_elems - img0 * a.sN2) * 2) : xr;
+  const __amdgpu_buffer_rsrc_t wr =
+      pg_rsrc(reinterpret_cast<const bf16*>(a.w) + (X2 ? seg0 * a.w_sstride : 0), (long long)a.Cout * a.K * 2);
 
   // ---- loader decode: this lane fills slot (lane & 7) of row (lane >> 3)
   // of each 8-row wave instruction, with k-chunk csrc = slot ^ (row & 7)
   const int lrow = lane / CPR, lslot = lane % CPR;
   const int csrc = KS == 64 ? (lslot ^ lrow) : (lslot ^ ((lrow >> 2) & 2));
-  int rowoff[IPX];
+  int rowoff[IPX], rowoff2[X2 ? IPX : 1];
   unsigned rmask[IPX];
 #pragma unroll
   for (int u = 0; u < IPX; ++u) {
@@ -107,6 +113,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
     const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
     const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
     rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2);
+    if constexpr (X2) rowoff2[u] = (int)(((img - img0) * a.sN2 + (long long)oh * a.sH2 + (long long)ow * a.sW2) * 2);
     unsigned msk = 0;
     for (int r = 0; r < a.R; ++r)
       for (int s = 0; s < a.S; ++s) {
@@ -130,9 +137,15 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
     char* chs = pxs + PXB;
     int rs, tapoff;
     bool kval;
+    bool src2 = false;  // X2: this stage's k lie in the second operand
     if constexpr (!MULTI) {
       rs = u_r * a.S + u_s;
-      tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + u_ci + csrc * 8) * 2;
+      int ci = u_ci;
+      if constexpr (X2) {
+        src2 = u_ci >= a.C1;
+        if (src2) ci -= a.C1;
+      }
+      tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + ci + csrc * 8) * 2;
       kval = true;
       u_ci += KS;
       if (u_ci == a.C) {
@@ -151,7 +164,12 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
 #pragma unroll
     for (int u = 0; u < IPX; ++u) {
       const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
-      glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+      if constexpr (X2) {
+        if (src2) glds16(xr2, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff2[u] + tapoff) : PG_OOB);
+        else glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+      } else {
+        glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+      }
     }
     const bool wk = kt * KS + csrc * 8 < a.K;
 #pragma unroll
@@ -235,8 +253,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
   if constexpr (GLB) {
     const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
     EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
-    pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true>(a, acc, bpx, bch, wpx, wch,
-                                                                                          fr, fq, red, sgg);
+    pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true, X2>(a, acc, bpx, bch, wpx,
+                                                                                              wch, fr, fq, red, sgg);
     if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
     return;
   }
@@ -280,7 +298,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
     __syncthreads();
   }
   const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
-  pg_epilogue_k<BK, TWO, S_RES, S_Y1, S_MK, BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, red, sg);
+  pg_epilogue_k<BK, TWO, S_RES, S_Y1, S_MK, BCH, MTC, NTP, WTPX, WTCH, false, 2, false, X2>(a, acc, bpx, bch, wpx, wch,
+                                                                                            fr, fq, red, sg);
   if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
 }
 
@@ -301,8 +320,9 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
 // loader waves already stream the next tile's stages
 // KS: k per stage as in pgemm_kernel (32: 64-B LDS rows, twice the stages in
 // the same LDS, uniform taps only)
+// X2: the two-operand / per-segment-weight fold of pgemm_kernel (1x1 only)
 template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS, int BK = 0, bool TWO = false,
-          int KS = 64>
+          int KS = 64, bool X2 = false>
 __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int BPX = 256, NWC = 8, NWL = 4;
   static_assert(WPX * WCH == NWC, "compute waves");
@@ -334,9 +354,9 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
     const int lw = wid - NWC;
     const int lrow = lane / CPR, lslot = lane % CPR;
     const int csrc = KS == 64 ? (lslot ^ lrow) : (lslot ^ ((lrow >> 2) & 2));
-    const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
-    __amdgpu_buffer_rsrc_t xr = wr;
-    int rowoff[LPX];
+    __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
+    __amdgpu_buffer_rsrc_t xr = wr, xr2 = wr;
+    int rowoff[LPX], rowoff2[X2 ? LPX : 1];
     unsigned rmask[LPX];
     unsigned woff[LCH];
     int u_ci = 0, u_s = 0, u_r = 0;
@@ -346,6 +366,11 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       const int bch = (int)(t % ntc) * BCH;
       const long long img0 = bpx / HoWo;
       xr = pg_rsrc(reinterpret_cast<const bf16*>(a.x) + img0 * a.sN, (a.x_elems - img0 * a.sN) * 2);
+      if constexpr (X2) {
+        xr2 = pg_rsrc(reinterpret_cast<const bf16*>(a.x2) + img0 * a.sN2, (a.x2_elems - img0 * a.sN2) * 2);
+        const long long sg = a.seg_m > 0 ? bpx / a.seg_m : 0;
+        wr = pg_rsrc(reinterpret_cast<const bf16*>(a.w) + sg * a.w_sstride, (long long)a.Cout * a.K * 2);
+      }
 #pragma unroll
       for (int u = 0; u < LPX; ++u) {
         const int row = (u * NWL + lw) * RPI + lrow;
@@ -357,6 +382,8 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
         const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
         const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
         rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2);
+        if constexpr (X2)
+          rowoff2[u] = (int)(((img - img0) * a.sN2 + (long long)oh * a.sH2 + (long long)ow * a.sW2) * 2);
         unsigned msk = 0;
         for (int r = 0; r < a.R; ++r)
           for (int s = 0; s < a.S; ++s) {
@@ -379,9 +406,15 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       char* chs = pxs + PXB;
       int rs, tapoff;
       bool kval;
+      bool src2 = false;
       if constexpr (!MULTI) {
         rs = u_r * a.S + u_s;
-        tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + u_ci + csrc * 8) * 2;
+        int ci = u_ci;
+        if constexpr (X2) {
+          src2 = u_ci >= a.C1;
+          if (src2) ci -= a.C1;
+        }
+        tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + ci + csrc * 8) * 2;
         kval = true;
         u_ci += KS;
         if (u_ci == a.C) {
@@ -400,7 +433,12 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
 #pragma unroll
       for (int u = 0; u < LPX; ++u) {
         const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
-        glds16(xr, pxs + (u * NWL + lw) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+        if constexpr (X2) {
+          if (src2) glds16(xr2, pxs + (u * NWL + lw) * 1024, ok ? (unsigned)(rowoff2[u] + tapoff) : PG_OOB);
+          else glds16(xr, pxs + (u * NWL + lw) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+        } else {
+          glds16(xr, pxs + (u * NWL + lw) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+        }
       }
       const bool wk = kt * KS + csrc * 8 < a.K;
 #pragma unroll
@@ -486,8 +524,8 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
       pg_epilogue_fwd<BCH, MTC, NTP, WTPX, WTCH>(a, acc, bpx, bch, wpx, wch, fr, fq, ws, wslot);
     } else if constexpr (BK != 0) {
       const EpiStage sg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, a.seg_m > 0 ? bpx / a.seg_m : 0};
-      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 2, true>(a, acc, bpx, bch, wpx, wch,
-                                                                                          fr, fq, red, sg);
+      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 2, true, X2>(a, acc, bpx, bch, wpx,
+                                                                                              wch, fr, fq, red, sg);
       if (sums) stats_flush<BCH>(red, red_cnt, NWC * (ti + 1) - 1, a, bch, slot, lane, bpx, BPX);
     } else {
       pg_epilogue<BNB, BCH, MTC, NTP, WTPX, WTCH, 1>(a, acc, bpx, bch, wpx, wch, fr, fq, red);
@@ -1280,8 +1318,70 @@ static bool pg_k32w8_launch(const PgArgs& a, bool multi, hipStream_t st) {
   return true;
 }
 
+// The folded BatchNorm-backward data gradient (a.x2: artsbir_conv1x1_dgrad_fold):
+// the candidates instantiated with the two-operand loader — 2 (256 x 64), 16 (the
+// 128 x 128 GLB tile, plain or ACT epilogue), 19 (256 x 128 GLB, plain), 10 / 14
+// (the persistent streaming kernel, plain / ACT, 64- or 128-channel blocks) and 22
+// (pp256, in pp256_launch); epilogue: per-segment bias (+ the kind-1 mask and
+// BN-backward reduction of the BatchNorm before the conv's input)
+static bool pg_fold_launch(const PgArgs& a, int c, hipStream_t st) {
+  if (!a.x2 || !a.bias || a.relu || a.stats || a.res_mode) return false;
+  if (a.bnb && (a.bnb != 1 || a.bnb_nt != 1)) return false;
+  bool multi;
+  if (!pg_supported(a, multi) || multi) return false;
+  const bool k1 = a.bnb == 1;
+  auto ntl = [&](int bpx, int bch) { return ((a.M + bpx - 1) / bpx) * ((a.Cout + bch - 1) / bch); };
+  switch (c) {
+    case 2: {
+      if (!pg_fold_ok(a, 256, 64) || ntl(256, 64) > 0x7fffffffLL) return false;
+      const dim3 g((unsigned)ntl(256, 64));
+      if (k1) hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, false, 1, false, false, 64, false, true>), g, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((pgemm_kernel<256, 64, 4, 2, 3, false, 0, false, false, 64, false, true>), g, dim3(512), 0, st, a);
+      set_last_kernel(k1 ? "pgemm_kernel<256,64,bnb,fold>" : "pgemm_kernel<256,64,fold>");
+      return true;
+    }
+    case 16: {
+      if (!pg_fold_ok(a, 128, 32) || ntl(128, 128) > 0x7fffffffLL) return false;
+      const dim3 g((unsigned)ntl(128, 128));
+      if (k1) hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 3, false, 1, false, false, 32, true, true>), g, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 3, false, 0, false, false, 32, true, true>), g, dim3(256), 0, st, a);
+      set_last_kernel(k1 ? "pgemm_kernel<128,128,k32,glb,bnb,fold>" : "pgemm_kernel<128,128,k32,glb,fold>");
+      return true;
+    }
+    case 19: {
+      if (k1 || !pg_fold_ok(a, 256, 32) || ntl(256, 128) > 0x7fffffffLL) return false;
+      hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, false, 0, false, false, 32, true, true>),
+                         dim3((unsigned)ntl(256, 128)), dim3(512), 0, st, a);
+      set_last_kernel("pgemm_kernel<256,128,k32,glb,fold>");
+      return true;
+    }
+    case 10:
+    case 14: {
+      if ((c == 14) != k1 || !pg_fold_ok(a, 256, 64) || a.Cout < 64) return false;
+      const int bch = (k1 || a.Cout <= 64) ? 64 : 128;  // the ACT epilogue: 64-channel blocks (pstream_launch_k)
+      const long long nt = ntl(256, bch);
+      if (nt > 0x7fffffffLL) return false;
+      const int grid = (int)(nt < 256 ? nt : 256);
+      if (k1)
+        hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false, true, false, 1, false, 64, true>), dim3(grid), dim3(768), 0,
+                           st, a, (int)nt);
+      else if (bch == 64)
+        hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false, false, false, 0, false, 64, true>), dim3(grid), dim3(768),
+                           0, st, a, (int)nt);
+      else
+        hipLaunchKernelGGL((pstream_kernel<128, 4, 2, 3, false, false, false, 0, false, 64, true>), dim3(grid), dim3(768),
+                           0, st, a, (int)nt);
+      set_last_kernel(k1 ? "pstream_kernel<64,bnbk,fold>" : bch == 64 ? "pstream_kernel<64,fold>" : "pstream_kernel<128,fold>");
+      return true;
+    }
+    default:
+      return false;
+  }
+}
+
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel
 bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
+  if (a.x2 || a.w_sstride) return c == 22 ? pp256_launch(a, false, st) : pg_fold_launch(a, c, st);
   const bool act = a.bias != nullptr || a.relu != 0;  // bias / ReLU epilogue: pgemm_kernel and pstream only
   if (act && (a.stats || a.bnb)) return false;
   // res_mode 3 (gated data gradient, pg_epilogue_k only): the plain pgemm_kernel tiles

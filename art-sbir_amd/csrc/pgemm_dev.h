@@ -444,9 +444,9 @@ __device__ __forceinline__ void pg_epilogue(const PgArgs& a, const f32x4 (&acc)[
             for (int e = 0; e < 8; ++e) v[e] += rsc[u] * to_f(rv[u].v[e]);
           }
           if constexpr (!BNB) {
-            if (a.bias) {
+            if (a.bias) {  // (per BN segment for a folded BatchNorm backward)
 #pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] += a.bias[ch0 + e];
+              for (int e = 0; e < 8; ++e) v[e] += a.bias[wseg * a.bias_sstride + ch0 + e];
             }
             if (a.relu) {
 #pragma unroll
@@ -558,8 +558,10 @@ __device__ __forceinline__ void epi_prefetch(const PgArgs& a, EpiRegs<MTC / 2, N
 // target; S_RES / S_Y1 / S_MK: that operand is staged in LDS (else read from
 // global memory in batches of EJB pixel tiles); y_0 and the mask bits of BK 3
 // are always staged, the BN constants always come from the LDS table.
+// FB: the per-segment bias of a folded BatchNorm backward (artsbir_conv1x1_dgrad_fold)
+// is added to the accumulators first, before any mask / BN-backward reduction.
 template <int BK, bool TWO, bool S_RES, bool S_Y1, bool S_MK, int BCH, int MTC, int NTP, int WTPX, int WTCH,
-          bool REG = false, int EJB = 2, bool GLB = false>
+          bool REG = false, int EJB = 2, bool GLB = false, bool FB = false>
 __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
                                               int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg,
                                               const EpiRegs<MTC / 2, NTP>* er = nullptr) {
@@ -581,6 +583,8 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
     float s1[8], s2[8], s3[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
+    float fbias[FB ? 8 : 1];
+    if constexpr (FB) loadf8v(a.bias + wseg * a.bias_sstride + chc, fbias);
     // BN constants (LDS table): xhat_t = (y - m_t) * xa_t; ACT mask (y - mm) * ms + mh > 0
     float xa0[8], m0[8], xa1[8], m1[8], mm[8], ms[8], mh[8];
     if constexpr (BNB && GLB) {  // the same rows pg_prm_fill tabulates, straight from the (L2-resident) vectors
@@ -656,6 +660,10 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j0 + u][r]; v[4 + r] = acc[2 * p + 1][j0 + u][r]; }
+        if constexpr (FB) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += fbias[e];
+        }
         if (BK == 0 && a.res_mode == 3) {  // gate: the QuickGELU backward at the pre-activation in the res slot
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= pg_quickgelu_grad(to_f(rv[u].v[e]));
@@ -663,7 +671,7 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rsc * to_f(rv[u].v[e]);
         }
-        if constexpr (BK == 0) {
+        if constexpr (BK == 0 && !FB) {
           if (a.bias) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += a.bias[chc + e];

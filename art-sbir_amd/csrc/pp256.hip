@@ -92,7 +92,10 @@ __device__ __forceinline__ unsigned pp_nol2(unsigned w, float s0, float s1, floa
   return keep ? r : 0u;
 }
 
-template <int BK, bool TWO, bool TAPS>
+// X2 (1x1 only): the folded BatchNorm-backward data gradient — the reduction
+// runs over x (k < C1) and then x2; the tile's BN segment selects the weights
+// and the bias (artsbir_conv1x1_dgrad_fold)
+template <int BK, bool TWO, bool TAPS, bool X2 = false>
 __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   constexpr int NW = PP_NW, BCH = PP_BCH;
   constexpr int WTPX = 64, WTCH = 128, NTP = WTPX / 16, MTC = WTCH / 16;
@@ -125,12 +128,15 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   // the most negative row offset of a padded tap is still >= 0 (the per-row
   // part is the VGPR offset, which alone decides out-of-range)
   const int bias = (a.pad * (int)a.sH + a.pad * (int)a.sW) * 2;
-  const __amdgpu_buffer_rsrc_t xr =
+  __amdgpu_buffer_rsrc_t xr =
       pg_rsrc(reinterpret_cast<const char*>(a.x) + pg_uniform(img0 * a.sN * 2 - bias),
               (a.x_elems - img0 * a.sN) * 2 + bias);
-  const __amdgpu_buffer_rsrc_t wr = pg_rsrc(a.w, (long long)a.Cout * a.K * 2);
+  const long long wseg0 = X2 && a.seg_m > 0 ? bpx / a.seg_m : 0;
+  const __amdgpu_buffer_rsrc_t wr =
+      pg_rsrc(reinterpret_cast<const char*>(a.w) + pg_uniform(wseg0 * a.w_sstride * 2), (long long)a.Cout * a.K * 2);
   int rowoff[IPX];
   unsigned rmask[IPX], vofs[IPX], woff[ICH];
+  unsigned vofs2[X2 ? IPX : 1];  // X2: row offsets into the second operand
 #pragma unroll
   for (int u = 0; u < IPX; ++u) {
     const int row = (u * NW + wid) * PP_RPI + lrow;
@@ -150,7 +156,14 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
       }
     rmask[u] = msk;
     vofs[u] = (msk & 1u) ? (unsigned)rowoff[u] : PG_OOB;
+    if constexpr (X2)
+      vofs2[u] = valid ? (unsigned)(((img - img0) * a.sN2 + (long long)oh * a.sH2 + (long long)ow * a.sW2) * 2 + csrc * 16)
+                       : PG_OOB;
   }
+  const __amdgpu_buffer_rsrc_t xr2 =
+      X2 ? pg_rsrc(reinterpret_cast<const char*>(a.x2) + pg_uniform(img0 * a.sN2 * 2), (a.x2_elems - img0 * a.sN2) * 2)
+         : xr;
+  const unsigned c1b = X2 ? (unsigned)a.C1 * 2u : 0u;  // byte offset of k = C1 in a row of x
 #pragma unroll
   for (int u = 0; u < ICH; ++u) {
     const int ch = bch + pg_perm((u * NW + wid) * PP_RPI + lrow);
@@ -167,6 +180,14 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
 #pragma unroll
     for (int u = 0; u < IPX; ++u) pp_glds(xr, lds0 + slot * PP_BUF + u * NW * 1024, vofs[u], px_soff);
     px_soff += PP_KS * 2;
+    if constexpr (X2) {
+      if (px_soff == c1b) {  // past the first operand's C1 channels: the second one from its k = 0
+        xr = xr2;
+        px_soff = 0;
+#pragma unroll
+        for (int u = 0; u < IPX; ++u) vofs[u] = vofs2[u];
+      }
+    }
     if constexpr (TAPS) {
       u_ci += PP_KS;
       if (u_ci == aC) {  // next tap: its row validity
@@ -298,8 +319,8 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
 #ifndef PP_EJB
 #define PP_EJB 4  // pixel tiles whose epilogue operands are loaded together (2: 1-4 % slower fused dgrads, tools/gpu/r4_ej.sh)
 #endif
-  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, PP_EJB, true>(a, acc, bpx, bch, wpx, wch, fr,
-                                                                                        fq, red, sgg);
+  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, PP_EJB, true, X2>(a, acc, bpx, bch, wpx,
+                                                                                                wch, fr, fq, red, sgg);
   if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, (int)(blockIdx.x % ARTSBIR_NSLOT), lane, bpx, PP_BPX);
 }
 
@@ -314,6 +335,17 @@ bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st) {
   if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 + 2LL * (a.pad * a.sH + a.pad * a.sW) > 0x7fffffffLL) return false;
   if (a.M > (1LL << 40)) return false;
   if (a.seg_m > 0 && (a.seg_m % 64 != 0 || a.seg_m < 256 || a.M % a.seg_m != 0)) return false;
+  if (a.x2 || a.w_sstride) {  // the folded BatchNorm-backward data gradient (plain or ACT epilogue + bias)
+    if (!a.x2 || !a.bias || !pg_fold_ok(a, PP_BPX, PP_KS) || a.relu || a.stats || a.res_mode) return false;
+    if (a.bnb && (a.bnb != 1 || a.bnb_nt != 1 || a.Cout % 8 != 0)) return false;
+    if (((256 + HoWo - 1) / HoWo + 2) * a.sN2 * 2 > 0x7fffffffLL) return false;
+    const long long T = ((a.M + PP_BPX - 1) / PP_BPX) * ((a.Cout + PP_BCH - 1) / PP_BCH);
+    if (T > 0x7fffffffLL) return false;
+    if (a.bnb) hipLaunchKernelGGL((pp256_kernel<1, false, false, true>), dim3((unsigned)T), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((pp256_kernel<0, false, false, true>), dim3((unsigned)T), dim3(512), 0, st, a);
+    set_last_kernel(a.bnb ? "pp256_kernel<bnb,fold>" : "pp256_kernel<fold>");
+    return true;
+  }
   const bool act = a.bias != nullptr || a.relu != 0;
   if (act && (a.stats || a.bnb)) return false;
   if (a.bnb && (a.stats || a.Cout % 8 != 0)) return false;

@@ -64,6 +64,10 @@ FUSED_EVAL = os.environ.get("ARTSBIR_FUSED_EVAL", "1") != "0"
 # instead of the epilogue's f32 atomics, so a forward is bit-identical from run
 # to run and ReLU masks cannot flip between runs
 DETERMINISTIC = os.environ.get("ARTSBIR_DETERMINISTIC", "0") == "1"
+# ARTSBIR_FOLD_BN=0 runs the block-output BatchNorm backward (bn3 and the
+# downsample BN) as its own apply pass before the 1x1 convs' data / weight
+# gradients instead of folding it through them (artsbir_conv1x1_dgrad_fold)
+FOLD_BN = [os.environ.get("ARTSBIR_FOLD_BN", "1") != "0"]
 
 
 def set_deterministic(on: bool = True) -> bool:
@@ -918,6 +922,78 @@ class Engine:
                  tag=f"dgrad+bn{fused[0].kind} {B}x{H}x{W}x{co}->{C} {R}x{S} res{res_mode}")
         return dx
 
+    # ------------------------------------ BatchNorm backward folded through a 1x1 conv
+    def _fold_weights(self, packs, conv, coef, st: BNState):
+        """per-segment weights [G][Ci][Co + Ci] and bias [G][Ci] of the folded data
+        gradient (artsbir_bn_fold_bwd_prep): the g side diag(c1) W, the x side
+        W^T diag(b') W, the bias k W"""
+        _, wd = packs
+        co, ci = conv.weight.shape[:2]
+        G = self._G
+        dev = wd.device
+        wout = self._empty(G, ci, co + ci, device=dev)
+        bias = torch.empty(G, ci, dtype=torch.float32, device=dev)
+        amat = self._empty(G, ci, co, device=dev)
+        es = wout.element_size()
+        call("artsbir_bn_fold_bwd_prep", self.dt, co, ci, ptr(wd), ptr(coef), ptr(st.buf), 4 * co, G, ptr(wout),
+             ptr(bias), ptr(amat), _s(), kernel="fold_prep+gemm", flops=2.0 * G * ci * ci * co,
+             nbytes=float(es * (ci * co * (1 + 2 * G) + G * ci * (co + ci))), tag=f"fold_prep {co}->{ci} x{G}")
+        return wout, bias
+
+    def _dgrad_fold(self, g, x, fold, conv, fused=None):
+        """dx = [g | x] w_s^T + bias_s (artsbir_conv1x1_dgrad_fold): the data
+        gradient of a 1x1 conv through the BatchNorm after it, from the masked
+        gradient g at the BN output and the conv input x"""
+        wout, bias = fold
+        B, H, W, ci = x.shape
+        co = conv.weight.shape[0]
+        dx = self._empty(B, H, W, ci, device=x.device)
+        d = self._desc(B, H, W, ci, co, 1, 1, 1, 0)
+        px = B * H * W
+        es = dx.element_size()
+        nb = px * co + px * ci + self._G * ci * (co + ci) + px * ci + (px * ci if fused is not None else 0)
+        call("artsbir_conv1x1_dgrad_fold", d, ptr(g), ptr(x), ptr(wout), ptr(bias), ptr(dx),
+             ctypes.byref(fused[0]) if fused is not None else None, self._G, 4 * ci, _s(), kernel="auto",
+             flops=2.0 * px * ci * (co + ci), nbytes=float(es * nb),
+             tag=f"dgrad_fold{'+bn1' if fused is not None else ''} {B}x{H}x{W}x{co}+{ci}->{ci}")
+        return dx
+
+    def _wgrad_fold(self, g, x, conv, fw, coef, st: BNState, grads):
+        """weight gradient of a 1x1 conv through the BatchNorm after it (side
+        stream): per segment g^T x, the Gram matrix x^T x and the column sums of
+        x, combined by artsbir_bn_fold_wgrad_combine into the gradient buffer"""
+        if SKIP_WGRAD[0]:
+            return
+        main = torch.cuda.current_stream()
+        side = self._side_stream(g.device) if OVERLAP_WGRAD else main
+        if side is not main:
+            side.wait_stream(main)
+        G = self._G
+        B, H, W, ci = x.shape
+        co = conv.weight.shape[0]
+        Bs = B // G
+        Ms = Bs * H * W
+        es = x.element_size()
+        with torch.cuda.stream(side):
+            P = torch.zeros(G, co, ci, dtype=torch.float32, device=x.device)
+            gram = torch.zeros(G, ci, ci, dtype=torch.float32, device=x.device)
+            cs = torch.zeros(G, ci, dtype=torch.float32, device=x.device)
+            for s in range(G):
+                gs, xs = g[s * Bs:(s + 1) * Bs], x[s * Bs:(s + 1) * Bs]
+                call("artsbir_gemm_tn", self.dt, Ms, co, ci, ptr(gs), co, ptr(xs), ci, ptr(P[s]), _s(),
+                     kernel="auto", flops=2.0 * Ms * co * ci, nbytes=float(es * Ms * (co + ci) + 4 * co * ci),
+                     tag=f"wgrad_fold {Ms}x{co}x{ci}")
+                call("artsbir_gemm_tn", self.dt, Ms, ci, ci, ptr(xs), ci, ptr(xs), ci, ptr(gram[s]), _s(),
+                     kernel="auto", flops=2.0 * Ms * ci * ci, nbytes=float(es * Ms * ci + 4 * ci * ci),
+                     tag=f"gram {Ms}x{ci}")
+                call("artsbir_colsum", self.dt, ptr(xs), Ms, ci, ci, ptr(cs[s]), _s())
+            call("artsbir_bn_fold_wgrad_combine", self.dt, co, ci, G, ptr(P), ptr(gram), ptr(cs), ptr(fw), ptr(coef),
+                 ptr(st.buf), 4 * co, ptr(grads[conv.weight]), _s(), kernel="fold_wgrad_combine_kernel",
+                 flops=2.0 * G * co * ci * ci, nbytes=float(4 * G * (co * ci + ci * ci) + 8 * co * ci),
+                 tag=f"fold_combine {co}x{ci}")
+        if side is not main:
+            self._side_keep.extend([g, x, coef, st.buf, P, gram, cs])
+
     def _block_bwd(self, blk, bp, c, dout, grads, ws, fused_res=None, prev=None):
         """backward of one Bottleneck.  dout: gradient of the block output, or —
         when fused_res is given — g = dout * relu-mask with the block-output BN
@@ -929,26 +1005,46 @@ class Engine:
         s = blk.stride
         has_ds = blk.downsample is not None
         bnmods = [blk.bn3] + ([blk.downsample[2]] if has_ds else [])
-        if fused_res is not None:
+        # the block-output BN backward folded through conv3 / the downsample conv
+        # (csrc/fold.hip): no dy3 / dyd tensors, their apply pass and re-reads gone
+        fold = fused_res is not None and FOLD_BN[0]
+        dys = coefs = None
+        if fold:
+            _, slots, targets = fused_res
+            B3, H3, W3, _ = y3.shape
+            coefs = self._bn_coefs(targets, bnmods, slots, grads, float(B3 // self._G * H3 * W3))
+            gid = dout
+        elif fused_res is not None:
             dys = self._bn_finish(dout, fused_res, bnmods, grads)
             gid = dout  # the identity branch's gradient is g itself
         else:
             targets = [(y3, b3)] + ([(yd, bd)] if has_ds else [])
             gid = None if has_ds else torch.empty_like(dout)
             dys = self._bn_bwd(0, dout, targets, bnmods, ws, grads, mask=out, gout=gid)
-        dy3 = dys[0]
         c3in = Act(p2)
-        held = self._wgrad_pre(dy3, c3in, blk.conv3, 1, 0, grads)
         c3out = c3in.shape[:3] + (blk.conv3.weight.shape[1],)
-        if s == 1 and _fuse_bnb():
-            f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
-            g2 = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out, fused=f2)
-            self._wgrad_post(held)
-            dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
+        if fold:
+            fw3 = self._fold_weights(bp["conv3"], blk.conv3, coefs[0], b3)
+            self._wgrad_fold(dout, p2, blk.conv3, bp["conv3"][0], coefs[0], b3, grads)
+            if s == 1:
+                f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
+                g2 = self._dgrad_fold(dout, p2, fw3, blk.conv3, fused=f2)
+                dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
+            else:
+                dp = self._dgrad_fold(dout, p2, fw3, blk.conv3)
+                dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s)
         else:
-            dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out)
-            self._wgrad_post(held)
-            dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
+            dy3 = dys[0]
+            held = self._wgrad_pre(dy3, c3in, blk.conv3, 1, 0, grads)
+            if s == 1 and _fuse_bnb():
+                f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
+                g2 = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out, fused=f2)
+                self._wgrad_post(held)
+                dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
+            else:
+                dp = self._dgrad(dy3, bp["conv3"][1], blk.conv3, 0, c3out)
+                self._wgrad_post(held)
+                dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
         held = self._wgrad_pre(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
         if _fuse_bnb():
             f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
@@ -961,12 +1057,17 @@ class Engine:
             dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
         held1 = self._wgrad_pre(dy1, Act(h), blk.conv1, 1, 0, grads)
         if has_ds:
-            dyd = dys[1]
             din = pd if s > 1 else h
             dconv = blk.downsample[1]
-            held = self._wgrad_pre(dyd, Act(din), dconv, 1, 0, grads)
-            res = self._dgrad(dyd, bp["down"][1], dconv, 0, din.shape)
-            self._wgrad_post(held)
+            if fold:
+                fwd_ = self._fold_weights(bp["down"], dconv, coefs[1], bd)
+                self._wgrad_fold(dout, din, dconv, bp["down"][0], coefs[1], bd, grads)
+                res = self._dgrad_fold(dout, din, fwd_, dconv)
+            else:
+                dyd = dys[1]
+                held = self._wgrad_pre(dyd, Act(din), dconv, 1, 0, grads)
+                res = self._dgrad(dyd, bp["down"][1], dconv, 0, din.shape)
+                self._wgrad_post(held)
             res_mode = 2 if s > 1 else 1
         else:
             res, res_mode = gid, 1

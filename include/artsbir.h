@@ -120,6 +120,38 @@ int artsbir_conv2d_dgrad_bnb(const artsbir_conv_desc* d, const void* dy, const v
                              const void* res, int res_mode, const artsbir_bn_bwd_desc* bnb, int nseg,
                              long long param_stride, void* stream);
 
+/* The BatchNorm2d(train) backward folded through the 1x1 Conv2d in front of it
+ * (models.py:219-220 conv3 -> bn3, models.py:227-229 downsample conv -> BN;
+ * replaces artsbir_bn_bwd_apply + artsbir_conv2d_dgrad of that conv, see
+ * csrc/fold.hip for the algebra).  d: the FORWARD conv (x [N][H][W][C],
+ * C = Ci; Cout = Co; 1x1, stride 1).  g [N][H][W][Co]: the masked gradient at
+ * the BN output; x: the conv's input; w [nseg][Ci][Co + Ci] and bias
+ * [nseg][Ci] f32 from artsbir_bn_fold_bwd_prep.  dx [N][H][W][Ci] =
+ * [g | x] w_s^T + bias_s for the pixels of segment s (nseg equal segments of
+ * the batch).  bnb (optional, kind 1, one target): dx is the gradient at the
+ * output of the BN(+ReLU) feeding x; g' = dx * mask is stored and the BN
+ * reduction fused as in artsbir_conv2d_dgrad_bnb (param_stride as there). */
+int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                               const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                               long long param_stride, void* stream);
+/* Weights of artsbir_conv1x1_dgrad_fold for every BN segment s:
+ * wout[s][ci][co] = c1_s[co] W[co][ci], wout[s][ci][Co + k] = sum_co W[co][ci] b'_s[co] W[co][k]
+ * (b' = -c1 c3 istd), bias[s][ci] = sum_co W[co][ci] (-c1 (c2 - c3 istd mean))[co].
+ * wt: the conv's data-gradient operand W^T [Ci][Co] (compute dtype); coef
+ * [nseg][3][Co] from artsbir_bn_bwd_finalize_seg; prm: the BN parameter blocks
+ * (mean, istd, ...) [Co] of segment s at + s*pstride; amat: workspace
+ * [nseg][Ci][Co] of the compute dtype. */
+int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* wt, const float* coef, const float* prm,
+                             long long pstride, int nseg, void* wout, float* bias, void* amat, void* stream);
+/* The weight gradient of that conv: dw[co][ci] += sum_s c1_s[co] P_s[co][ci] +
+ * b'_s[co] (W Gram_s)[co][ci] + k_s[co] colsums_s[ci], with P_s = g_s^T x_s
+ * [nseg][Co][Ci], Gram_s = x_s^T x_s [nseg][Ci][Ci], colsums_s = 1^T x_s
+ * [nseg][Ci] (f32, from artsbir_gemm_tn / artsbir_colsum), w the forward weight
+ * [Co][Ci] (compute dtype), k = -c1 (c2 - c3 istd mean). */
+int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const float* P, const float* gram,
+                                  const float* colsums, const void* w, const float* coef, const float* prm,
+                                  long long pstride, float* dw, void* stream);
+
 /* ---- layout / parameter packing ---------------------------------------- */
 /* x.type(weight dtype) + NCHW -> NHWC8 (models.py:352); x [B][Cin<=8][H][W] f32. */
 int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, void* out, void* stream);
