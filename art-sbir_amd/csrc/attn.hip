@@ -441,7 +441,9 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16* __restrict__ 
       gf[s] = at_row(gimg, q, s, hh);
     }
     f32x16 dq0 = at_zero(), dq1 = at_zero();
-    for (int kb = 0; kb < nb; ++kb) {
+    // one key block; CHK: the last block when L % 32 != 0
+    auto qblock = [&](int kb, auto chk) {
+      constexpr bool CHK = decltype(chk)::value;
       f32x16 st = at_zero(), dpt = at_zero();
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -451,16 +453,19 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16* __restrict__ 
       bf16x8 df0, df1;
 #pragma unroll
       for (int rho = 0; rho < 16; ++rho) {
-        // no validity test without a mask: a key >= L has zero K and V rows, so
-        // its dS (finite) meets a zero row of K in dQ; rows q >= L are not stored
+        // without a mask a key >= L has zero K and V rows, so its dS meets a zero
+        // row of K in dQ (rows q >= L are not stored); its p = exp2(-lse2) is
+        // zeroed all the same in the last block (CHK), or a row whose log-sum-exp
+        // is below ~-88 would make it inf and the product with the zero K row NaN
         float p;
+        const int key = 32 * kb + at_crow(rho, hh);
         if (MASK) {
-          const int key = 32 * kb + at_crow(rho, hh);
           float v = st[rho] * AT_SC2;
           if (key < L && qok) v += mask[(long long)q * L + key] * AT_LOG2E;
           p = (key < L && qok) ? __builtin_amdgcn_exp2f(v - lq2) : 0.f;
         } else {
           p = __builtin_amdgcn_exp2f(fmaf(st[rho], AT_SC2, -lq2));
+          if (CHK) p = key < L ? p : 0.f;
         }
         const float ds = p * (dpt[rho] - D);
         if (rho < 8) df0[rho] = (bf16)ds;
@@ -470,7 +475,10 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(const bf16* __restrict__ 
       dq0 = at_mfma(at_trfrag(kimg, 32 * kb + 16, 0, lane), df1, dq0);
       dq1 = at_mfma(at_trfrag(kimg, 32 * kb, 32, lane), df0, dq1);
       dq1 = at_mfma(at_trfrag(kimg, 32 * kb + 16, 32, lane), df1, dq1);
-    }
+    };
+    const int nfull = (L & 31) ? nb - 1 : nb;
+    for (int kb = 0; kb < nfull; ++kb) qblock(kb, std::false_type{});
+    if (nfull < nb) qblock(nfull, std::true_type{});
     if (qok) at_store_t(dqkv + (long long)q * rs + (long long)n * ld + h * 64, dq0, dq1, 0.125f, hh);
   }
 
@@ -557,7 +565,6 @@ bool attn_bwd_mfma(const bf16* qkv, const bf16* o, const bf16* dout, const float
   const int nthr = ((L + 31) / 32) * 64;
   // ARTSBIR_ATTN_BWD2=1: the two-kernel form (timing comparison)
   static const bool two = [] { const char* e = getenv("ARTSBIR_ATTN_BWD2"); return e && atoi(e) != 0; }();
-  // the one-workgroup form addresses rows by 32-bit buffer offsets
   if (!two) {
     if (mask)
       hipLaunchKernelGGL(attn_bwd_kernel<true>, dim3((unsigned)grid), dim3(nthr), 0, st, qkv, o, dout, lse, L, N, heads,

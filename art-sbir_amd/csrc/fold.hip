@@ -55,86 +55,34 @@ __global__ void __launch_bounds__(256) fold_prep_kernel(const T* __restrict__ wt
   if (threadIdx.x == 0) bias[(long long)s * Ci + ci] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// dW[co][ci] += sum_s c1_s[co] P_s[co][ci] + b'_s[co] (W Gram_s)[co][ci] + k_s[co] cs_s[ci]
-// one 64 x 64 tile of dW per workgroup, 4 x 4 values per thread; the W Gram_s
-// product in f32 through LDS (32-k slices of diag(b'_s) W and of Gram_s)
-template <typename T>
+// dW[co][ci] += sum_s c1_s[co] P_s[co][ci] + b'_s[co] T[co][s Ci + ci] + k_s[co] cs_s[ci]
+// with T = W [Gram_0 | Gram_1 | ...] (an f32 GEMM before it): elementwise, 4
+// values of one dW row per thread
 __global__ void __launch_bounds__(256) fold_wgrad_combine_kernel(const float* __restrict__ P,
-                                                                 const float* __restrict__ gram,
-                                                                 const float* __restrict__ cs,
-                                                                 const T* __restrict__ w, int Co, int Ci, int nseg,
-                                                                 const float* __restrict__ coef,
+                                                                 const float* __restrict__ T,
+                                                                 const float* __restrict__ cs, int Co, int Ci,
+                                                                 int nseg, const float* __restrict__ coef,
                                                                  const float* __restrict__ prm, long long pstride,
                                                                  float* __restrict__ dw) {
-  __shared__ float ws[64][33];
-  __shared__ __attribute__((aligned(16))) float gs[32][64];
-  const int co0 = blockIdx.y * 64, ci0 = blockIdx.x * 64;
-  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
-  float acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  const int cq = Ci / 4;
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)Co * cq) return;
+  const int co = (int)(i / cq), ci = (int)(i - (long long)co * cq) * 4;
+  float4 acc = *reinterpret_cast<const float4*>(dw + (long long)co * Ci + ci);
   for (int s = 0; s < nseg; ++s) {
-    const float* c1 = coef + (long long)s * 3 * Co;
-    const float* c2 = c1 + Co;
-    const float* c3 = c2 + Co;
-    const float* mean = prm + s * pstride;
-    const float* istd = mean + Co;
-    const float* gm = gram + (long long)s * Ci * Ci;
-    for (int k0 = 0; k0 < Ci; k0 += 32) {
-      for (int i = tid; i < 64 * 32; i += 256) {
-        const int r = i >> 5, kk = i & 31;
-        const int co = co0 + r, k = k0 + kk;
-        float v = 0.f;
-        if (co < Co && k < Ci) v = -c1[co] * c3[co] * istd[co] * to_f(w[(long long)co * Ci + k]);
-        ws[r][kk] = v;
-      }
-      for (int i = tid; i < 32 * 64; i += 256) {
-        const int kk = i >> 6, c = i & 63;
-        const int k = k0 + kk, ci = ci0 + c;
-        gs[kk][c] = (k < Ci && ci < Ci) ? gm[(long long)k * Ci + ci] : 0.f;
-      }
-      __syncthreads();
-#pragma unroll 8
-      for (int kk = 0; kk < 32; ++kk) {
-        const float4 g4 = *reinterpret_cast<const float4*>(&gs[kk][tx * 4]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float a = ws[ty * 4 + i][kk];
-          acc[i][0] += a * g4.x;
-          acc[i][1] += a * g4.y;
-          acc[i][2] += a * g4.z;
-          acc[i][3] += a * g4.w;
-        }
-      }
-      __syncthreads();
-    }
-    const float* ps = P + (long long)s * Co * Ci;
-    const float* css = cs + (long long)s * Ci;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co0 + ty * 4 + i;
-      if (co >= Co) continue;
-      const float a1 = c1[co];
-      const float k = -a1 * (c2[co] - c3[co] * istd[co] * mean[co]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ci = ci0 + tx * 4 + j;
-        if (ci < Ci) acc[i][j] += a1 * ps[(long long)co * Ci + ci] + k * css[ci];
-      }
-    }
+    const float* c = coef + (long long)s * 3 * Co;
+    const float* mp = prm + s * pstride;
+    const float c1 = c[co], c2 = c[Co + co], c3 = c[2 * Co + co], mean = mp[co], istd = mp[Co + co];
+    const float bp = -c1 * c3 * istd, k = -c1 * (c2 - c3 * istd * mean);
+    const float4 p = *reinterpret_cast<const float4*>(P + ((long long)s * Co + co) * Ci + ci);
+    const float4 t = *reinterpret_cast<const float4*>(T + (long long)co * nseg * Ci + (long long)s * Ci + ci);
+    const float4 q = *reinterpret_cast<const float4*>(cs + (long long)s * Ci + ci);
+    acc.x += c1 * p.x + bp * t.x + k * q.x;
+    acc.y += c1 * p.y + bp * t.y + k * q.y;
+    acc.z += c1 * p.z + bp * t.z + k * q.z;
+    acc.w += c1 * p.w + bp * t.w + k * q.w;
   }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = co0 + ty * 4 + i;
-    if (co >= Co) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ci = ci0 + tx * 4 + j;
-      if (ci < Ci) dw[(long long)co * Ci + ci] += acc[i][j];
-    }
-  }
+  *reinterpret_cast<float4*>(dw + (long long)co * Ci + ci) = acc;
 }
 
 }  // namespace artsbir
@@ -167,20 +115,29 @@ extern "C" int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* w
 
 extern "C" int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const float* P, const float* gram,
                                              const float* colsums, const void* w, const float* coef,
-                                             const float* prm, long long pstride, float* dw, void* stream) {
-  if (Co <= 0 || Ci <= 0 || nseg < 1) { set_error("bn_fold_wgrad_combine: bad shape"); return -1; }
-  if (!P || !gram || !colsums || !w || !coef || !prm || !dw) {
+                                             const float* prm, long long pstride, float* dw, float* workspace,
+                                             void* stream) {
+  if (Co <= 0 || Ci <= 0 || Co % 8 || Ci % 8 || nseg < 1) { set_error("bn_fold_wgrad_combine: bad shape"); return -1; }
+  if (!P || !gram || !colsums || !w || !coef || !prm || !dw || !workspace) {
     set_error("bn_fold_wgrad_combine: null operand");
     return -1;
   }
-  const dim3 g((unsigned)((Ci + 63) / 64), (unsigned)((Co + 63) / 64));
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == ARTSBIR_DT_BF16)
-    hipLaunchKernelGGL(fold_wgrad_combine_kernel<bf16>, g, dim3(256), 0, st, P, gram, colsums,
-                       reinterpret_cast<const bf16*>(w), Co, Ci, nseg, coef, prm, pstride, dw);
-  else
-    hipLaunchKernelGGL(fold_wgrad_combine_kernel<float>, g, dim3(256), 0, st, P, gram, colsums,
-                       reinterpret_cast<const float*>(w), Co, Ci, nseg, coef, prm, pstride, dw);
+  // T = W [Gram_0 | ... ] in f32 (the Gram matrices are [nseg * Ci][Ci] rows, symmetric)
+  const float* wf = reinterpret_cast<const float*>(w);
+  float* T = workspace;
+  if (dtype == ARTSBIR_DT_BF16) {
+    float* wc = workspace;
+    T = workspace + (long long)Co * Ci;
+    if (artsbir_cast(ARTSBIR_DT_BF16, w, ARTSBIR_DT_F32, wc, (long long)Co * Ci, stream)) return -1;
+    wf = wc;
+  }
+  if (artsbir_gemm_nt(ARTSBIR_DT_F32, Co, nseg * Ci, Ci, wf, Ci, gram, T, (long long)nseg * Ci, 1, 0, nullptr, nullptr,
+                      stream))
+    return -1;
+  const long long n = (long long)Co * (Ci / 4);
+  hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, T, colsums, Co,
+                     Ci, nseg, coef, prm, pstride, dw);
   ARTSBIR_CHECK_LAUNCH("fold_wgrad_combine");
   return 0;
 }

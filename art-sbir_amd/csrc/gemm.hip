@@ -440,6 +440,11 @@ struct WgradArgs {
   long long M;
   long long m_per_split;  // multiple of BK
   float* dw;               // [Cout][K] f32
+  // dY in two parts along Cout (PwArgs: same fields; the pipelined kernels only)
+  const void* dy2 = nullptr;
+  long long dy2_elems = 0, ldd2 = 0;
+  int Cout1 = 0;
+  float* dw2 = nullptr;
 };
 
 __device__ __forceinline__ void transpose_unit(const uint4 (&in)[8], uint4 (&out)[8], bf16) {
@@ -1288,6 +1293,7 @@ static PwArgs to_pw(const WgradArgs& a) {
   p.H = a.H; p.W = a.W; p.C = a.C; p.R = a.R; p.S = a.S; p.stride = a.stride; p.pad = a.pad;
   p.Ho = a.Ho; p.Wo = a.Wo; p.dense = a.dense; p.ldx = a.ldx;
   p.Cout = a.Cout; p.K = a.K; p.M = a.M; p.m_per_split = 0; p.dw = a.dw;
+  p.dy2 = a.dy2; p.dy2_elems = a.dy2_elems; p.ldd2 = a.ldd2; p.Cout1 = a.Cout1; p.dw2 = a.dw2;
   static const int dbg = getenv("ARTSBIR_PW_DBG") ? atoi(getenv("ARTSBIR_PW_DBG")) : 0;
   p.dbg = dbg;
   return p;
@@ -1300,6 +1306,7 @@ static void launch_wgrad_old(WgradArgs& a, hipStream_t st);
 static bool run_wg_candidate(int c, WgradArgs& a, hipStream_t st) {
   if (c >= 100) return pw256_launch(to_pw(a), c - 100, st);
   if (c >= 0) return pwgrad_launch(to_pw(a), c, st);
+  if (a.dy2) return false;  // the register-staged kernel reads one dY
   launch_wgrad_old<bf16>(a, st);
   return true;
 }
@@ -1315,6 +1322,7 @@ static int tune_wgrad(const WgradArgs& a, hipStream_t st) {
   }
   WgradArgs at = a;
   at.dw = g_tune_dw;
+  if (a.dy2) at.dw2 = g_tune_dw + (size_t)a.Cout1 * a.K;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -1354,7 +1362,8 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
     if (force) {
       choice = atoi(force);
     } else {
-      const WgKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.dense, a.K, a.ldd, a.ldx};
+      // (dense 2: dY in two parts, artsbir_gemm_tn2)
+      const WgKey key{a.M, a.H, a.W, a.C, a.Cout, a.R, a.S, a.stride, a.pad, a.dy2 ? 2 : a.dense, a.K, a.ldd, a.ldx};
       std::lock_guard<std::mutex> lk(g_tune_mu);
       auto it = g_wg_choice.find(key);
       if (it != g_wg_choice.end()) {
@@ -1376,6 +1385,7 @@ static int launch_wgrad(WgradArgs& a, hipStream_t st) {
       return 0;
     }
   }
+  if (a.dy2) return 1;  // no pipelined kernel took the two-part dY: the caller splits it
   launch_wgrad_old<T>(a, st);
   ARTSBIR_CHECK_LAUNCH("wgrad");
   return 0;
@@ -1471,6 +1481,34 @@ extern "C" int artsbir_tune_load(const char* path) {
   }
   fclose(f);
   return n;
+}
+
+// dw[n][k] += sum_m dy[m][n] x[m][k] (n < N1) and dw2[n][k] += sum_m dy2[m][n] x[m][k]
+// (n < N2) in one launch where a pipelined kernel takes it (the folded BatchNorm
+// backward's g^T x and x^T x, fold.hip), else as two artsbir_gemm_tn
+extern "C" int artsbir_gemm_tn2(int dtype, long long M, int N1, int N2, int K, const void* dy, long long ldd,
+                                const void* dy2, long long ldd2, const void* x, long long ldx, float* dw, float* dw2,
+                                void* stream) {
+  if (N1 % 8 || N2 % 8 || K % 8 || ldd % 8 || ldd2 % 8 || ldx % 8) {
+    set_error("gemm_tn2: N1=%d N2=%d K=%d and the row strides must be multiples of 8", N1, N2, K);
+    return -1;
+  }
+  if (M <= 0) return 0;
+  if (dtype == ARTSBIR_DT_BF16) {
+    WgradArgs a;
+    a.dy = dy; a.ldd = ldd; a.dy_elems = (M - 1) * ldd + N1;
+    a.x = x; a.x_elems = (M - 1) * ldx + K;
+    a.sN = 0; a.sH = 0; a.sW = 0; a.H = 1; a.W = 1; a.C = K;
+    a.R = 1; a.S = 1; a.stride = 1; a.pad = 0; a.Ho = 1; a.Wo = 1;
+    a.dense = 1; a.ldx = ldx;
+    a.in_scale = nullptr; a.in_shift = nullptr; a.in_relu = 0;
+    a.Cout = N1 + N2; a.K = K; a.M = M; a.dw = dw;
+    a.dy2 = dy2; a.ldd2 = ldd2; a.dy2_elems = (M - 1) * ldd2 + N2; a.Cout1 = N1; a.dw2 = dw2;
+    const int rc = launch_wgrad<bf16>(a, (hipStream_t)stream);
+    if (rc <= 0) return rc;
+  }
+  const int rc = artsbir_gemm_tn(dtype, M, N1, K, dy, ldd, x, ldx, dw, stream);
+  return rc ? rc : artsbir_gemm_tn(dtype, M, N2, K, dy2, ldd2, x, ldx, dw2, stream);
 }
 
 extern "C" int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void* dy, long long ldd,

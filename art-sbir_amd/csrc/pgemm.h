@@ -70,6 +70,14 @@ struct PwArgs {
   long long m_per_split;  // set by the launcher
   float* dw;              // f32 [Cout][K], accumulated
   int dbg;                // profiling (ARTSBIR_PW_DBG): bit 0 skips the dW atomics
+  // dY in two parts along Cout (dense only; the folded BatchNorm backward's
+  // g^T x and x^T x in one launch, artsbir_gemm_tn2): rows co >= Cout1 read dy2
+  // (column co - Cout1, row stride ldd2) and accumulate into dw2 + (co - Cout1) * K;
+  // Cout1 is a multiple of the kernel's Cout tile
+  const void* dy2 = nullptr;
+  long long dy2_elems = 0, ldd2 = 0;
+  int Cout1 = 0;
+  float* dw2 = nullptr;
 };
 // candidate c (0 .. pwgrad_num_cfgs()-1) of the pipelined wgrad kernel;
 // false, launching nothing, if it does not apply to the shape

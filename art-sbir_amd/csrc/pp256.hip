@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   const __amdgpu_buffer_rsrc_t xr2 =
       X2 ? pg_rsrc(reinterpret_cast<const char*>(a.x2) + pg_uniform(img0 * a.sN2 * 2), (a.x2_elems - img0 * a.sN2) * 2)
          : xr;
-  const unsigned c1b = X2 ? (unsigned)a.C1 * 2u : 0u;  // byte offset of k = C1 in a row of x
+  unsigned c1b = X2 ? (unsigned)a.C1 * 2u : 0u;  // byte offset of k = C1 in a row of x (switched once)
 #pragma unroll
   for (int u = 0; u < ICH; ++u) {
     const int ch = bch + pg_perm((u * NW + wid) * PP_RPI + lrow);
@@ -184,6 +184,7 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
       if (px_soff == c1b) {  // past the first operand's C1 channels: the second one from its k = 0
         xr = xr2;
         px_soff = 0;
+        c1b = 0xffffffffu;  // once: the second operand may be wider than the first
 #pragma unroll
         for (int u = 0; u < IPX; ++u) vofs[u] = vofs2[u];
       }

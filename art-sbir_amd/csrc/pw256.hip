@@ -106,16 +106,22 @@ __global__ void __launch_bounds__(512, 1) pw256_kernel(PwArgs a, int ntiles) {
     lrow[u] = row;
     lch[u] = 4 * (st & 7) + ((lane & 3) ^ ((row >> 2) & 3));
   }
+  // dY in two parts along Cout (a.dy2, dense): this tile's rows come from one of them
+  const bool s2 = DENSE && a.dy2 != nullptr && co0 >= a.Cout1;
+  const long long ldd = s2 ? a.ldd2 : a.ldd;
+  const int cb = s2 ? co0 - a.Cout1 : co0;  // first dY column of the tile
+  const int colim = (DENSE && a.dy2) ? (s2 ? a.Cout - a.Cout1 : a.Cout1) : a.Cout;
+  float* const dwp = s2 ? a.dw2 : a.dw;
   // dY rows from m_beg; out-of-range co or rows past m_end read zeros
-  const __amdgpu_buffer_rsrc_t dr = pg_rsrc(reinterpret_cast<const bf16*>(a.dy) + m_beg * a.ldd,
-                                            (m_end - m_beg) * a.ldd * 2);
+  const __amdgpu_buffer_rsrc_t dr = pg_rsrc(reinterpret_cast<const bf16*>(s2 ? a.dy2 : a.dy) + m_beg * ldd,
+                                            (m_end - m_beg) * ldd * 2);
   unsigned aoff[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    const int co = co0 + 8 * lch[u];
-    aoff[u] = co < a.Cout ? (unsigned)(lrow[u] * a.ldd * 2 + co * 2) : PW_OOB;
+    const int co = cb + 8 * lch[u];
+    aoff[u] = co < colim ? (unsigned)(lrow[u] * ldd * 2 + co * 2) : PW_OOB;
   }
-  const unsigned a_step = (unsigned)(PW_KS * a.ldd * 2);
+  const unsigned a_step = (unsigned)(PW_KS * ldd * 2);
   // X: dense rows from m_beg, or the implicit im2col of the conv input
   const int HoWo = a.Ho * a.Wo;
   const long long img_beg = DENSE ? 0 : m_beg / HoWo;
@@ -261,6 +267,7 @@ __global__ void __launch_bounds__(512, 1) pw256_kernel(PwArgs a, int ntiles) {
   }
 
   // acc[i][j][r]: co = co0 + 128 wco + 16 i + 4 g + r, k = k0 + 64 wkk + 16 j + t
+  // (relative to the tile's part of dY: cb, colim, dwp)
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -268,8 +275,8 @@ __global__ void __launch_bounds__(512, 1) pw256_kernel(PwArgs a, int ntiles) {
       const int k = k0 + 64 * wkk + 16 * j + t;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + 128 * wco + 16 * i + 4 * g + r;
-        if (co < a.Cout && k < a.K) atomicAdd(a.dw + (long long)co * a.K + k, acc[i][j][r]);
+        const int co = cb + 128 * wco + 16 * i + 4 * g + r;
+        if (co < colim && k < a.K) atomicAdd(dwp + (long long)co * a.K + k, acc[i][j][r]);
       }
     }
 }
@@ -284,6 +291,7 @@ bool pw256_launch(PwArgs a, int level, hipStream_t st) {
   // 64-channel layers), not by the MFMAs
   if (a.Cout < 64 || a.K < 64 || a.Cout % 8 || a.K % 8 || a.M <= 0) return false;
   if (a.ldd % 8 || (a.dense && a.ldx % 8)) return false;
+  if (a.dy2 && (!a.dense || a.Cout1 % PW_BT != 0 || !a.dw2 || a.ldd2 % 8)) return false;
   if (!a.dense && (a.C % 8 || a.R * a.S > 32 || (long long)a.Ho * a.Wo < PW_KS)) return false;
   const int ntiles = ((a.Cout + PW_BT - 1) / PW_BT) * ((a.K + PW_BT - 1) / PW_BT);
   const long long ksteps = (a.M + PW_KS - 1) / PW_KS;
@@ -293,7 +301,9 @@ bool pw256_launch(PwArgs a, int level, hipStream_t st) {
   long long per = (ksteps + splits - 1) / splits;
   if (per < 16) per = 16;  // at least 16 K-tiles (512 rows) per workgroup
   // K-tile offsets (32 rows x ld) summed over a split stay below 2^30 (PW_OOB stays out of range)
-  const long long row_bytes = (a.dense ? (a.ldx > a.ldd ? a.ldx : a.ldd) : a.ldd) * 2;
+  long long ldmax = a.dense ? (a.ldx > a.ldd ? a.ldx : a.ldd) : a.ldd;
+  if (a.dy2 && a.ldd2 > ldmax) ldmax = a.ldd2;
+  const long long row_bytes = ldmax * 2;
   long long cap = (1LL << 30) / (row_bytes * PW_KS) - 1;
   if (!a.dense) {
     const long long imgs = 0x7fffffffLL / (a.sN * 2) - 2;  // image-relative conv offsets below 2^31

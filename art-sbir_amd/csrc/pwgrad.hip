@@ -133,8 +133,14 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
   if (m_end > a.M) m_end = a.M;
   const int nk = (int)((m_end - m_beg + BM - 1) / BM);
 
-  const __amdgpu_buffer_rsrc_t dr = pw_rsrc(reinterpret_cast<const bf16*>(a.dy) + m_beg * a.ldd,
-                                            (a.dy_elems - m_beg * a.ldd) * 2);
+  // dY in two parts along Cout (a.dy2): this tile's rows come from one of them
+  const bool s2 = DENSE && a.dy2 != nullptr && co0 >= a.Cout1;
+  const bf16* dyp = reinterpret_cast<const bf16*>(s2 ? a.dy2 : a.dy);
+  const long long ldd = s2 ? a.ldd2 : a.ldd;
+  const int cb = s2 ? co0 - a.Cout1 : co0;                            // first dY column of the tile
+  const int colim = (DENSE && a.dy2) ? (s2 ? a.Cout - a.Cout1 : a.Cout1) : a.Cout;
+  float* const dwp = s2 ? a.dw2 : a.dw;
+  const __amdgpu_buffer_rsrc_t dr = pw_rsrc(dyp + m_beg * ldd, ((s2 ? a.dy2_elems : a.dy_elems) - m_beg * ldd) * 2);
   const int HoWo = a.Ho * a.Wo;
   const long long img_beg = DENSE ? 0 : m_beg / HoWo;
   const __amdgpu_buffer_rsrc_t xr =
@@ -154,8 +160,8 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
     const int pr = g * 4 + lpr;
     const int f = pw_src<BCO>(pr, lslot);
     a_m[u] = f / BCO;
-    const int co = co0 + f % BCO;
-    a_col[u] = co < a.Cout ? (unsigned)(co * 2) : PW_OOB;
+    const int co = cb + f % BCO;
+    a_col[u] = co < colim ? (unsigned)(co * 2) : PW_OOB;
   }
   int b_m[LB];
   unsigned b_tap[LB];  // DENSE: byte offset of the k columns; conv: ci * 2
@@ -194,7 +200,7 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
       if (!a_on[u]) continue;
       const long long m = mrow0 + a_m[u];
       const bool ok = m_beg + m < m_end && a_col[u] != PW_OOB;
-      pw_glds16(dr, as + (u * NW + wid) * 1024, ok ? (unsigned)(m * a.ldd * 2) + a_col[u] : PW_OOB);
+      pw_glds16(dr, as + (u * NW + wid) * 1024, ok ? (unsigned)(m * ldd * 2) + a_col[u] : PW_OOB);
     }
 #pragma unroll
     for (int u = 0; u < LB; ++u) {
@@ -305,6 +311,7 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
     return;
   }
   // acc[i][j][r]: co = co0 + wco*WTCO + 16 i + 4 g + r, k = k0 + wkk*WTK + 16 j + t
+  // (relative to the tile's part of dY: cb, colim, dwp)
 #pragma unroll
   for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -312,8 +319,8 @@ __global__ void __launch_bounds__(64 * WCO * WKK) pwgrad_kernel(PwArgs a) {
       const int k = k0 + wkk * WTK + 16 * j + t;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wco * WTCO + 16 * i + 4 * g + r;
-        if (co < a.Cout && k < a.K) atomicAdd(a.dw + (long long)co * a.K + k, acc[i][j][r]);
+        const int co = cb + wco * WTCO + 16 * i + 4 * g + r;
+        if (co < colim && k < a.K) atomicAdd(dwp + (long long)co * a.K + k, acc[i][j][r]);
       }
     }
 }
@@ -640,12 +647,14 @@ int pwgrad_level(int c) { return c >= 0 && c < kNumPw * kNumLevels ? c / kNumPw 
 // candidate c = cfg + kNumPw * level of the pipelined wgrad; false (nothing
 // launched) if not applicable
 bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
-  if (cand >= kNumPw * kNumLevels) return cand < pwgrad_num_cfgs() && hwgrad_launch(a, cand - kNumPw * kNumLevels, st);
+  if (cand >= kNumPw * kNumLevels)
+    return !a.dy2 && cand < pwgrad_num_cfgs() && hwgrad_launch(a, cand - kNumPw * kNumLevels, st);
   if (cand < 0 || cand >= kNumPw * kNumLevels) return false;
   const int c = cand % kNumPw, level = cand / kNumPw;
   if (a.Cout % 8 || a.K % 8 || a.M <= 0) return false;
   if (!a.dense && (a.C % 8 || a.R * a.S > 32)) return false;
   const PwCfg& g = kPw[c];
+  if (a.dy2 && (!a.dense || a.Cout1 % g.bco != 0 || !a.dw2 || a.ldd2 % 8)) return false;
   // skip shapes where most of the tile would be padding
   if (g.bco > 32 && a.Cout <= g.bco / 2) return false;
   if (g.bkk > 128 && a.K <= g.bkk / 2) return false;
@@ -657,7 +666,9 @@ bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
   if (splits < 1) splits = 1;
   long long per = (ksteps + splits - 1) / splits;
   // keep workgroup-relative byte offsets below 2^31 and pixel indices below 2^22
-  const long long row_bytes = (a.dense ? (a.ldx > a.ldd ? a.ldx : a.ldd) : a.ldd) * 2;
+  long long ldmax = a.dense ? (a.ldx > a.ldd ? a.ldx : a.ldd) : a.ldd;
+  if (a.dy2 && a.ldd2 > ldmax) ldmax = a.ldd2;
+  const long long row_bytes = ldmax * 2;
   long long cap = (0x7fffffffLL / row_bytes) / 64 - 1;
   if (!a.dense) {
     const long long HoWo = (long long)a.Ho * a.Wo;

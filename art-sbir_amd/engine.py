@@ -975,24 +975,25 @@ class Engine:
         Ms = Bs * H * W
         es = x.element_size()
         with torch.cuda.stream(side):
-            P = torch.zeros(G, co, ci, dtype=torch.float32, device=x.device)
-            gram = torch.zeros(G, ci, ci, dtype=torch.float32, device=x.device)
-            cs = torch.zeros(G, ci, dtype=torch.float32, device=x.device)
+            # [P | Gram | colsums] of every segment in one zeroed buffer, then the
+            # combine's workspace (W in f32, T = W Gram)
+            nP, nG = G * co * ci, G * ci * ci
+            buf = torch.zeros(nP + nG + G * ci, dtype=torch.float32, device=x.device)
+            P, gram, cs = buf[:nP].view(G, co, ci), buf[nP:nP + nG].view(G, ci, ci), buf[nP + nG:].view(G, ci)
+            wsp = torch.empty(co * ci * (G + 1), dtype=torch.float32, device=x.device)
             for s in range(G):
                 gs, xs = g[s * Bs:(s + 1) * Bs], x[s * Bs:(s + 1) * Bs]
-                call("artsbir_gemm_tn", self.dt, Ms, co, ci, ptr(gs), co, ptr(xs), ci, ptr(P[s]), _s(),
-                     kernel="auto", flops=2.0 * Ms * co * ci, nbytes=float(es * Ms * (co + ci) + 4 * co * ci),
-                     tag=f"wgrad_fold {Ms}x{co}x{ci}")
-                call("artsbir_gemm_tn", self.dt, Ms, ci, ci, ptr(xs), ci, ptr(xs), ci, ptr(gram[s]), _s(),
-                     kernel="auto", flops=2.0 * Ms * ci * ci, nbytes=float(es * Ms * ci + 4 * ci * ci),
-                     tag=f"gram {Ms}x{ci}")
+                # g_s^T x_s and x_s^T x_s, one launch (the x rows read once for both)
+                call("artsbir_gemm_tn2", self.dt, Ms, co, ci, ci, ptr(gs), co, ptr(xs), ci, ptr(xs), ci, ptr(P[s]),
+                     ptr(gram[s]), _s(), kernel="auto", flops=2.0 * Ms * (co + ci) * ci,
+                     nbytes=float(es * Ms * (co + ci) + 4 * (co + ci) * ci), tag=f"wgrad_fold {Ms}x{co}+{ci}x{ci}")
                 call("artsbir_colsum", self.dt, ptr(xs), Ms, ci, ci, ptr(cs[s]), _s())
             call("artsbir_bn_fold_wgrad_combine", self.dt, co, ci, G, ptr(P), ptr(gram), ptr(cs), ptr(fw), ptr(coef),
-                 ptr(st.buf), 4 * co, ptr(grads[conv.weight]), _s(), kernel="fold_wgrad_combine_kernel",
-                 flops=2.0 * G * co * ci * ci, nbytes=float(4 * G * (co * ci + ci * ci) + 8 * co * ci),
+                 ptr(st.buf), 4 * co, ptr(grads[conv.weight]), ptr(wsp), _s(), kernel="fold_combine",
+                 flops=2.0 * G * co * ci * ci, nbytes=float(4 * (G * (co * ci + ci * ci) + 3 * co * ci)),
                  tag=f"fold_combine {co}x{ci}")
         if side is not main:
-            self._side_keep.extend([g, x, coef, st.buf, P, gram, cs])
+            self._side_keep.extend([g, x, coef, st.buf, buf, wsp])
 
     def _block_bwd(self, blk, bp, c, dout, grads, ws, fused_res=None, prev=None):
         """backward of one Bottleneck.  dout: gradient of the block output, or —

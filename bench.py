@@ -125,6 +125,7 @@ def roofline(prof, peak_of, traffic_file=None):
     roofline time max(bytes / HBM peak, FLOPs / MFMA peak): a kernel name pools
     MFMA-bound and HBM-bound shapes, whose pooled GB/s or TFLOP/s alone
     understates both; sum(roofline time) / sum(time) does not."""
+    main_sid = torch.cuda.current_stream().cuda_stream
     agg = {}
     for kname, fl, nb, e0, e1, *_ in prof:
         a = agg.setdefault(kname, [0.0, 0.0, 0, 0.0, 0.0])
@@ -180,8 +181,9 @@ def roofline(prof, peak_of, traffic_file=None):
                                   "tflops": round(v[2] / (v[0] / 1e3) / 1e12, 1) if v[0] else None,
                                   "gbs": round(v[3] / (v[0] / 1e3) / 1e9, 1) if v[0] else None}
                               for f, v in sorted(fam.items(), key=lambda kv: -kv[1][0])},
-                 "streams_kernel_ms": {("main" if i == 0 else f"side{i}"): round(ms, 3) for i, (sid, ms) in
-                                       enumerate(sorted(streams.items(), key=lambda kv: -kv[1]))}})
+                 # the caller's stream (the step's main stream) by its handle, the others by theirs
+                 "streams_kernel_ms": {("main" if sid == main_sid else f"stream_{sid:x}"): round(ms, 3)
+                                       for sid, ms in sorted(streams.items(), key=lambda kv: -kv[1])}})
     return roof
 
 
@@ -190,15 +192,15 @@ def launch_family(kernel, tag):
     data gradients, plain data gradients, weight gradients (the overlapped side
     stream), the elementwise BatchNorm / ReLU / pool passes, everything else"""
     t = (tag or "").split(" ")[0]
-    if t.startswith("dgrad+bn"):
+    if t.startswith(("dgrad+bn", "dgrad_fold+bn")):
         return "bn_backward_dgrad"
-    if t == "dgrad":
+    if t in ("dgrad", "dgrad_fold"):
         return "dgrad"
-    if t in ("wgrad", "gemm_tn"):
+    if t in ("wgrad", "gemm_tn", "wgrad_fold", "gram", "fold_combine"):
         return "weight_gradient"
     if t in ("fwd", "fwd_act", "gemm_nt"):
         return "forward_gemm"
-    if t.startswith(("act_pool", "block_out", "bn_")):
+    if t.startswith(("act_pool", "block_out", "bn_", "fold_prep")):
         return "elementwise_bn"
     return "other"
 

@@ -84,6 +84,12 @@ int artsbir_gemm_nt_gate(long long M, int N, int K, const void* a, long long lda
 /* dw[n][k] += sum_m dy[m][n] * x[m][k]  (f32 atomics) — nn.Linear weight gradient. */
 int artsbir_gemm_tn(int dtype, long long M, int N, int K, const void* dy, long long ldd,
                     const void* x, long long ldx, float* dw, void* stream);
+/* Two weight-gradient GEMMs over one x in one launch (dense rows, bf16; f32 or a
+ * shape no pipelined kernel takes: two artsbir_gemm_tn):
+ * dw[n][k] += sum_m dy[m][n] x[m][k] (n < N1), dw2[n][k] += sum_m dy2[m][n] x[m][k]
+ * (n < N2) — the folded BatchNorm backward's g^T x and x^T x (csrc/fold.hip). */
+int artsbir_gemm_tn2(int dtype, long long M, int N1, int N2, int K, const void* dy, long long ldd, const void* dy2,
+                     long long ldd2, const void* x, long long ldx, float* dw, float* dw2, void* stream);
 
 /* data gradient of a stride-1 'same' convolution: dx[m][ci] = sum dy * flipped w
  * (wd = artsbir_pack_weight mode 1, [Cin][R][S][Cout]) (+ residual: res_mode 1 =
@@ -146,11 +152,12 @@ int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* wt, const fl
 /* The weight gradient of that conv: dw[co][ci] += sum_s c1_s[co] P_s[co][ci] +
  * b'_s[co] (W Gram_s)[co][ci] + k_s[co] colsums_s[ci], with P_s = g_s^T x_s
  * [nseg][Co][Ci], Gram_s = x_s^T x_s [nseg][Ci][Ci], colsums_s = 1^T x_s
- * [nseg][Ci] (f32, from artsbir_gemm_tn / artsbir_colsum), w the forward weight
- * [Co][Ci] (compute dtype), k = -c1 (c2 - c3 istd mean). */
+ * [nseg][Ci] (f32, from artsbir_gemm_tn2 / artsbir_colsum), w the forward weight
+ * [Co][Ci] (compute dtype), k = -c1 (c2 - c3 istd mean).  workspace: f32,
+ * Co * Ci * (nseg + 1) floats. */
 int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const float* P, const float* gram,
                                   const float* colsums, const void* w, const float* coef, const float* prm,
-                                  long long pstride, float* dw, void* stream);
+                                  long long pstride, float* dw, float* workspace, void* stream);
 
 /* ---- layout / parameter packing ---------------------------------------- */
 /* x.type(weight dtype) + NCHW -> NHWC8 (models.py:352); x [B][Cin<=8][H][W] f32. */

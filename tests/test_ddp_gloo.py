@@ -1,4 +1,4 @@
-"""The N>1 paths on CPU with the gloo backend, world_size 2:
+"""The N>1 paths on CPU with the gloo backend at world sizes 2, 4 and 8:
 gradient averaging over the flat gradient buffer (ddp.py), rank-0 parameter
 and BN-buffer broadcast, and the gallery-sharded retrieval protocol of
 knn.knn_sharded itself (owner's positive key -> all_reduce MAX, per-shard
@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-WORLD = 2
+WORLDS = [2, 4, 8]
 
 
 def _free_port():
@@ -25,19 +25,25 @@ def _free_port():
     return port
 
 
-def _run(fn, *args):
+def _run(fn, *args, world=2):
     port = _free_port()
-    mp.spawn(_entry, args=(fn, port, args), nprocs=WORLD, join=True)
+    mp.spawn(_entry, args=(fn, port, world, args), nprocs=world, join=True)
 
 
-def _entry(rank, fn, port, args):
+def _entry(rank, fn, port, world, args):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fn(rank, *args)
     finally:
         dist.destroy_process_group()
+
+
+def _mean_rank1():
+    """mean of rank + 1 over the ranks: what averaging a per-rank (rank + 1) gives"""
+    return (dist.get_world_size() + 1) / 2.0
 
 
 def _allreduce(rank):
@@ -46,12 +52,13 @@ def _allreduce(rank):
     flat = torch.arange(n, dtype=torch.float32) * (rank + 1)
     model = types.SimpleNamespace(_hip_engine=types.SimpleNamespace(_grads=types.SimpleNamespace(flat=flat)))
     ddp.allreduce_gradients(model, bucket_bytes=256)  # 64-element buckets, last one ragged
-    want = torch.arange(n, dtype=torch.float32) * 1.5
+    want = torch.arange(n, dtype=torch.float32) * _mean_rank1()
     assert torch.allclose(flat, want), (flat - want).abs().max()
 
 
-def test_allreduce_gradients_averages_flat_buffer():
-    _run(_allreduce)
+@pytest.mark.parametrize("world", WORLDS)
+def test_allreduce_gradients_averages_flat_buffer(world):
+    _run(_allreduce, world=world)
 
 
 def _broadcast(rank):
@@ -73,8 +80,9 @@ def _broadcast(rank):
             assert torch.all(b == 0)
 
 
-def test_broadcast_parameters_and_buffers():
-    _run(_broadcast)
+@pytest.mark.parametrize("world", [2, 4])
+def test_broadcast_parameters_and_buffers(world):
+    _run(_broadcast, world=world)
 
 
 def _cpu_local_search(queries, shard, k, positives, compute, g_base=0, dpos=None, metric="euclidean"):
@@ -109,18 +117,32 @@ def _cpu_positive_keys(queries, shard, g_base, positives, metric="euclidean"):
     return out
 
 
+def _ragged_bounds(n, world):
+    """shard boundaries of n rows over world ranks, ragged as a 1,000,000-row
+    gallery split 8 ways by whole batches is: odd sizes, and at world 8 one shard
+    shorter than the top-k list (5 rows)"""
+    b = [0] + [i * n // world + (13 if i % 2 else -21) for i in range(1, world)] + [n]
+    if world == 8:
+        b[3] = b[2] + 5
+    return b
+
+
 def _sharded(rank, k, metric):
     """knn.knn_sharded's own collective code (all_reduce MAX of the positives' keys,
     all_gather_into_tensor of the lists, merge, all_reduce SUM of the ranks) over
     gloo, with CPU stand-ins for the GPU search and merge"""
     import knn
     from oracle import retrieval as oret
+    world = dist.get_world_size()
     g, qs, pos = oret.synthetic_gallery(1000, 16, 32, seed_g=5, seed_q=6)
-    g[900:910] = g[0:10]  # duplicates straddling the shard boundary -> cross-shard ties
+    g[900:910] = g[0:10]  # duplicate rows in three shards (two at world 2) -> cross-shard ties
+    g[480:490] = g[0:10]
     qs[:4] = g[:4]
     pos = pos.copy()
     pos[5] = -1  # a query without a positive
-    bounds = [0, 537, 1000]  # ragged shards
+    pos[6] = 903  # positives among the duplicates
+    pos[7] = 484
+    bounds = _ragged_bounds(1000, world)
     lo, hi = bounds[rank], bounds[rank + 1]
     mi, md, rk = knn.knn_sharded(torch.from_numpy(qs), torch.from_numpy(g[lo:hi]), lo, k, torch.from_numpy(pos),
                                  metric=metric, local_search=_cpu_local_search, positive_keys=_cpu_positive_keys,
@@ -134,13 +156,15 @@ def _sharded(rank, k, metric):
             assert rk[i].item() == oret.rank_of(d_full, pos[i])
 
 
-def test_sharded_retrieval_protocol_matches_unsharded_oracle():
-    _run(_sharded, 10, "euclidean")
+@pytest.mark.parametrize("world", WORLDS)
+def test_sharded_retrieval_protocol_matches_unsharded_oracle(world):
+    _run(_sharded, 10, "euclidean", world=world)
 
 
-def test_sharded_retrieval_protocol_cosine_short_shard():
-    """cosine keys and k = 20 (the lists of both shards are merged by (key, index))"""
-    _run(_sharded, 20, "cosine")
+@pytest.mark.parametrize("world", WORLDS)
+def test_sharded_retrieval_protocol_cosine_short_shard(world):
+    """cosine keys and k = 20 (the lists of every shard are merged by (key, index))"""
+    _run(_sharded, 20, "cosine", world=world)
 
 
 def test_merge_topk_short_shards():
@@ -177,18 +201,19 @@ def _overlapped(rank):
         lo = b
     assert lo == n
     r.finish()
-    want = torch.arange(n, dtype=torch.float32) * 1.5
+    want = torch.arange(n, dtype=torch.float32) * _mean_rank1()
     assert torch.allclose(flat, want), (flat - want).abs().max()
     # a step whose backward never drove the reducer: finish() falls back to the plain all-reduce
     flat2 = torch.ones(50) * (rank + 1)
     model = types.SimpleNamespace(_hip_engine=types.SimpleNamespace(_grads=types.SimpleNamespace(flat=flat2)))
     r2 = ddp.OverlappedReducer(bucket_bytes=64, model=model)
     r2.finish()
-    assert torch.allclose(flat2, torch.full((50,), 1.5))
+    assert torch.allclose(flat2, torch.full((50,), _mean_rank1()))
 
 
-def test_overlapped_reducer_protocol():
-    _run(_overlapped)
+@pytest.mark.parametrize("world", WORLDS)
+def test_overlapped_reducer_protocol(world):
+    _run(_overlapped, world=world)
 
 
 class _ProjModel(torch.nn.Module):
@@ -246,9 +271,10 @@ def _sharded_inference(rank, tmp, metric):
     assert any(p < 0 for p in inference._positives(kag, ids.image_paths))  # sketches without a gallery photo
 
 
-@pytest.mark.parametrize("metric", ["euclidean", "cosine"])
-def test_sharded_gallery_inference_matches_unsharded(tmp_path, metric):
-    _run(_sharded_inference, str(tmp_path), metric)
+@pytest.mark.parametrize("world,metric", [(2, "euclidean"), (2, "cosine"), (4, "euclidean"), (8, "euclidean")])
+def test_sharded_gallery_inference_matches_unsharded(tmp_path, world, metric):
+    """13 gallery photos over 2 / 4 / 8 ranks: ragged, at world 8 some ranks hold one"""
+    _run(_sharded_inference, str(tmp_path), metric, world=world)
 
 
 def _allreduce_autograd_model(rank):
@@ -261,20 +287,22 @@ def _allreduce_autograd_model(rank):
         p.grad = torch.full(p.shape, float((rank + 1) * (i + 1)))
     m[1].bias.grad = None  # a parameter without a gradient is skipped
     ddp.allreduce_gradients(m, bucket_bytes=64)  # several buckets, split at tensor boundaries
+    mr = _mean_rank1()
     for i, p in enumerate(m.parameters()):
         if p.grad is not None:
-            assert torch.allclose(p.grad, torch.full(p.shape, 1.5 * (i + 1))), i
+            assert torch.allclose(p.grad, torch.full(p.shape, mr * (i + 1))), i
     ts = [torch.arange(5, dtype=torch.float64) * (rank + 1), torch.ones(3, dtype=torch.bfloat16) * (rank + 1)]
     ddp.allreduce_tensors(ts, bucket_bytes=1 << 20)  # a dtype change starts a new bucket
-    assert torch.allclose(ts[0], torch.arange(5, dtype=torch.float64) * 1.5)
-    assert torch.allclose(ts[1].float(), torch.full((3,), 1.5))
+    assert torch.allclose(ts[0], torch.arange(5, dtype=torch.float64) * mr)
+    assert torch.allclose(ts[1].float(), torch.full((3,), mr), rtol=1e-2)
     r = ddp.attach_overlapped_reducer(m)  # no engine: finish() is the plain coalesced all-reduce
     for p in m.parameters():
         if p.grad is not None:
             p.grad.fill_(float(rank))
     r.finish()
-    assert all(torch.allclose(p.grad, torch.full(p.shape, 0.5)) for p in m.parameters() if p.grad is not None)
+    assert all(torch.allclose(p.grad, torch.full(p.shape, mr - 1)) for p in m.parameters() if p.grad is not None)
 
 
-def test_allreduce_gradients_without_engine():
-    _run(_allreduce_autograd_model)
+@pytest.mark.parametrize("world", WORLDS)
+def test_allreduce_gradients_without_engine(world):
+    _run(_allreduce_autograd_model, world=world)

@@ -255,7 +255,44 @@ def test_wgrad_fold_combine(case, dtype, dev):
     init = torch.randn(Co, Ci)
     dw = init.clone().to(dev)
     cd, pd = coef.to(dev), prm.to(dev)
+    ws = torch.empty(Co * Ci * (G + 1), device=dev)
     _hip.call("artsbir_bn_fold_wgrad_combine", _hip.dtype_code(dtype), Co, Ci, G, P.data_ptr(), gram.data_ptr(),
-              cs.data_ptr(), wd.data_ptr(), cd.data_ptr(), pd.data_ptr(), 4 * Co, dw.data_ptr(), _hip.stream())
+              cs.data_ptr(), wd.data_ptr(), cd.data_ptr(), pd.data_ptr(), 4 * Co, dw.data_ptr(), ws.data_ptr(),
+              _hip.stream())
     torch.cuda.synchronize()
     assert _rel(dw.double().cpu() - init.double(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("cfg", ["auto", "100", "101", "102", "1", "2", "3", "7", "12", "-1"])
+@pytest.mark.parametrize("M,N1,N2", [(3000, 256, 64), (5000, 512, 128), (777, 1024, 256), (4096, 2048, 512)])
+def test_gemm_tn2(M, N1, N2, cfg, dev):
+    """artsbir_gemm_tn2: g^T x and x^T x in one launch (dY in two parts along
+    Cout) on the forced weight-gradient candidate, vs torch float64"""
+    import _kernels
+    old = os.environ.get("ARTSBIR_WGRAD_CFG")
+    if cfg == "auto":
+        os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+    else:
+        os.environ["ARTSBIR_WGRAD_CFG"] = cfg
+    try:
+        g = torch.Generator().manual_seed(17)
+        dy = torch.randn(M, N1, generator=g).bfloat16()
+        x = torch.randn(M, N2, generator=g).bfloat16()
+        ref1 = dy.double().T @ x.double()
+        ref2 = x.double().T @ x.double()
+        init1, init2 = torch.randn(N1, N2, generator=g), torch.randn(N2, N2, generator=g)
+        dw, dw2 = init1.clone().to(dev), init2.clone().to(dev)
+        dyd, xd = dy.to(dev), x.to(dev)
+        _hip.call("artsbir_gemm_tn2", _hip.DT_BF16, M, N1, N2, N2, dyd.data_ptr(), N1, xd.data_ptr(), N2, xd.data_ptr(),
+                  N2, dw.data_ptr(), dw2.data_ptr(), _hip.stream())
+        torch.cuda.synchronize()
+        if cfg not in ("auto", "-1"):
+            # the forced candidate takes both parts in one launch, or the split fallback ran it twice
+            _kernels.require(cfg, wgrad=True)
+        assert _rel(dw.double().cpu() - init1.double(), ref1) < 1e-4
+        assert _rel(dw2.double().cpu() - init2.double(), ref2) < 1e-4
+    finally:
+        if old is None:
+            os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+        else:
+            os.environ["ARTSBIR_WGRAD_CFG"] = old

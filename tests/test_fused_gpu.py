@@ -11,10 +11,11 @@ import torch
 import torch.nn.functional as F
 
 import _hip
+import _kernels
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "22", "23", "-2"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "22", "-2"]
 
 
 @pytest.fixture
@@ -32,11 +33,6 @@ def _set(cfg):
         os.environ.pop("ARTSBIR_PGEMM_CFG", None)
     else:
         os.environ["ARTSBIR_PGEMM_CFG"] = cfg
-    # candidate 23 (persistent pp256): 8 workgroups, so these small shapes walk several tiles each
-    if cfg == "23":
-        os.environ["ARTSBIR_PP_GRID"] = "8"
-    else:
-        os.environ.pop("ARTSBIR_PP_GRID", None)
 
 
 def _nhwc(x):
@@ -72,6 +68,7 @@ def test_conv_fwd_segment_stats(case, cfg, dev, cfg_env):
     _hip.call("artsbir_conv2d_fwd_seg", d, xd.data_ptr(), wd.data_ptr(), y.data_ptr(), G, stats.data_ptr(),
               _hip.stream())
     torch.cuda.synchronize()
+    _kernels.require(cfg)
     out = y.float().cpu().view(N, H, W, Co).permute(0, 3, 1, 2)
     assert torch.allclose(out, ref, atol=3e-2, rtol=1e-2), (out - ref).abs().max()
     s = stats.sum(1).cpu()
@@ -165,6 +162,7 @@ def test_dgrad_fused_bn_reduce(case, cfg, bits, dev, cfg_env):
     _hip.call("artsbir_conv2d_dgrad_bnb", d, dyd.data_ptr(), wdflip.data_ptr(), dx.data_ptr(),
               resd.data_ptr() if resd is not None else None, rm, desc, G, 4 * Ci, _hip.stream())
     torch.cuda.synchronize()
+    _kernels.require(cfg)
     got = dx.float().cpu()
     flat = lambda t: t.permute(0, 2, 3, 1).reshape(-1, Ci)  # noqa: E731
     per = N // G * H * W

@@ -8,6 +8,7 @@ import torch
 import torch.nn.functional as F
 
 import _hip
+import _kernels
 
 pytestmark = pytest.mark.gpu
 
@@ -28,7 +29,7 @@ CASES = [
     (2, 32, 16, 32, 64, 3, 3, 1, 1),    # halo-tiled, 16 x 16 tiles, 32 -> 64 channels
     (3, 17, 23, 64, 32, 3, 3, 1, 1),    # halo-tiled, 8 x 16 tiles with row and column tails
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21", "22", "23"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21", "22"]
 
 
 @pytest.fixture
@@ -46,11 +47,6 @@ def _set(cfg):
         os.environ.pop("ARTSBIR_PGEMM_CFG", None)
     else:
         os.environ["ARTSBIR_PGEMM_CFG"] = cfg
-    # candidate 23 (persistent pp256): 8 workgroups, so these small shapes walk several tiles each
-    if cfg == "23":
-        os.environ["ARTSBIR_PP_GRID"] = "8"
-    else:
-        os.environ.pop("ARTSBIR_PP_GRID", None)
 
 
 def _nhwc(x):
@@ -75,6 +71,7 @@ def test_pgemm_fwd_stats(case, cfg, dev, cfg_env):
     _hip.call("artsbir_conv2d_fwd", d, xd.data_ptr(), wd.data_ptr(), y.data_ptr(), Co, 0, 0, None, None, None, 0,
               stats.data_ptr(), _hip.stream())
     torch.cuda.synchronize()
+    _kernels.require(cfg)
     out = y.float().cpu().view(N, Ho, Wo, Co).permute(0, 3, 1, 2)
     assert torch.isfinite(out).all()
     assert torch.allclose(out, ref, atol=2e-2, rtol=1e-2), (out - ref).abs().max()
@@ -124,6 +121,7 @@ def test_pgemm_dgrad_residual(case, cfg, dev, cfg_env):
     _hip.call("artsbir_conv2d_dgrad", d, dyd.data_ptr(), wdd.data_ptr(), dx.data_ptr(),
               resd.data_ptr() if resd is not None else None, rm, _hip.stream())
     torch.cuda.synchronize()
+    _kernels.require(cfg)
     out = dx.float().cpu().view(N, H, W, Ci).permute(0, 3, 1, 2)
     assert torch.isfinite(out).all()
     assert torch.allclose(out, ref, atol=2e-2, rtol=1e-2), (out - ref).abs().max()
@@ -175,6 +173,7 @@ def test_wgrad_accumulates(case, cfg, dev):
         _hip.call("artsbir_conv2d_wgrad", d, dyd.data_ptr(), xd.data_ptr(), None, None, 0, dw.data_ptr(),
                   _hip.stream())
         torch.cuda.synchronize()
+        _kernels.require(cfg, wgrad=True)
         assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
     finally:
         if old is None:
@@ -197,6 +196,7 @@ def test_gemm_tn_strided(M, N, K, ldd, ldx, cfg, dev):
         _hip.call("artsbir_gemm_tn", _hip.DT_BF16, M, N, K, dyd.data_ptr(), ldd, xd.data_ptr(), ldx, dw.data_ptr(),
                   _hip.stream())
         torch.cuda.synchronize()
+        _kernels.require(cfg, wgrad=True)
         assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
     finally:
         os.environ.pop("ARTSBIR_WGRAD_CFG", None)
@@ -241,6 +241,7 @@ def test_conv_fwd_act(case, cfg, mode, dev, cfg_env):
                   resd.data_ptr() if resd is not None else None, 1 if resd is not None else 0,
                   0 if mode == "bias" else 1, _hip.stream())
     torch.cuda.synchronize()
+    _kernels.require(cfg)
     out = y.float().cpu().permute(0, 3, 1, 2)
     assert torch.allclose(out, ref, atol=3e-2, rtol=1e-2), (out - ref).abs().max()
 

@@ -399,6 +399,8 @@ def test_gemm_nt_gate_matches_gemm_then_quickgelu_bwd(M, N, K, cfg, dev, monkeyp
     slots = torch.zeros(_hip.NSLOT, 2, N, device=dev)
     _hip.call("artsbir_gemm_nt_gate", M, N, K, a.data_ptr(), K, b.data_ptr(), out.data_ptr(), N, x.data_ptr(),
               slots.data_ptr(), _hip.stream())
+    import _kernels
+    _kernels.require(cfg)
     xd = x.double().cpu()
     sg = torch.sigmoid(1.702 * xd)
     ref = (a.double().cpu() @ b.double().cpu().T) * (sg + 1.702 * xd * sg * (1 - sg))

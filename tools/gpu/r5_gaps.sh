@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5: main-stream idle gaps and the weight-gradient tail of the C2 step,
+# with and without the folded BN backward, overlapped and main stream alone
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+for f in 1 0; do
+  for m in overlap skip; do
+    ARTSBIR_FOLD_BN=$f timeout -k 10 300 python -u tools/step_gaps.py --mode $m > gpurun_out/r5_gaps_f${f}_$m.txt 2>&1 || { echo FAIL $f $m; tail -20 gpurun_out/r5_gaps_f${f}_$m.txt; exit 1; }
+    head -4 gpurun_out/r5_gaps_f${f}_$m.txt
+  done
+done
