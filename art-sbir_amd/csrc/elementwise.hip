@@ -832,46 +832,54 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ slots, int C, d
 
 // ------------------------------------------------------------------ colsum
 // out[c] += sum_{r<rows} x[r*ld + c]   (x is T or f32): a 256-thread block owns
-// 512 columns (64 lanes x 8) of a strip of rows; its 4 waves take every 4th
-// row, 4 rows in flight per lane, then one LDS reduction and ONE atomic per
-// column per block (few blocks per column: the atomics on one address
+// up to 512 columns (CPR 8-column chunks) of a strip of rows; a wave reads
+// 64 / CPR rows per instruction (narrow tensors — 64 columns: 8 rows — keep every
+// lane busy), 8 rows in flight per lane, then one LDS reduction and ONE atomic
+// per column per block (few blocks per column: the atomics on one address
 // serialise in the memory-side atomic unit)
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, long long rows, long long ld, long long C,
                                                      long long rows_per_block, float* __restrict__ out) {
-  __shared__ float red[3][512];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long long c0 = (long long)blockIdx.x * 512 + lane * 8;
-  const bool cok = c0 < C;
+  __shared__ float red[256][9];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long cb = (long long)blockIdx.x * 512;
+  const long long cw = C - cb < 512 ? C - cb : 512;  // columns of this block
+  const int cpr = (int)(cw / 8);                     // 8-column chunks per row
+  const int rpw = cpr >= 64 ? 1 : 64 / cpr;          // rows per wave instruction
+  const int rr = lane / cpr, cc = lane - rr * cpr;
+  const bool on = rr < rpw;
+  const long long c0 = cb + cc * 8;
   long long r0 = blockIdx.y * rows_per_block, r1 = r0 + rows_per_block;
   if (r1 > rows) r1 = rows;
+  const long long step = 4LL * rpw;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (cok) {
-    long long r = r0 + w;
-    for (; r + 28 < r1; r += 32) {
+  if (on) {
+    long long r = r0 + w * rpw + rr;
+    for (; r + 7 * step < r1; r += 8 * step) {
       float v[8][8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) load8<T>(x + (r + 4 * u) * ld + c0, v[u]);
+      for (int u = 0; u < 8; ++u) load8<T>(x + (r + u * step) * ld + c0, v[u]);
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         acc[e] += ((v[0][e] + v[1][e]) + (v[2][e] + v[3][e])) + ((v[4][e] + v[5][e]) + (v[6][e] + v[7][e]));
     }
-    for (; r < r1; r += 4) {
+    for (; r < r1; r += step) {
       float v[8];
       load8<T>(x + r * ld + c0, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += v[e];
     }
   }
-  if (w > 0) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[w - 1][lane * 8 + e] = acc[e];
-  }
+  for (int e = 0; e < 8; ++e) red[tid][e] = on ? acc[e] : 0.f;
   __syncthreads();
-  if (w == 0 && cok) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      atomicAdd(out + c0 + e, acc[e] + red[0][lane * 8 + e] + red[1][lane * 8 + e] + red[2][lane * 8 + e]);
+  // column chunk q: the threads (wave, row slot) that read it
+  for (int q = tid; q < cpr * 8; q += 256) {
+    const int ch = q >> 3, e = q & 7;
+    float s = 0.f;
+    for (int ww = 0; ww < 4; ++ww)
+      for (int r = 0; r < rpw; ++r) s += red[ww * 64 + r * cpr + ch][e];
+    atomicAdd(out + cb + q, s);
   }
 }
 

@@ -85,9 +85,133 @@ __global__ void __launch_bounds__(256) fold_wgrad_combine_kernel(const float* __
   *reinterpret_cast<float4*>(dw + (long long)co * Ci + ci) = acc;
 }
 
+// C[m][n] (ldc) = sum_k A[m][k] B[n][k] for the two small GEMMs of the fold
+// (the x-side weights W^T diag(b') W; T = W Gram in the weight gradient), with a
+// footprint that lets it share a CU with the other stream's GEMM workgroups: a
+// 64 x 64 tile per 4-wave workgroup, 32-k LDS stages double-buffered in 16 KB
+// (24 KB with an f32 B) — the 128-160 KB tiles of the pipelined kernels wait for
+// a CU the weight gradients have left, which cost these ~20-50 us GEMMs ~150 us
+// each in the step.  A bf16 [M][K]; B bf16, or f32 split into two bf16 parts
+// (hi + lo, so the f32 Gram matrices keep ~16 significant bits) [N][K]; f32
+// accumulation on v_mfma_f32_16x16x32_bf16; output bf16 or f32.  M, N % 64 == 0,
+// K % 32 == 0.
+__device__ __forceinline__ int fg_slot(int row, int chunk) { return chunk ^ ((row >> 2) & 2); }
+
+template <bool BF32, bool OF32>
+__global__ void __launch_bounds__(256) fold_gemm_kernel(const bf16* __restrict__ A, long long lda,
+                                                        const void* __restrict__ Bv, long long ldb, void* C,
+                                                        long long ldc, int M, int N, int K) {
+  constexpr int NB = BF32 ? 2 : 1;  // B parts (hi, lo)
+  __shared__ __attribute__((aligned(16))) char smem[2][(1 + NB) * 64 * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntn = N / 64;
+  const int m0 = (blockIdx.x / ntn) * 64, n0 = (blockIdx.x % ntn) * 64;
+  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
+  const int lr = tid >> 2, lc = tid & 3;  // loader: row, 16-B chunk of a 64-B row
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 ra, rb[NB];
+  auto load = [&](int k0) {
+    ra = *reinterpret_cast<const uint4*>(A + (long long)(m0 + lr) * lda + k0 + lc * 8);
+    if constexpr (BF32) {
+      const float* bp = reinterpret_cast<const float*>(Bv) + (long long)(n0 + lr) * ldb + k0 + lc * 8;
+      const float4 f0 = *reinterpret_cast<const float4*>(bp), f1 = *reinterpret_cast<const float4*>(bp + 4);
+      const float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      bf16 hi[8], lo[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hi[e] = (bf16)f[e];
+        lo[e] = (bf16)(f[e] - (float)hi[e]);
+      }
+      rb[0] = *reinterpret_cast<const uint4*>(hi);
+      rb[NB - 1] = *reinterpret_cast<const uint4*>(lo);
+    } else {
+      rb[0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16*>(Bv) + (long long)(n0 + lr) * ldb + k0 + lc * 8);
+    }
+  };
+  auto store = [&](int buf) {
+    char* s = smem[buf];
+    const int o = lr * 64 + (fg_slot(lr, lc) << 4);
+    *reinterpret_cast<uint4*>(s + o) = ra;
+#pragma unroll
+    for (int p = 0; p < NB; ++p) *reinterpret_cast<uint4*>(s + (1 + p) * 4096 + o) = rb[p];
+  };
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nk = K / 32;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load((kt + 1) * 32);
+    const char* s = smem[cur];
+    uint4 af[2], bfr[NB][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = wm + 16 * i + fr;
+      af[i] = *reinterpret_cast<const uint4*>(s + r * 64 + (fg_slot(r, fq) << 4));
+    }
+#pragma unroll
+    for (int p = 0; p < NB; ++p)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = wn + 16 * j + fr;
+        bfr[p][j] = *reinterpret_cast<const uint4*>(s + (1 + p) * 4096 + r * 64 + (fg_slot(r, fq) << 4));
+      }
+#pragma unroll
+    for (int p = 0; p < NB; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&bfr[p][j]),
+                                                              *reinterpret_cast<const bf16x8*>(&af[i]), acc[i][j], 0,
+                                                              0, 0);
+    if (kt + 1 < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  // acc[i][j][r]: row m = m0 + wm + 16 i + fr, column n = n0 + wn + 16 j + 4 fq + r
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const long long m = m0 + wm + 16 * i + fr;
+      const int n = n0 + wn + 16 * j + 4 * fq;
+      if constexpr (OF32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(C) + m * ldc + n) =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      } else {
+        bf16 o[4] = {(bf16)acc[i][j][0], (bf16)acc[i][j][1], (bf16)acc[i][j][2], (bf16)acc[i][j][3]};
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(C) + m * ldc + n) = *reinterpret_cast<const uint2*>(o);
+      }
+    }
+}
+
 }  // namespace artsbir
 
 using namespace artsbir;
+
+// the fold's small GEMMs on fold_gemm_kernel where the shape allows, else artsbir_gemm_nt
+static int fold_gemm(int dtype, bool b_f32, int M, int N, int K, const void* a, long long lda, const void* b,
+                     long long ldb, void* c, long long ldc, bool out_f32, hipStream_t st) {
+  const bool ok = dtype == ARTSBIR_DT_BF16 && M % 64 == 0 && N % 64 == 0 && K % 32 == 0 && lda % 8 == 0 &&
+                  ldb % 8 == 0 && ldc % 4 == 0 && (long long)(M / 64) * (N / 64) < 0x7fffffffLL;
+  if (!ok) {
+    if (b_f32 && dtype == ARTSBIR_DT_BF16) { set_error("fold_gemm: f32 B needs 64-multiple shapes"); return -1; }
+    return artsbir_gemm_nt(dtype, M, N, K, a, lda, b, c, ldc, out_f32 ? 1 : 0, 0, nullptr, nullptr, st);
+  }
+  const dim3 g((unsigned)((M / 64) * (N / 64)));
+  const bf16* A = reinterpret_cast<const bf16*>(a);
+  if (b_f32 && out_f32) hipLaunchKernelGGL((fold_gemm_kernel<true, true>), g, dim3(256), 0, st, A, lda, b, ldb, c, ldc, M, N, K);
+  else if (b_f32) hipLaunchKernelGGL((fold_gemm_kernel<true, false>), g, dim3(256), 0, st, A, lda, b, ldb, c, ldc, M, N, K);
+  else if (out_f32) hipLaunchKernelGGL((fold_gemm_kernel<false, true>), g, dim3(256), 0, st, A, lda, b, ldb, c, ldc, M, N, K);
+  else hipLaunchKernelGGL((fold_gemm_kernel<false, false>), g, dim3(256), 0, st, A, lda, b, ldb, c, ldc, M, N, K);
+  ARTSBIR_CHECK_LAUNCH("fold_gemm");
+  return 0;
+}
 
 extern "C" int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* wt, const float* coef,
                                         const float* prm, long long pstride, int nseg, void* wout, float* bias,
@@ -109,8 +233,8 @@ extern "C" int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* w
   // the x-side weights W^T diag(b') W of every segment in one GEMM: rows s*Ci + ci
   // of A times W^T (as [N = Ci][K = Co]) into columns Co.. of wout's rows
   const size_t es = dtype == ARTSBIR_DT_BF16 ? 2 : 4;
-  return artsbir_gemm_nt(dtype, (long long)nseg * Ci, Ci, Co, amat, Co, wt,
-                         reinterpret_cast<char*>(wout) + Co * es, Co + Ci, 0, 0, nullptr, nullptr, stream);
+  return fold_gemm(dtype, false, nseg * Ci, Ci, Co, amat, Co, wt, Co, reinterpret_cast<char*>(wout) + Co * es, Co + Ci,
+                   false, st);
 }
 
 extern "C" int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const float* P, const float* gram,
@@ -123,18 +247,21 @@ extern "C" int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg
     return -1;
   }
   hipStream_t st = (hipStream_t)stream;
-  // T = W [Gram_0 | ... ] in f32 (the Gram matrices are [nseg * Ci][Ci] rows, symmetric)
-  const float* wf = reinterpret_cast<const float*>(w);
+  // T = W [Gram_0 | ... ] (the Gram matrices are [nseg * Ci][Ci] rows, symmetric):
+  // bf16 W against the f32 Gram split into two bf16 parts, f32 out; in the f32
+  // mode an f32 GEMM
   float* T = workspace;
-  if (dtype == ARTSBIR_DT_BF16) {
+  if (dtype == ARTSBIR_DT_BF16 && (Co % 64 || Ci % 64)) {
+    // shapes off the 64-tile (small test models): W in f32, one f32 GEMM
     float* wc = workspace;
     T = workspace + (long long)Co * Ci;
     if (artsbir_cast(ARTSBIR_DT_BF16, w, ARTSBIR_DT_F32, wc, (long long)Co * Ci, stream)) return -1;
-    wf = wc;
-  }
-  if (artsbir_gemm_nt(ARTSBIR_DT_F32, Co, nseg * Ci, Ci, wf, Ci, gram, T, (long long)nseg * Ci, 1, 0, nullptr, nullptr,
-                      stream))
+    if (artsbir_gemm_nt(ARTSBIR_DT_F32, Co, nseg * Ci, Ci, wc, Ci, gram, T, (long long)nseg * Ci, 1, 0, nullptr,
+                        nullptr, stream))
+      return -1;
+  } else if (fold_gemm(dtype, true, Co, nseg * Ci, Ci, w, Ci, gram, Ci, T, (long long)nseg * Ci, true, st)) {
     return -1;
+  }
   const long long n = (long long)Co * (Ci / 4);
   hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, T, colsums, Co,
                      Ci, nseg, coef, prm, pstride, dw);

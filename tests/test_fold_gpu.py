@@ -296,3 +296,21 @@ def test_gemm_tn2(M, N1, N2, cfg, dev):
             os.environ.pop("ARTSBIR_WGRAD_CFG", None)
         else:
             os.environ["ARTSBIR_WGRAD_CFG"] = old
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("rows,C,ld", [(100000, 64, 64), (5000, 128, 128), (777, 256, 264), (3000, 320, 320),
+                                       (4000, 768, 768), (1000, 1544, 1552), (33, 8, 8)])
+def test_colsum_narrow_and_wide(rows, C, ld, dtype, dev):
+    """artsbir_colsum (the fold's column sums of x; the bias gradients) for narrow
+    tensors (a wave reads 64 / (C / 8) rows per instruction), ragged row counts,
+    strided rows and column tails of the 512-column blocks; it accumulates"""
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(rows, ld, generator=g).to(dtype)
+    init = torch.randn(C, generator=g)
+    out = init.clone().to(dev)
+    xd = x.to(dev)
+    _hip.call("artsbir_colsum", _hip.dtype_code(dtype), xd.data_ptr(), rows, ld, C, out.data_ptr(), _hip.stream())
+    torch.cuda.synchronize()
+    ref = init.double() + x[:, :C].double().sum(0)
+    assert _rel(out.double().cpu() - init.double(), ref - init.double()) < 1e-5

@@ -6,7 +6,7 @@ event), then per stream the busy time, and on the main stream the idle gaps
 (> --gap us) with the launch that ended each one — the final join with the
 weight-gradient stream shows as the gap before the optimizer.
 
-    python tools/step_gaps.py [--batch 384] [--gap 20] [--tune-cache F] [--mode overlap|skip]
+    python tools/step_gaps.py [--batch 384] [--gap 20] [--tune-cache F] [--mode overlap|skip|serial]
 """
 import argparse
 import collections
@@ -25,13 +25,15 @@ def main():
     ap.add_argument("--batch", type=int, default=384)
     ap.add_argument("--gap", type=float, default=20.0)
     ap.add_argument("--tune-cache", default=os.path.join(ROOT, "profiles", "tune_r4.txt"))
-    ap.add_argument("--mode", default="overlap", choices=["overlap", "skip"])
+    ap.add_argument("--mode", default="overlap", choices=["overlap", "skip", "serial"])
     ap.add_argument("--side-tail", type=int, default=25, help="side-stream launches listed after main's last one")
+    ap.add_argument("--by-tag", type=int, default=0, help="also list the N largest (kernel, tag) groups")
     args = ap.parse_args()
     import _hip
     import bench
     import engine
     engine.SKIP_WGRAD[0] = args.mode == "skip"
+    engine.OVERLAP_WGRAD = args.mode != "serial"  # serial: the weight gradients in order on the main stream
     import losses
     import models
     import optim
@@ -107,6 +109,22 @@ def main():
               f"{len(after)} launches, {sum(min(e - s, e - lastmain_bwd) for s, e, *_ in after):.2f} ms")
         for s, e, k, t, sid in after[:args.side_tail]:
             print(f"    {s:8.2f} - {e:8.2f} ms  {k:40s} {t}")
+    if args.by_tag:
+        _by_tag(rows, args.by_tag)
+
+
+def _by_tag(rows, n):
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for s, e, k, t, sid in rows:
+        a = agg[(k, t)]
+        a[0] += 1
+        a[1] += e - s
+    fam = collections.defaultdict(float)
+    for (k, t), (c, ms) in agg.items():
+        fam[t.split(" ")[0]] += ms
+    print("  per tag family (ms): " + ", ".join(f"{f} {v:.2f}" for f, v in sorted(fam.items(), key=lambda x: -x[1])))
+    for (k, t), (c, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:n]:
+        print(f"    {ms:7.3f} ms {c:3d}x  {k:40s} {t}")
 
 
 if __name__ == "__main__":
