@@ -313,14 +313,22 @@ __global__ void act_pool_kernel(const T* __restrict__ x, const float* __restrict
 // (BN parameters loaded once, no per-element index division) and UN units per
 // trip with every load issued before the trip's stores; segment = blockIdx.y
 // (Bs images each), units = output pixels.  C / 8 <= 256.
-template <typename T, int P>
+// CS: also the column sums of the stored output per segment, into one of
+// ARTSBIR_NSLOT replica rows of colsum[s][slot][C] (the folded BatchNorm
+// backward's 1^T x of the next conv's input, csrc/fold.hip: no extra pass over x)
+template <typename T, int P, bool CS = false>
 __global__ void __launch_bounds__(256) act_pool_cg_kernel(const T* __restrict__ x, const float* __restrict__ bn,
                                                           int relu, int Bs, int H, int W, int C, int units_per_block,
-                                                          T* __restrict__ out) {
+                                                          T* __restrict__ out, float* __restrict__ colsum = nullptr) {
   const int s = blockIdx.y;
   const int CG = C / 8, RL = 256 / CG;
   const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
-  if (rl >= RL) return;
+  float csum[CS ? 8 : 1];
+  if constexpr (CS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  }
+  if (!CS && rl >= RL) return;
   const int Ho = H / P, Wo = W / P;
   const int units = Bs * Ho * Wo;
   const T* xs = x + (long long)s * Bs * H * W * C + cg * 8;
@@ -330,7 +338,7 @@ __global__ void __launch_bounds__(256) act_pool_cg_kernel(const T* __restrict__ 
   const int u0 = blockIdx.x * units_per_block;
   const int u1 = min(u0 + units_per_block, units);
   constexpr int UN = P == 1 ? 4 : 2;
-  for (int ub = u0 + rl; ub < u1; ub += RL * UN) {
+  for (int ub = u0 + rl; rl < RL && ub < u1; ub += RL * UN) {
     float v[UN][P * P][8];
 #pragma unroll
     for (int i = 0; i < UN; ++i) {
@@ -363,6 +371,22 @@ __global__ void __launch_bounds__(256) act_pool_cg_kernel(const T* __restrict__ 
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] *= inv;
       store8<T>(os + (long long)(ub + i * RL) * C, acc);
+      if constexpr (CS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += to_f(from_f<T>(acc[e]));  // the stored values
+      }
+    }
+  }
+  if constexpr (CS) {  // the RL lanes of each channel group, then one atomic per channel
+    __shared__ float red[256][9];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[threadIdx.x][e] = rl < RL ? csum[e] : 0.f;
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const int g = c >> 3, e = c & 7;
+      float t = 0.f;
+      for (int r = 0; r < RL; ++r) t += red[r * CG + g][e];
+      atomicAdd(colsum + ((long long)s * ARTSBIR_NSLOT + blockIdx.x % ARTSBIR_NSLOT) * C + c, t);
     }
   }
 }
@@ -1136,8 +1160,8 @@ extern "C" int artsbir_bn_stats_det(int dtype, const void* y, int nseg, long lon
   return 0;
 }
 
-extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W,
-                                int C, int nseg, void* out, void* stream) {
+extern "C" int artsbir_act_pool_colsum(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H,
+                                       int W, int C, int nseg, void* out, float* colsum, void* stream) {
   if (C % 8) { set_error("act_pool: C %% 8 != 0"); return -1; }
   if (nseg < 1 || B % nseg) { set_error("act_pool: %d segments do not split %d images", nseg, B); return -1; }
   if (pool > 1 && (H % pool || W % pool)) { set_error("act_pool: H,W not divisible by pool"); return -1; }
@@ -1147,19 +1171,33 @@ extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int r
   if (C / 8 <= 256 && (pool <= 1 || pool == 2) && units * C < (1LL << 40) && units < 0x7fffffffLL) {
     const int upb = cg_units_per_block(units, nseg, C);
     const dim3 g((unsigned)((units + upb - 1) / upb), (unsigned)nseg);
-    if (pool == 2)
-      DISPATCH_T(dtype, hipLaunchKernelGGL((act_pool_cg_kernel<T, 2>), g, dim3(256), 0, (hipStream_t)stream,
-                                           (const T*)x, bn, relu, B / nseg, H, W, C, upb, (T*)out));
-    else
-      DISPATCH_T(dtype, hipLaunchKernelGGL((act_pool_cg_kernel<T, 1>), g, dim3(256), 0, (hipStream_t)stream,
-                                           (const T*)x, bn, relu, B / nseg, H, W, C, upb, (T*)out));
+#define AP_GO(PV, CSV)                                                                                        \
+  DISPATCH_T(dtype, hipLaunchKernelGGL((act_pool_cg_kernel<T, PV, CSV>), g, dim3(256), 0, (hipStream_t)stream, \
+                                       (const T*)x, bn, relu, B / nseg, H, W, C, upb, (T*)out, colsum))
+    if (pool == 2 && colsum) AP_GO(2, true);
+    else if (pool == 2) AP_GO(2, false);
+    else if (colsum) AP_GO(1, true);
+    else AP_GO(1, false);
+#undef AP_GO
     ARTSBIR_CHECK_LAUNCH("act_pool");
     return 0;
   }
   DISPATCH_T(dtype, hipLaunchKernelGGL(act_pool_kernel<T>, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
                                        (const T*)x, bn, relu, pool > 1 ? pool : 0, B, H, W, C, nseg, (T*)out));
   ARTSBIR_CHECK_LAUNCH("act_pool");
+  if (colsum) {  // the generic kernel's shapes: a column-sum pass per segment into replica row 0
+    const long long seg_rows = (long long)(B / nseg) * Ho * Wo, es = dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+    for (int s = 0; s < nseg; ++s)
+      if (artsbir_colsum(dtype, reinterpret_cast<const char*>(out) + s * seg_rows * C * es, seg_rows, C, C,
+                         colsum + (long long)s * ARTSBIR_NSLOT * C, stream))
+        return -1;
+  }
   return 0;
+}
+
+extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W,
+                                int C, int nseg, void* out, void* stream) {
+  return artsbir_act_pool_colsum(dtype, x, bn, relu, pool, B, H, W, C, nseg, out, nullptr, stream);
 }
 
 extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,

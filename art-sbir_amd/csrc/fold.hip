@@ -60,8 +60,8 @@ __global__ void __launch_bounds__(256) fold_prep_kernel(const T* __restrict__ wt
 // values of one dW row per thread
 __global__ void __launch_bounds__(256) fold_wgrad_combine_kernel(const float* __restrict__ P,
                                                                  const float* __restrict__ T,
-                                                                 const float* __restrict__ cs, int Co, int Ci,
-                                                                 int nseg, const float* __restrict__ coef,
+                                                                 const float* __restrict__ cs, int cs_slots, int Co,
+                                                                 int Ci, int nseg, const float* __restrict__ coef,
                                                                  const float* __restrict__ prm, long long pstride,
                                                                  float* __restrict__ dw) {
   const int cq = Ci / 4;
@@ -76,7 +76,11 @@ __global__ void __launch_bounds__(256) fold_wgrad_combine_kernel(const float* __
     const float bp = -c1 * c3 * istd, k = -c1 * (c2 - c3 * istd * mean);
     const float4 p = *reinterpret_cast<const float4*>(P + ((long long)s * Co + co) * Ci + ci);
     const float4 t = *reinterpret_cast<const float4*>(T + (long long)co * nseg * Ci + (long long)s * Ci + ci);
-    const float4 q = *reinterpret_cast<const float4*>(cs + (long long)s * Ci + ci);
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);  // the column sums' replica rows of segment s
+    for (int r = 0; r < cs_slots; ++r) {
+      const float4 v = *reinterpret_cast<const float4*>(cs + ((long long)s * cs_slots + r) * Ci + ci);
+      q.x += v.x; q.y += v.y; q.z += v.z; q.w += v.w;
+    }
     acc.x += c1 * p.x + bp * t.x + k * q.x;
     acc.y += c1 * p.y + bp * t.y + k * q.y;
     acc.z += c1 * p.z + bp * t.z + k * q.z;
@@ -238,7 +242,7 @@ extern "C" int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* w
 }
 
 extern "C" int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const float* P, const float* gram,
-                                             const float* colsums, const void* w, const float* coef,
+                                             const float* colsums, int cs_slots, const void* w, const float* coef,
                                              const float* prm, long long pstride, float* dw, float* workspace,
                                              void* stream) {
   if (Co <= 0 || Ci <= 0 || Co % 8 || Ci % 8 || nseg < 1) { set_error("bn_fold_wgrad_combine: bad shape"); return -1; }
@@ -263,8 +267,8 @@ extern "C" int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg
     return -1;
   }
   const long long n = (long long)Co * (Ci / 4);
-  hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, T, colsums, Co,
-                     Ci, nseg, coef, prm, pstride, dw);
+  hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, T, colsums,
+                     cs_slots < 1 ? 1 : cs_slots, Co, Ci, nseg, coef, prm, pstride, dw);
   ARTSBIR_CHECK_LAUNCH("fold_wgrad_combine");
   return 0;
 }

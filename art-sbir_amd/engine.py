@@ -408,17 +408,21 @@ class Engine:
         B, Ho, Wo, _ = y.shape
         return y, self._bn(bnmod, sb, (B // self._G) * Ho * Wo, train)
 
-    def _act_pool(self, x, bn, relu, pool):
+    def _act_pool(self, x, bn, relu, pool, colsum=False):
+        """relu(bn(x)) (+ 2x2 avgpool), one launch for all G segments (segment s
+        normalised with its own BN block).  colsum: also return the output's column
+        sums per segment, [G][NSLOT][C] replica rows (the folded BN backward's
+        1^T x of the conv that reads it)"""
         B, H, W, C = x.shape
         p = max(pool, 1)
         out = self._empty(B, H // p, W // p, C, device=x.device)
-        G = bn.G if bn is not None else 1
-        # one launch for all G segments (segment s normalised with its own BN block)
-        call("artsbir_act_pool", self.dt, ptr(x), ptr(bn.block) if bn is not None else None, relu, pool, B, H, W,
-             C, G, ptr(out), _s(), kernel="act_pool_kernel",
+        G = bn.G if bn is not None else self._G
+        cs = torch.zeros(G, NSLOT, C, dtype=torch.float32, device=x.device) if colsum else None
+        call("artsbir_act_pool_colsum", self.dt, ptr(x), ptr(bn.block) if bn is not None else None, relu, pool, B, H,
+             W, C, G, ptr(out), ptr(cs), _s(), kernel="act_pool_kernel",
              nbytes=float(x.element_size() * B * C * (H * W + (H // p) * (W // p))),
              tag=f"act_pool {B}x{H}x{W}x{C} pool{pool}")
-        return out
+        return (out, cs) if colsum else out
 
     # ------------------------------------------------ inference (folded BN)
     def bn_stats_changed(self):
@@ -548,14 +552,20 @@ class Engine:
         y2, b2 = self._conv_bn(Act(a1), m.conv2, m.bn2, fw2, 1, 1, train, stats)
         a2 = self._act_pool(y2, b2, 1, 0)
         y3, b3 = self._conv_bn(Act(a2), m.conv3, m.bn3, fw3, 1, 1, train, stats)
-        h = self._act_pool(y3, b3, 1, 2)
+        fold = train and save and self._fold_on()
+        h_cs = None
+        if fold:  # the stem output is the first block's downsample input: its column sums for the fold
+            h, h_cs = self._act_pool(y3, b3, 1, 2, colsum=True)
+        else:
+            h = self._act_pool(y3, b3, 1, 2)
         if save:
             ctx["stem"] = dict(x0=x0, y1=y1, a1=a1, y2=y2, a2=a2, y3=y3, b1=b1, b2=b2, b3=b3)
 
         # residual stages (models.py:354-357)
         bctx = []
         for blk, bp in zip(m.blocks(), pk["blocks"]):
-            h, c = self._block_fwd(blk, bp, h, train, stats)
+            h, c = self._block_fwd(blk, bp, h, train, stats, fold=fold, h_cs=h_cs)
+            h_cs = None
             bctx.append(c if save else None)
         ctx["blocks"] = bctx
 
@@ -565,7 +575,12 @@ class Engine:
             ctx["attn"] = actx
         return out, (ctx if save else None)
 
-    def _block_fwd(self, blk, bp, h, train, stats):
+    def _fold_on(self):
+        """whether the backward folds the block-output BN through conv3 / the
+        downsample conv (it needs the column sums of their inputs from the forward)"""
+        return FOLD_BN[0] and _fuse_bnb() and type(self) is Engine
+
+    def _block_fwd(self, blk, bp, h, train, stats, fold=False, h_cs=None):
         B, H, W, Cin = h.shape
         s = blk.stride
         # BN+ReLU outputs are materialised once (bf16): cheaper than re-applying
@@ -573,16 +588,24 @@ class Engine:
         y1, b1 = self._conv_bn(Act(h), blk.conv1, blk.bn1, bp["conv1"][0], 1, 0, train, stats)
         a1 = self._act_pool(y1, b1, 1, 0)
         y2, b2 = self._conv_bn(Act(a1), blk.conv2, blk.bn2, bp["conv2"][0], 1, 1, train, stats)
-        p2 = self._act_pool(y2, b2, 1, s if s > 1 else 0)
+        cs2 = csd = None
+        if fold:  # conv3's input with its column sums (the folded BN backward's 1^T x)
+            p2, cs2 = self._act_pool(y2, b2, 1, s if s > 1 else 0, colsum=True)
+        else:
+            p2 = self._act_pool(y2, b2, 1, s if s > 1 else 0)
         c3in = Act(p2)
         y3, b3 = self._conv_bn(c3in, blk.conv3, blk.bn3, bp["conv3"][0], 1, 0, train, stats)
         yd = bd = pd = None
         if blk.downsample is not None:
             if s > 1:
-                pd = self._act_pool(h, None, 0, s)
+                if fold:
+                    pd, csd = self._act_pool(h, None, 0, s, colsum=True)
+                else:
+                    pd = self._act_pool(h, None, 0, s)
                 din = pd
             else:
                 din = h
+                csd = h_cs
             yd, bd = self._conv_bn(Act(din), blk.downsample[1], blk.downsample[2], bp["down"][0], 1, 0, train, stats)
         out = torch.empty_like(y3)
         G = self._G
@@ -601,7 +624,7 @@ class Engine:
                                                                                                   is not None else 0)),
              tag=f"block_out {rows * G}x{C}")
         ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, bits=bits, b1=b1, b2=b2, b3=b3,
-                   bd=bd)
+                   bd=bd, cs2=cs2, csd=csd)
         return out, ctx
 
     def _attnpool_fwd(self, ap, pk, h):
@@ -958,10 +981,11 @@ class Engine:
              tag=f"dgrad_fold{'+bn1' if fused is not None else ''} {B}x{H}x{W}x{co}+{ci}->{ci}")
         return dx
 
-    def _wgrad_fold(self, g, x, conv, fw, coef, st: BNState, grads):
+    def _wgrad_fold(self, g, x, conv, fw, coef, st: BNState, grads, cs=None):
         """weight gradient of a 1x1 conv through the BatchNorm after it (side
         stream): per segment g^T x, the Gram matrix x^T x and the column sums of
-        x, combined by artsbir_bn_fold_wgrad_combine into the gradient buffer"""
+        x (cs [G][slots][Ci], from the forward's act_pool, else a column-sum pass
+        here), combined by artsbir_bn_fold_wgrad_combine into the gradient buffer"""
         if SKIP_WGRAD[0]:
             return
         main = torch.cuda.current_stream()
@@ -978,8 +1002,11 @@ class Engine:
             # [P | Gram | colsums] of every segment in one zeroed buffer, then the
             # combine's workspace (W in f32, T = W Gram)
             nP, nG = G * co * ci, G * ci * ci
-            buf = torch.zeros(nP + nG + G * ci, dtype=torch.float32, device=x.device)
-            P, gram, cs = buf[:nP].view(G, co, ci), buf[nP:nP + nG].view(G, ci, ci), buf[nP + nG:].view(G, ci)
+            own_cs = cs is None
+            buf = torch.zeros(nP + nG + (G * ci if own_cs else 0), dtype=torch.float32, device=x.device)
+            P, gram = buf[:nP].view(G, co, ci), buf[nP:nP + nG].view(G, ci, ci)
+            if own_cs:
+                cs = buf[nP + nG:].view(G, 1, ci)
             wsp = torch.empty(co * ci * (G + 1), dtype=torch.float32, device=x.device)
             for s in range(G):
                 gs, xs = g[s * Bs:(s + 1) * Bs], x[s * Bs:(s + 1) * Bs]
@@ -987,13 +1014,15 @@ class Engine:
                 call("artsbir_gemm_tn2", self.dt, Ms, co, ci, ci, ptr(gs), co, ptr(xs), ci, ptr(xs), ci, ptr(P[s]),
                      ptr(gram[s]), _s(), kernel="auto", flops=2.0 * Ms * (co + ci) * ci,
                      nbytes=float(es * Ms * (co + ci) + 4 * (co + ci) * ci), tag=f"wgrad_fold {Ms}x{co}+{ci}x{ci}")
-                call("artsbir_colsum", self.dt, ptr(xs), Ms, ci, ci, ptr(cs[s]), _s())
-            call("artsbir_bn_fold_wgrad_combine", self.dt, co, ci, G, ptr(P), ptr(gram), ptr(cs), ptr(fw), ptr(coef),
-                 ptr(st.buf), 4 * co, ptr(grads[conv.weight]), ptr(wsp), _s(), kernel="fold_combine",
+                if own_cs:
+                    call("artsbir_colsum", self.dt, ptr(xs), Ms, ci, ci, ptr(cs[s]), _s(), kernel="colsum_kernel",
+                         nbytes=float(es * Ms * ci), tag=f"colsum {Ms}x{ci}")
+            call("artsbir_bn_fold_wgrad_combine", self.dt, co, ci, G, ptr(P), ptr(gram), ptr(cs), cs.shape[1], ptr(fw),
+                 ptr(coef), ptr(st.buf), 4 * co, ptr(grads[conv.weight]), ptr(wsp), _s(), kernel="fold_combine",
                  flops=2.0 * G * co * ci * ci, nbytes=float(4 * (G * (co * ci + ci * ci) + 3 * co * ci)),
                  tag=f"fold_combine {co}x{ci}")
         if side is not main:
-            self._side_keep.extend([g, x, coef, st.buf, buf, wsp])
+            self._side_keep.extend([g, x, coef, st.buf, buf, wsp, cs])
 
     def _block_bwd(self, blk, bp, c, dout, grads, ws, fused_res=None, prev=None):
         """backward of one Bottleneck.  dout: gradient of the block output, or —
@@ -1026,7 +1055,7 @@ class Engine:
         c3out = c3in.shape[:3] + (blk.conv3.weight.shape[1],)
         if fold:
             fw3 = self._fold_weights(bp["conv3"], blk.conv3, coefs[0], b3)
-            self._wgrad_fold(dout, p2, blk.conv3, bp["conv3"][0], coefs[0], b3, grads)
+            self._wgrad_fold(dout, p2, blk.conv3, bp["conv3"][0], coefs[0], b3, grads, c.get("cs2"))
             if s == 1:
                 f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
                 g2 = self._dgrad_fold(dout, p2, fw3, blk.conv3, fused=f2)
@@ -1062,7 +1091,7 @@ class Engine:
             dconv = blk.downsample[1]
             if fold:
                 fwd_ = self._fold_weights(bp["down"], dconv, coefs[1], bd)
-                self._wgrad_fold(dout, din, dconv, bp["down"][0], coefs[1], bd, grads)
+                self._wgrad_fold(dout, din, dconv, bp["down"][0], coefs[1], bd, grads, c.get("csd"))
                 res = self._dgrad_fold(dout, din, fwd_, dconv)
             else:
                 dyd = dys[1]

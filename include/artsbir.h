@@ -152,12 +152,13 @@ int artsbir_bn_fold_bwd_prep(int dtype, int Co, int Ci, const void* wt, const fl
 /* The weight gradient of that conv: dw[co][ci] += sum_s c1_s[co] P_s[co][ci] +
  * b'_s[co] (W Gram_s)[co][ci] + k_s[co] colsums_s[ci], with P_s = g_s^T x_s
  * [nseg][Co][Ci], Gram_s = x_s^T x_s [nseg][Ci][Ci], colsums_s = 1^T x_s
- * [nseg][Ci] (f32, from artsbir_gemm_tn2 / artsbir_colsum), w the forward weight
- * [Co][Ci] (compute dtype), k = -c1 (c2 - c3 istd mean).  workspace: f32,
- * Co * Ci * (nseg + 1) floats. */
+ * [nseg][cs_slots][Ci] summed over the replica rows (f32, from artsbir_gemm_tn2 and
+ * artsbir_act_pool_colsum / artsbir_colsum), w the forward weight [Co][Ci]
+ * (compute dtype), k = -c1 (c2 - c3 istd mean).  workspace: f32, Co * Ci *
+ * (nseg + 1) floats. */
 int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const float* P, const float* gram,
-                                  const float* colsums, const void* w, const float* coef, const float* prm,
-                                  long long pstride, float* dw, float* workspace, void* stream);
+                                  const float* colsums, int cs_slots, const void* w, const float* coef,
+                                  const float* prm, long long pstride, float* dw, float* workspace, void* stream);
 
 /* ---- layout / parameter packing ---------------------------------------- */
 /* x.type(weight dtype) + NCHW -> NHWC8 (models.py:352); x [B][Cin<=8][H][W] f32. */
@@ -215,6 +216,12 @@ int artsbir_bn_stats_det(int dtype, const void* y, int nseg, long long rows, int
  * nseg segments of B/nseg images (the triplet branches): segment s uses bn + s*4*C. */
 int artsbir_act_pool(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W, int C,
                      int nseg, void* out, void* stream);
+/* The same, also accumulating the column sums of the stored output per segment:
+ * colsum[s][r][c] += sum over segment s's output pixels of out[.][c], spread over
+ * replica rows r < ARTSBIR_NSLOT (the consumer sums them) — the 1^T x of the folded
+ * BatchNorm backward of the conv that reads out (csrc/fold.hip). */
+int artsbir_act_pool_colsum(int dtype, const void* x, const float* bn, int relu, int pool, int B, int H, int W, int C,
+                            int nseg, void* out, float* colsum, void* stream);
 /* Bottleneck tail (models.py:234-235): out = relu(bn3(y3) + (bn_d(yd) | identity));
  * nseg segments of rows/nseg rows, segment s with the blocks + s*4*C. */
 int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,

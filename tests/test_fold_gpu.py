@@ -256,8 +256,10 @@ def test_wgrad_fold_combine(case, dtype, dev):
     dw = init.clone().to(dev)
     cd, pd = coef.to(dev), prm.to(dev)
     ws = torch.empty(Co * Ci * (G + 1), device=dev)
+    # the column sums as replica rows (as act_pool_colsum leaves them): 3 rows summing to cs
+    cs3 = torch.stack([cs * 0.25, cs * 0.5, cs * 0.25], 1).contiguous()
     _hip.call("artsbir_bn_fold_wgrad_combine", _hip.dtype_code(dtype), Co, Ci, G, P.data_ptr(), gram.data_ptr(),
-              cs.data_ptr(), wd.data_ptr(), cd.data_ptr(), pd.data_ptr(), 4 * Co, dw.data_ptr(), ws.data_ptr(),
+              cs3.data_ptr(), 3, wd.data_ptr(), cd.data_ptr(), pd.data_ptr(), 4 * Co, dw.data_ptr(), ws.data_ptr(),
               _hip.stream())
     torch.cuda.synchronize()
     assert _rel(dw.double().cpu() - init.double(), ref) < 1e-4
@@ -314,3 +316,32 @@ def test_colsum_narrow_and_wide(rows, C, ld, dtype, dev):
     torch.cuda.synchronize()
     ref = init.double() + x[:, :C].double().sum(0)
     assert _rel(out.double().cpu() - init.double(), ref - init.double()) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
+@pytest.mark.parametrize("B,G,H,W,C,pool,bn", [(6, 3, 16, 16, 64, 0, True), (6, 3, 16, 16, 128, 2, True),
+                                               (4, 2, 8, 8, 512, 2, False), (3, 3, 7, 7, 2048, 0, True),
+                                               (2, 1, 6, 10, 256, 2, False)])
+def test_act_pool_colsum(B, G, H, W, C, pool, bn, dtype, dev):
+    """artsbir_act_pool_colsum: relu(bn(x)) (+ avgpool) as artsbir_act_pool, plus the
+    per-segment column sums of the stored output over the replica rows"""
+    g = torch.Generator().manual_seed(29)
+    x = torch.randn(B, H, W, C, generator=g).to(dtype)
+    prm = torch.zeros(G, 4, C)
+    prm[:, 0] = torch.randn(G, C, generator=g) * 0.2
+    prm[:, 2] = torch.rand(G, C, generator=g) + 0.5
+    prm[:, 3] = torch.randn(G, C, generator=g) * 0.3
+    xd, pd = x.to(dev), prm.to(dev)
+    p = pool if pool > 1 else 1
+    out = torch.empty(B, H // p, W // p, C, dtype=dtype, device=dev)
+    out2 = torch.empty_like(out)
+    cs = torch.zeros(G, _hip.NSLOT, C, device=dev)
+    relu = 1 if bn else 0
+    _hip.call("artsbir_act_pool_colsum", _hip.dtype_code(dtype), xd.data_ptr(), pd.data_ptr() if bn else None, relu,
+              pool, B, H, W, C, G, out.data_ptr(), cs.data_ptr(), _hip.stream())
+    _hip.call("artsbir_act_pool", _hip.dtype_code(dtype), xd.data_ptr(), pd.data_ptr() if bn else None, relu, pool,
+              B, H, W, C, G, out2.data_ptr(), _hip.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out, out2)
+    o = out.double().cpu().reshape(G, -1, C)
+    assert _rel(cs.double().cpu().sum(1), o.sum(1)) < 1e-5

@@ -24,7 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=384)
     ap.add_argument("--gap", type=float, default=20.0)
-    ap.add_argument("--tune-cache", default=os.path.join(ROOT, "profiles", "tune_r4.txt"))
+    ap.add_argument("--tune-cache", default=os.path.join(ROOT, "profiles", "tune_r5.txt"))
     ap.add_argument("--mode", default="overlap", choices=["overlap", "skip", "serial"])
     ap.add_argument("--side-tail", type=int, default=25, help="side-stream launches listed after main's last one")
     ap.add_argument("--by-tag", type=int, default=0, help="also list the N largest (kernel, tag) groups")
