@@ -71,20 +71,25 @@ def short(name):
     if m:
         k, t = m.group(1), [x.strip() for x in m.group(2).split(",")]
         fb = ",bnb" if t[-1] == "true" and k == "sconv_kernel" else ""
-        if k == "pgemm_kernel":  # <BPX, BCH, WPX, WCH, NSTAGE, MULTI, BK, TWO, PF, KS, GLB>
+        if k == "pgemm_kernel":  # <BPX, BCH, WPX, WCH, NSTAGE, MULTI, BK, TWO, PF, KS, GLB, X2>
             k32 = ",k32" if len(t) > 9 and t[9] == "32" else ""
             glb = ",glb" if len(t) > 10 and t[10] == "true" else ""
-            return f"{k}<{t[0]},{t[1]}{k32}{glb}{',bnb' if t[6] != '0' else ''}{',pf' if t[8] == 'true' else ''}>"
+            fold = ",fold" if len(t) > 11 and t[11] == "true" else ""
+            return f"{k}<{t[0]},{t[1]}{k32}{glb}{',bnb' if t[6] != '0' else ''}{',pf' if t[8] == 'true' else ''}{fold}>"
+        if k == "pp256_kernel":  # <BK, TWO, TAPS, X2>
+            tags = (["bnb"] if t[0] != "0" else []) + (["fold"] if len(t) > 3 and t[3] == "true" else [])
+            return f"{k}<{','.join(tags)}>" if tags else k
         if k == "pwgrad_kernel":  # <BM, BN, WM, WN, NSTAGE, ...>: the 256 x 256 tiles carry their wave grid
             return f"{k}<{t[0]},{t[1]}{f',w{t[2]}x{t[3]}' if t[0] == t[1] == '256' else ''}>"
         if k == "hwgrad_kernel":  # <CT, OT, TR, NWC>: the 4-wave 64 x 64 variant is named w4
             return f"{k}<{t[0]},{t[1]}{',w4' if t[0] == t[1] == '64' and t[3] == '4' else ''}>"
-        if k == "pstream_kernel":  # <BCH, WPX, WCH, NSTAGE, MULTI, BNB, FWDS, BK, TWO, KS>
+        if k == "pstream_kernel":  # <BCH, WPX, WCH, NSTAGE, MULTI, BNB, FWDS, BK, TWO, KS, X2>
+            fold = ",fold" if len(t) > 10 and t[10] == "true" else ""
             if len(t) > 9 and t[9] == "32":
                 return f"{k}<{t[0]},k32>"
             if t[5] == "true":
-                return f"{k}<{t[0]},{'bnbk' if len(t) > 7 and t[7] != '0' else 'bnb'}>"
-            return f"{k}<{t[0]}>"
+                return f"{k}<{t[0]},{'bnbk' if len(t) > 7 and t[7] != '0' else 'bnb'}{fold}>"
+            return f"{k}<{t[0]}{fold}>"
         if k == "hconv_kernel":
             return f"{k}<{t[0]},{t[1]},{t[2]}x{t[3]}{',bnb' if t[4] == 'true' else ''}>"
         if k == "sconv_kernel":
