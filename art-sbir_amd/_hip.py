@@ -103,6 +103,7 @@ SIGNATURES = {
     "artsbir_bn_fold": [_vp, _c_int, _c_ll, _vp, _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp],
     "artsbir_conv2d_dgrad_bnb": [_P, _vp, _vp, _vp, _vp, _c_int, _PB, _c_int, _c_ll, _vp],
     "artsbir_conv1x1_dgrad_fold": [_P, _vp, _vp, _vp, _vp, _vp, _PB, _c_int, _c_ll, _vp],
+    "artsbir_conv1x1_dgrad_fold_wg": [_P, _vp, _vp, _vp, _vp, _vp, _PB, _c_int, _c_ll, _vp, _vp, _vp],
     "artsbir_bn_fold_bwd_prep": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_bn_fold_wgrad_combine": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_ll, _vp,
                                       _vp, _vp],

@@ -139,6 +139,8 @@ struct ConvArgs {
   long long x2_elems = 0, sN2 = 0, sH2 = 0, sW2 = 0;
   int C1 = 0;
   long long w_sstride = 0, bias_sstride = 0;
+  float* wg_p = nullptr;  // the fold's weight-gradient operands in the same pass (pg_fold_wg_launch)
+  float* wg_gram = nullptr;
 };
 
 template <typename T, int BM, int BN, bool UNIFORM_TAP, bool AFFINE>
@@ -874,6 +876,12 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
       p.bnb_mbn = bd->mask_bn; p.bnb_mask = bd->mask;
       p.bnb_pstride = a.bnb_pstride;
     }
+    if (a.wg_p) {  // one kernel produces the data gradient and the weight-gradient operands
+      p.wg_p = a.wg_p; p.wg_gram = a.wg_gram;
+      if (!pg_fold_wg_launch(p, st)) return 1;
+      ARTSBIR_CHECK_LAUNCH("pgemm");
+      return 0;
+    }
     int choice;
     const char* force = getenv("ARTSBIR_PGEMM_CFG");
     static const char* force_bnb = getenv("ARTSBIR_BNB_CFG");  // experiment: the fused BN-backward dgrads only
@@ -906,7 +914,7 @@ static int launch_conv(const ConvArgs& a, hipStream_t st) {
     }
   }
   if (a.res_mode == 3) { set_error("gemm_nt_gate: no kernel for this shape"); return -1; }
-  if (a.x2) return 1;  // a two-operand fold no pipelined kernel took: the caller's fallback
+  if (a.x2 || a.wg_p) return 1;  // a two-operand fold no pipelined kernel took: the caller's fallback
   return run_old<T>(a, st);
 }
 
@@ -1101,9 +1109,8 @@ static artsbir_bn_bwd_desc bnb_segment(const artsbir_bn_bwd_desc* bd, int s, lon
   return d;
 }
 
-extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
-                                          const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
-                                          long long param_stride, void* stream) {
+static int fold_check(const artsbir_conv_desc* d, const void* g, const void* x, const void* w, const float* bias,
+                      void* dx, const artsbir_bn_bwd_desc* bnb, int nseg) {
   if (check_conv(d)) return -1;
   if (d->R != 1 || d->S != 1 || d->stride != 1 || d->pad != 0) { set_error("conv1x1_dgrad_fold: 1x1 stride-1 convolutions only"); return -1; }
   if (!g || !x || !w || !bias || !dx) { set_error("conv1x1_dgrad_fold: null operand"); return -1; }
@@ -1113,11 +1120,15 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
     set_error("conv1x1_dgrad_fold: the fused BN backward must be kind 1 with one target");
     return -1;
   }
+  return 0;
+}
+
+// the two-operand / per-segment-weight launch arguments of the fold
+static ConvArgs fold_conv_args(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                               const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                               long long param_stride) {
   const int Co = d->Cout, Ci = d->C, K = Co + Ci;
-  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
-  const bool bf = d->dtype == ARTSBIR_DT_BF16;
-  const long long es = bf ? 2 : 4;
-  hipStream_t st = (hipStream_t)stream;
+  const long long M = (long long)d->N * d->H * d->W;
   ConvArgs a;
   a.x = g; a.sW = Co; a.sH = (long long)d->W * Co; a.sN = (long long)d->H * d->W * Co; a.x_elems = M * Co;
   a.x2 = x; a.sW2 = Ci; a.sH2 = (long long)d->W * Ci; a.sN2 = (long long)d->H * d->W * Ci; a.x2_elems = M * Ci;
@@ -1131,6 +1142,19 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
   a.res = nullptr; a.res_mode = 0; a.relu = 0;
   a.nseg = nseg; a.bnb_desc = bnb; a.bnb_pstride = param_stride;
   a.w_sstride = (long long)Ci * K; a.bias_sstride = Ci;
+  return a;
+}
+
+extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                                          const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                                          long long param_stride, void* stream) {
+  if (fold_check(d, g, x, w, bias, dx, bnb, nseg)) return -1;
+  const int Co = d->Cout, Ci = d->C, K = Co + Ci;
+  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
+  const bool bf = d->dtype == ARTSBIR_DT_BF16;
+  const long long es = bf ? 2 : 4;
+  hipStream_t st = (hipStream_t)stream;
+  const ConvArgs a = fold_conv_args(d, g, x, w, bias, dx, bnb, nseg, param_stride);
   // one launch over every segment, else one per segment (the tiles of a
   // launch then never straddle two), on the two-operand pipelined kernels
   if (bf) {
@@ -1186,6 +1210,37 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
     p.y = reinterpret_cast<char*>(dx) + s * seg_m * Ci * es;
     const int rc = bf ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
     if (rc) return -1;
+  }
+  return 0;
+}
+
+// The fold's data gradient and, from the same pass, the operands of its weight
+// gradient (artsbir.h: artsbir_conv1x1_dgrad_fold_wg): per segment s
+// P[s] += g_s^T x_s ([Co][Ci]) and gram[s] += x_s^T x_s ([Ci][Ci]), f32.  One
+// kernel where pg_fold_wg_launch takes the shape; otherwise the data gradient
+// (artsbir_conv1x1_dgrad_fold) and one artsbir_gemm_tn2 per segment.
+extern "C" int artsbir_conv1x1_dgrad_fold_wg(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                                             const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                                             long long param_stride, float* P, float* gram, void* stream) {
+  if (fold_check(d, g, x, w, bias, dx, bnb, nseg)) return -1;
+  if (!P || !gram) { set_error("conv1x1_dgrad_fold_wg: null weight-gradient operand"); return -1; }
+  const int Co = d->Cout, Ci = d->C;
+  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
+  const long long es = d->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+  static const bool off = getenv("ARTSBIR_FOLD_WG") && atoi(getenv("ARTSBIR_FOLD_WG")) == 0;  // measurement switch
+  if (d->dtype == ARTSBIR_DT_BF16 && !off) {
+    ConvArgs a = fold_conv_args(d, g, x, w, bias, dx, bnb, nseg, param_stride);
+    a.wg_p = P; a.wg_gram = gram;
+    const int rc = launch_conv<bf16>(a, (hipStream_t)stream);
+    if (rc <= 0) return rc;
+  }
+  if (artsbir_conv1x1_dgrad_fold(d, g, x, w, bias, dx, bnb, nseg, param_stride, stream)) return -1;
+  for (int s = 0; s < nseg; ++s) {
+    const char* gs = reinterpret_cast<const char*>(g) + s * seg_m * Co * es;
+    const char* xs = reinterpret_cast<const char*>(x) + s * seg_m * Ci * es;
+    if (artsbir_gemm_tn2(d->dtype, seg_m, Co, Ci, Ci, gs, Co, xs, Ci, xs, Ci, P + (long long)s * Co * Ci,
+                         gram + (long long)s * Ci * Ci, stream))
+      return -1;
   }
   return 0;
 }

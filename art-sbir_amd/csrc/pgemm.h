@@ -50,6 +50,11 @@ struct PgArgs {
   int C1 = 0;
   long long w_sstride = 0;
   long long bias_sstride = 0;
+  // the fold's weight-gradient operands accumulated by the same pass (pstream
+  // WGK variant): wg_p[seg][k][Cout] += sum_m x[m][k] x2[m][co] for k < C1 and
+  // wg_gram[seg][k - C1][Cout] += sum_m x2[m][k - C1] x2[m][co] (f32, atomics)
+  float* wg_p = nullptr;
+  float* wg_gram = nullptr;
 };
 
 // Weight gradient dW[co][k] += sum_m dY[m][co] * Xcol[m][k] (pwgrad.hip).
@@ -106,6 +111,9 @@ inline bool pg_fold_ok(const PgArgs& a, int bpx, int ks) {
   if ((a.w_sstride || a.bias_sstride) && a.seg_m > 0 && a.seg_m % bpx != 0) return false;
   return true;
 }
+// The fold's data gradient with its weight-gradient operands in the same pass
+// (a.wg_p / a.wg_gram set): false, launching nothing, outside the shapes it takes
+bool pg_fold_wg_launch(const PgArgs& a, hipStream_t st);
 // Heuristic candidate for a shape (-1: unsupported).
 int pgemm_default_cfg(const PgArgs& a);
 

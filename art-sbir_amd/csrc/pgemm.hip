@@ -321,8 +321,11 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
 // KS: k per stage as in pgemm_kernel (32: 64-B LDS rows, twice the stages in
 // the same LDS, uniform taps only)
 // X2: the two-operand / per-segment-weight fold of pgemm_kernel (1x1 only)
+// WGK > 0: the fold (X2) with its weight-gradient operands accumulated by the
+// loader waves (pstream_wg_loader, K = WGK, 64 output channels)
+
 template <int BCH, int WPX, int WCH, int NSTAGE, bool MULTI, bool BNB, bool FWDS, int BK = 0, bool TWO = false,
-          int KS = 64, bool X2 = false>
+          int KS = 64, bool X2 = false, int WGK = 0>
 __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
   constexpr int BPX = 256, NWC = 8, NWL = 4;
   static_assert(WPX * WCH == NWC, "compute waves");
@@ -351,6 +354,11 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
 
   if (wid >= NWC) {
     // ------------------------------------------------------------ loaders
+    if constexpr (WGK > 0) {
+      static_assert(X2 && !MULTI && KS == 64 && !FWDS, "WGK: the fold's 64-k stages");
+      pstream_wg_loader<BCH, NSTAGE, LPX, LCH, STAGE, PXB, WGK>(a, smem, wid - NWC, lane, G, bslot, nk, total);
+      return;
+    }
     const int lw = wid - NWC;
     const int lrow = lane / CPR, lslot = lane % CPR;
     const int csrc = KS == 64 ? (lslot ^ lrow) : (lslot ^ ((lrow >> 2) & 2));
@@ -1377,6 +1385,35 @@ static bool pg_fold_launch(const PgArgs& a, int c, hipStream_t st) {
     default:
       return false;
   }
+}
+
+// The fold data gradient together with its weight-gradient operands (a.wg_p,
+// a.wg_gram): the persistent streaming kernel whose loader waves accumulate
+// g^T x and x^T x from the stages they stream (pstream_wg_loader).  Layers with
+// 64 input channels under a 256-channel output (K = 320: layer 1's conv3 and
+// downsample conv), contiguous NHWC operands, whole 256-pixel tiles.
+bool pg_fold_wg_launch(const PgArgs& a, hipStream_t st) {
+  if (!a.x2 || !a.wg_p || !a.wg_gram || !a.bias || a.relu || a.stats || a.res_mode) return false;
+  if (a.bnb && (a.bnb != 1 || a.bnb_nt != 1)) return false;
+  if (a.Cout != 64 || a.K != 320 || a.C1 != 256 || a.C != a.K) return false;
+  bool multi;
+  if (!pg_supported(a, multi) || multi || !pg_fold_ok(a, 256, 64)) return false;
+  if (a.M % 256 || (a.seg_m > 0 && a.seg_m % 256)) return false;
+  if (a.sW != a.C1 || a.sH != (long long)a.W * a.sW || a.sN != (long long)a.H * a.sH) return false;
+  if (a.sW2 != a.Cout || a.sH2 != (long long)a.W * a.sW2 || a.sN2 != (long long)a.H * a.sH2) return false;
+  const long long nt = a.M / 256;
+  if (nt > 0x7fffffffLL) return false;
+  const int grid = (int)(nt < 256 ? nt : 256);
+  if (a.bnb == 1) {
+    hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false, true, false, 1, false, 64, true, 320>), dim3(grid),
+                       dim3(768), 0, st, a, (int)nt);
+    set_last_kernel("pstream_kernel<64,bnbk,fold,wg>");
+  } else {
+    hipLaunchKernelGGL((pstream_kernel<64, 4, 2, 3, false, false, false, 0, false, 64, true, 320>), dim3(grid),
+                       dim3(768), 0, st, a, (int)nt);
+    set_last_kernel("pstream_kernel<64,fold,wg>");
+  }
+  return true;
 }
 
 // candidate c: 0..4 tile shapes of pgemm_kernel, 10 the persistent streaming kernel

@@ -56,6 +56,24 @@ __device__ __forceinline__ void glds16(__amdgpu_buffer_rsrc_t r, char* lds, unsi
       : "memory");
 }
 
+// the same with a wave-uniform byte offset added by the buffer unit (soffset):
+// rows u * stride of one lane base keep ONE address VGPR live, not one per row
+__device__ __forceinline__ void glds16_so(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff, unsigned soff) {
+  const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(pg_lds_t)lds);
+  const unsigned so = __builtin_amdgcn_readfirstlane(soff);
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\t"
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(base), "s"(r), "s"(so)
+      : "memory");
+}
+
 // the same with 4 B per lane (lds + 4 * lane)
 __device__ __forceinline__ void glds4(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
   const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long long)(pg_lds_t)lds);
@@ -822,5 +840,172 @@ __device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&a
     }
   }
 }
+
+// transposed 16-column fragment of a 64-k stage image (rows of 128 B, chunk
+// slot = chunk ^ (row & 7)): for the MFMA operand whose reduction runs over the
+// image's rows (pixels).  Lane 4q + p of 16-lane group g addresses row 8g + q
+// (+4 for the second read) of the 32-row block, columns 16 c0 + 4p .. + 3
+// (T10); lane (g, t) receives column 16 c0 + t of rows 8g .. 8g + 7.
+typedef short pg_v4s_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) pg_v4s_t* pg_lds_v4s_t;
+__device__ __forceinline__ int pg_tr_off(int g, int q, int p, int c0, int h) {
+  const int row = 8 * g + q + 4 * h;
+  return row * 128 + (((2 * c0 + (p >> 1)) ^ (q + 4 * h)) << 4) + 8 * (p & 1);
+}
+__device__ __forceinline__ bf16x8 pg_tr_frag(const char* base, int off_lo, int off_hi) {
+  const pg_v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (pg_lds_v4s_t)(const __attribute__((address_space(3))) void*)(base + off_lo));
+  const pg_v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (pg_lds_v4s_t)(const __attribute__((address_space(3))) void*)(base + off_hi));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// Loader waves of the fold data gradient that also accumulate its weight-gradient
+// operands (the backward of models.py:219-220 conv3 -> bn3 and 227-229 downsample
+// conv -> BN, folded as in fold.hip): besides streaming the stages they compute,
+// from the same LDS images, Q[k][co] = sum over the tile's pixels of
+// [g | x][m][k] * x[m][co] — g^T x (k < C1) and the Gram matrix x^T x — so the
+// weight gradient never reads g and x again.  The layer has one 64-channel block
+// (Cout == 64, K == WGK); the stage order of a tile puts the x chunk first, each
+// wave keeps the transposed x fragments of its 16 channels in registers for the
+// tile and Q (K x 16, f32) for as long as its tiles stay in one BN segment, then
+// adds it into wg_p / wg_gram with f32 atomics.  1x1 stride 1, M a whole number
+// of 256-pixel tiles (a.seg_m too), so no pixel row is ever out of range.
+template <int BCH, int NSTAGE, int LPX, int LCH, int STAGE, int PXB, int WGK>
+__device__ __forceinline__ void pstream_wg_loader(const PgArgs& a, char* smem, int lw, int lane, int G, int bslot,
+                                                  int nk, int total) {
+  static_assert(BCH == 64 && WGK % 64 == 0 && WGK > 64, "one 64-channel block, K = C1 + 64");
+  constexpr int NWL = 4, NKC = WGK / 64, NQ = WGK / 16, C1 = WGK - 64;
+  const int lrow = lane >> 3, lslot = lane & 7;
+  const int csrc = lslot ^ lrow;
+  // DMA source offsets of this lane's row of instruction u (row = 32 u + 8 lw + lrow)
+  const int r0 = 8 * lw + lrow;
+  const unsigned gofs = (unsigned)(r0 * a.sW * 2 + csrc * 16), gstep = (unsigned)(32 * a.sW * 2);
+  const unsigned xofs = (unsigned)(r0 * a.sW2 * 2 + csrc * 16), xstep = (unsigned)(32 * a.sW2 * 2);
+  // weight rows of instruction u: pg_perm(32 u + 8 lw + lrow) = 32 u + pg_perm(8 lw + lrow)
+  const unsigned woff = (unsigned)(pg_perm(8 * lw + lrow) * a.K * 2 + csrc * 16), wstep = (unsigned)(32 * a.K * 2);
+  // tiles per BN segment (uniform, 32-bit: segments by scalar division)
+  const int tps = __builtin_amdgcn_readfirstlane(a.seg_m > 0 ? (int)(a.seg_m / 256) : 0x7fffffff);
+  __amdgpu_buffer_rsrc_t gr = pg_rsrc(a.x, 0), xr = gr, wr = gr;
+  auto issue = [&](int sidx) {
+    const int i = sidx / nk, kt = sidx - i * nk;
+    if (kt == 0) {
+      const int tile = i * G + bslot;
+      const long long bpx = (long long)tile * 256;
+      const int sg = tile / tps;
+      gr = pg_rsrc(reinterpret_cast<const bf16*>(a.x) + bpx * a.sW, (a.M - bpx) * a.sW * 2);
+      xr = pg_rsrc(reinterpret_cast<const bf16*>(a.x2) + bpx * a.sW2, (a.M - bpx) * a.sW2 * 2);
+      wr = pg_rsrc(reinterpret_cast<const bf16*>(a.w) + sg * a.w_sstride, (long long)a.Cout * a.K * 2);
+    }
+    const int kofs = kt == 0 ? C1 : (kt - 1) * 64;  // the x chunk first
+    char* pxs = smem + (sidx % NSTAGE) * STAGE;
+    char* chs = pxs + PXB;
+#pragma unroll
+    for (int u = 0; u < LPX; ++u) {
+      if (kt == 0) glds16_so(xr, pxs + (u * NWL + lw) * 1024, xofs, u * xstep);
+      else glds16_so(gr, pxs + (u * NWL + lw) * 1024, gofs, u * gstep + kofs * 2);
+    }
+#pragma unroll
+    for (int u = 0; u < LCH; ++u) glds16_so(wr, chs + (u * NWL + lw) * 1024, woff, u * wstep + kofs * 2);
+  };
+  // MFMA operand fragments: lane (g, t = 4q + p)
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p = t & 3;
+  // column block c of a read is off(c = 0) ^ (c << 5): the chunk XOR of the
+  // image touches bits 4-6 only
+  const int alo = pg_tr_off(g, q, p, 0, 0), ahi = pg_tr_off(g, q, p, 0, 1);
+  f32x4 qacc[NQ];
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) qacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 xf[8];
+  int cur_seg = -1;
+  // Q rows k = 16 j + 4 g + r, column co = 16 lw + t (row stride Cout = 64)
+  auto flush = [&]() {
+    // uniform segment bases (SGPRs) + one 32-bit lane offset
+    float* P = a.wg_p + (long long)cur_seg * C1 * 64;
+    float* Gm = a.wg_gram + (long long)cur_seg * 64 * 64;
+    const int lo = 4 * g * 64 + 16 * lw + t;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      __builtin_amdgcn_sched_barrier(0);  // one 16-row block of addresses at a time
+      float* dst = (16 * j < C1) ? P + (lo + 16 * j * 64) : Gm + (lo + (16 * j - C1) * 64);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        atomicAdd(dst + r * 64, qacc[j][r]);
+        qacc[j][r] = 0.f;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto wgrad = [&](int s) {
+    const int i = s / nk, kt = s - i * nk;
+    const char* pxs = smem + (s % NSTAGE) * STAGE;
+    if (kt == 0) {
+      // this wave's 16 channels of the x chunk (recomputed here, not held across the loop)
+      int xlo, xhi;
+      asm volatile("v_xor_b32 %0, %1, %2" : "=v"(xlo) : "v"(alo), "s"(lw << 5));
+      asm volatile("v_xor_b32 %0, %1, %2" : "=v"(xhi) : "v"(ahi), "s"(lw << 5));
+#pragma unroll
+      for (int kp = 0; kp < 8; ++kp) xf[kp] = pg_tr_frag(pxs + kp * 4096, xlo, xhi);
+    }
+    const int kc = kt == 0 ? NKC - 1 : kt - 1;  // the stage's 64 rows of Q
+#pragma unroll
+    for (int c = 0; c < NKC; ++c) {
+      if (c != kc) continue;
+#pragma unroll
+      for (int kp = 0; kp < 8; ++kp) {
+        // one 32-pixel step at a time: 4 fragments live (the register budget of
+        // 3 waves per SIMD holds Q, the x fragments and no more)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jp = 0; jp < 4; jp += 2) {
+          // fragment offsets recomputed per use (asm volatile: not hoisted out of
+          // the loop, where the register allocator would spill them)
+          int o[4];
+          asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o[0]) : "v"(alo), "s"(jp << 5));
+          asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o[1]) : "v"(ahi), "s"(jp << 5));
+          asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o[2]) : "v"(alo), "s"((jp + 1) << 5));
+          asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o[3]) : "v"(ahi), "s"((jp + 1) << 5));
+          const bf16x8 a0 = pg_tr_frag(pxs + kp * 4096, o[0], o[1]);
+          const bf16x8 a1 = pg_tr_frag(pxs + kp * 4096, o[2], o[3]);
+          qacc[4 * c + jp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, xf[kp], qacc[4 * c + jp], 0, 0, 0);
+          qacc[4 * c + jp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, xf[kp], qacc[4 * c + jp + 1], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  constexpr int LPS = LPX + LCH;
+  for (int s = 0; s < NSTAGE - 1; ++s)
+    if (s < total) issue(s);
+  if (total > 0) {
+    int ahead = total - 1;
+    if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
+    wait_stages<LPS, NSTAGE>(ahead);
+  }
+  for (int s = 0; s < total; ++s) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s % nk == 0) {  // a new tile: flush Q when it starts another BN segment
+      const int sg = ((s / nk) * G + bslot) / tps;
+      if (sg != cur_seg) {
+        if (cur_seg >= 0) {
+          flush();
+          vm_wait<0>();  // the atomics and the stage in flight: the counted waits below see only DMA
+        }
+        cur_seg = sg;
+      }
+    }
+    if (s + NSTAGE - 1 < total) issue(s + NSTAGE - 1);
+    wgrad(s);
+    if (s + 1 < total) {
+      int ahead = total - 2 - s;
+      if (ahead > NSTAGE - 2) ahead = NSTAGE - 2;
+      wait_stages<LPS, NSTAGE>(ahead);
+    }
+  }
+  if (cur_seg >= 0) flush();
+}
+
 
 }  // namespace artsbir

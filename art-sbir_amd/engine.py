@@ -68,6 +68,9 @@ DETERMINISTIC = os.environ.get("ARTSBIR_DETERMINISTIC", "0") == "1"
 # downsample BN) as its own apply pass before the 1x1 convs' data / weight
 # gradients instead of folding it through them (artsbir_conv1x1_dgrad_fold)
 FOLD_BN = [os.environ.get("ARTSBIR_FOLD_BN", "1") != "0"]
+# the layer-1 fold data gradients also accumulate their weight-gradient operands
+# (artsbir_conv1x1_dgrad_fold_wg): g and x read once for both gradients
+FOLD_WG = [os.environ.get("ARTSBIR_FOLD_WG", "1") != "0"]
 
 
 def set_deterministic(on: bool = True) -> bool:
@@ -981,11 +984,44 @@ class Engine:
              tag=f"dgrad_fold{'+bn1' if fused is not None else ''} {B}x{H}x{W}x{co}+{ci}->{ci}")
         return dx
 
-    def _wgrad_fold(self, g, x, conv, fw, coef, st: BNState, grads, cs=None):
+    def _fold_wg_ok(self, x, conv):
+        """whether the fold's data gradient also produces its weight-gradient
+        operands in the same pass (artsbir_conv1x1_dgrad_fold_wg's one-kernel
+        shapes: layer 1, Ci 64 under Co 256, whole 256-pixel tiles per segment)"""
+        B, H, W, ci = x.shape
+        return (FOLD_WG[0] and not SKIP_WGRAD[0] and self.dtype == torch.bfloat16 and ci == 64
+                and conv.weight.shape[0] == 256 and (B // self._G) * H * W % 256 == 0)
+
+    def _dgrad_fold_wg(self, g, x, fold, conv, fw, coef, st: BNState, grads, cs=None, fused=None):
+        """_dgrad_fold whose kernel also accumulates g^T x and x^T x per segment
+        (artsbir_conv1x1_dgrad_fold_wg): the weight gradient then needs only the
+        small combine on the side stream, g and x are read once"""
+        wout, bias = fold
+        B, H, W, ci = x.shape
+        co = conv.weight.shape[0]
+        G = self._G
+        dx = self._empty(B, H, W, ci, device=x.device)
+        buf = torch.zeros(G * (co + ci) * ci, dtype=torch.float32, device=x.device)
+        P, gram = buf[:G * co * ci].view(G, co, ci), buf[G * co * ci:].view(G, ci, ci)
+        d = self._desc(B, H, W, ci, co, 1, 1, 1, 0)
+        px = B * H * W
+        es = dx.element_size()
+        nb = es * (px * co + px * ci + G * ci * (co + ci) + px * ci + (px * ci if fused is not None else 0)) \
+            + 4 * G * (co + ci) * ci
+        call("artsbir_conv1x1_dgrad_fold_wg", d, ptr(g), ptr(x), ptr(wout), ptr(bias), ptr(dx),
+             ctypes.byref(fused[0]) if fused is not None else None, G, 4 * ci, ptr(P), ptr(gram), _s(),
+             kernel="auto", flops=4.0 * px * ci * (co + ci), nbytes=float(nb),
+             tag=f"dgrad_fold_wg{'+bn1' if fused is not None else ''} {B}x{H}x{W}x{co}+{ci}->{ci}")
+        self._wgrad_fold(g, x, conv, fw, coef, st, grads, cs, pg=(P, gram, buf))
+        return dx
+
+    def _wgrad_fold(self, g, x, conv, fw, coef, st: BNState, grads, cs=None, pg=None):
         """weight gradient of a 1x1 conv through the BatchNorm after it (side
         stream): per segment g^T x, the Gram matrix x^T x and the column sums of
         x (cs [G][slots][Ci], from the forward's act_pool, else a column-sum pass
-        here), combined by artsbir_bn_fold_wgrad_combine into the gradient buffer"""
+        here), combined by artsbir_bn_fold_wgrad_combine into the gradient buffer.
+        pg: (P, Gram, buffer) already accumulated on the main stream by
+        _dgrad_fold_wg (only the combine runs here)"""
         if SKIP_WGRAD[0]:
             return
         main = torch.cuda.current_stream()
@@ -1003,17 +1039,24 @@ class Engine:
             # combine's workspace (W in f32, T = W Gram)
             nP, nG = G * co * ci, G * ci * ci
             own_cs = cs is None
-            buf = torch.zeros(nP + nG + (G * ci if own_cs else 0), dtype=torch.float32, device=x.device)
-            P, gram = buf[:nP].view(G, co, ci), buf[nP:nP + nG].view(G, ci, ci)
-            if own_cs:
-                cs = buf[nP + nG:].view(G, 1, ci)
+            if pg is not None:
+                P, gram, buf = pg
+                if own_cs:
+                    cs = torch.zeros(G, 1, ci, dtype=torch.float32, device=x.device)
+                    self._side_keep.append(cs)
+            else:
+                buf = torch.zeros(nP + nG + (G * ci if own_cs else 0), dtype=torch.float32, device=x.device)
+                P, gram = buf[:nP].view(G, co, ci), buf[nP:nP + nG].view(G, ci, ci)
+                if own_cs:
+                    cs = buf[nP + nG:].view(G, 1, ci)
             wsp = torch.empty(co * ci * (G + 1), dtype=torch.float32, device=x.device)
             for s in range(G):
                 gs, xs = g[s * Bs:(s + 1) * Bs], x[s * Bs:(s + 1) * Bs]
                 # g_s^T x_s and x_s^T x_s, one launch (the x rows read once for both)
-                call("artsbir_gemm_tn2", self.dt, Ms, co, ci, ci, ptr(gs), co, ptr(xs), ci, ptr(xs), ci, ptr(P[s]),
-                     ptr(gram[s]), _s(), kernel="auto", flops=2.0 * Ms * (co + ci) * ci,
-                     nbytes=float(es * Ms * (co + ci) + 4 * (co + ci) * ci), tag=f"wgrad_fold {Ms}x{co}+{ci}x{ci}")
+                if pg is None:
+                    call("artsbir_gemm_tn2", self.dt, Ms, co, ci, ci, ptr(gs), co, ptr(xs), ci, ptr(xs), ci,
+                         ptr(P[s]), ptr(gram[s]), _s(), kernel="auto", flops=2.0 * Ms * (co + ci) * ci,
+                         nbytes=float(es * Ms * (co + ci) + 4 * (co + ci) * ci), tag=f"wgrad_fold {Ms}x{co}+{ci}x{ci}")
                 if own_cs:
                     call("artsbir_colsum", self.dt, ptr(xs), Ms, ci, ci, ptr(cs[s]), _s(), kernel="colsum_kernel",
                          nbytes=float(es * Ms * ci), tag=f"colsum {Ms}x{ci}")
@@ -1055,14 +1098,19 @@ class Engine:
         c3out = c3in.shape[:3] + (blk.conv3.weight.shape[1],)
         if fold:
             fw3 = self._fold_weights(bp["conv3"], blk.conv3, coefs[0], b3)
-            self._wgrad_fold(dout, p2, blk.conv3, bp["conv3"][0], coefs[0], b3, grads, c.get("cs2"))
-            if s == 1:
-                f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2)
+            wg3 = self._fold_wg_ok(p2, blk.conv3)
+            wargs = (blk.conv3, bp["conv3"][0], coefs[0], b3, grads, c.get("cs2"))
+            if not wg3:
+                self._wgrad_fold(dout, p2, *wargs)
+            f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2) if s == 1 else None
+            if wg3:
+                g2 = self._dgrad_fold_wg(dout, p2, fw3, *wargs, fused=f2)
+            else:
                 g2 = self._dgrad_fold(dout, p2, fw3, blk.conv3, fused=f2)
+            if s == 1:
                 dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
             else:
-                dp = self._dgrad_fold(dout, p2, fw3, blk.conv3)
-                dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s)
+                dy2, = self._bn_bwd(1, g2, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s)
         else:
             dy3 = dys[0]
             held = self._wgrad_pre(dy3, c3in, blk.conv3, 1, 0, grads)
@@ -1091,8 +1139,12 @@ class Engine:
             dconv = blk.downsample[1]
             if fold:
                 fwd_ = self._fold_weights(bp["down"], dconv, coefs[1], bd)
-                self._wgrad_fold(dout, din, dconv, bp["down"][0], coefs[1], bd, grads, c.get("csd"))
-                res = self._dgrad_fold(dout, din, fwd_, dconv)
+                wargs = (dconv, bp["down"][0], coefs[1], bd, grads, c.get("csd"))
+                if self._fold_wg_ok(din, dconv):
+                    res = self._dgrad_fold_wg(dout, din, fwd_, *wargs)
+                else:
+                    self._wgrad_fold(dout, din, *wargs)
+                    res = self._dgrad_fold(dout, din, fwd_, dconv)
             else:
                 dyd = dys[1]
                 held = self._wgrad_pre(dyd, Act(din), dconv, 1, 0, grads)

@@ -140,6 +140,15 @@ int artsbir_conv2d_dgrad_bnb(const artsbir_conv_desc* d, const void* dy, const v
 int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
                                const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
                                long long param_stride, void* stream);
+/* artsbir_conv1x1_dgrad_fold plus the operands of the conv's weight gradient
+ * through the BN (artsbir_bn_fold_wgrad_combine), from the same read of g and x:
+ * P[s][co][ci] += sum over segment s of g[m][co] x[m][ci] and
+ * gram[s][k][ci] += sum x[m][k] x[m][ci] (f32, accumulated: zero them first).
+ * One kernel for layer-1 shapes (Ci = 64, Co = 256, bf16), else the data
+ * gradient followed by artsbir_gemm_tn2 per segment. */
+int artsbir_conv1x1_dgrad_fold_wg(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                                  const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                                  long long param_stride, float* P, float* gram, void* stream);
 /* Weights of artsbir_conv1x1_dgrad_fold for every BN segment s:
  * wout[s][ci][co] = c1_s[co] W[co][ci], wout[s][ci][Co + k] = sum_co W[co][ci] b'_s[co] W[co][k]
  * (b' = -c1 c3 istd), bias[s][ci] = sum_co W[co][ci] (-c1 (c2 - c3 istd mean))[co].

@@ -345,3 +345,78 @@ def test_act_pool_colsum(B, G, H, W, C, pool, bn, dtype, dev):
     assert torch.equal(out, out2)
     o = out.double().cpu().reshape(G, -1, C)
     assert _rel(cs.double().cpu().sum(1), o.sum(1)) < 1e-5
+
+
+def _kind1_desc(B, G, H, W, Ci, dtype, dev, seed=9):
+    """a kind-1 fused BN-backward descriptor (the BN2 before the conv's input)"""
+    g2 = torch.Generator().manual_seed(seed)
+    y2 = torch.randn(B, H, W, Ci, generator=g2).to(dtype).double()
+    bnp = torch.zeros(G, 4, Ci)
+    bnp[:, 0] = torch.randn(G, Ci, generator=g2) * 0.1
+    bnp[:, 1] = torch.rand(G, Ci, generator=g2) + 0.5
+    bnp[:, 2] = bnp[:, 1] * (torch.rand(G, Ci, generator=g2) + 0.5)
+    bnp[:, 3] = torch.randn(G, Ci, generator=g2) * 0.2
+    y2d, bnpd = y2.to(dev, dtype), bnp.to(dev)
+    slots = torch.zeros(G, _hip.NSLOT, 2, Ci, device=dev)
+    desc = _hip.BnBwdDesc()
+    desc.dtype, desc.kind, desc.pool, desc.ntarget = _hip.dtype_code(dtype), 1, 0, 1
+    desc.mask_bn = bnpd.data_ptr()
+    desc.y[0] = y2d.data_ptr()
+    desc.mean[0] = bnpd.data_ptr()
+    desc.istd[0] = bnpd[0, 1].data_ptr()
+    desc.slots[0] = slots.data_ptr()
+    desc.B, desc.H, desc.W, desc.C = B, H, W, Ci
+    return desc, (y2, bnp, slots, y2d, bnpd)
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["plain", "bnb"])
+@pytest.mark.parametrize("dtype,case", [
+    (torch.bfloat16, (2, 3, 16, 16, 256, 64)),    # 2 tiles per segment, one per workgroup
+    (torch.bfloat16, (32, 3, 32, 32, 256, 64)),   # 384 tiles over 256 workgroups: segment changes mid-stream
+    (torch.bfloat16, (4, 1, 56, 56, 256, 64)),    # one segment, 49 tiles
+    (torch.bfloat16, (4, 3, 8, 8, 512, 128)),     # no one-kernel form: data gradient + gemm_tn2 per segment
+    (torch.float32, (2, 3, 16, 16, 256, 64)),     # f32: the fallback
+])
+def test_dgrad_fold_wg(case, dtype, fused, dev, cfg_env):
+    """artsbir_conv1x1_dgrad_fold_wg: the fold's data gradient and, from the same
+    read of g and x, P_s += g_s^T x_s and Gram_s += x_s^T x_s (the weight
+    gradient's operands), against float64; the one-kernel shapes must run the
+    pstream kernel whose loader waves accumulate P and Gram"""
+    os.environ.pop("ARTSBIR_PGEMM_CFG", None)
+    Bs, G, H, W, Co, Ci = case
+    B = Bs * G
+    gr, x, w, coef, prm, y = _problem(case, 13, dtype)
+    wout, bias, keep = _prep(w, coef, prm, G, dtype, dev)
+    _, dxr = _reference_dx(gr, x, w, coef, prm, y, G)
+    gd, xd = gr.to(dev, dtype), x.to(dev, dtype)
+    dx = torch.full((B, H, W, Ci), float("nan"), dtype=dtype, device=dev)
+    d = _hip.conv_desc(dtype, B, H, W, Ci, Co, 1, 1, 1, 0)
+    desc, aux = _kind1_desc(B, G, H, W, Ci, dtype, dev) if fused else (None, None)
+    gen = torch.Generator().manual_seed(3)
+    p0, q0 = torch.randn(G, Co, Ci, generator=gen), torch.randn(G, Ci, Ci, generator=gen)
+    P, gram = p0.clone().to(dev), q0.clone().to(dev)       # accumulated into
+    _hip.call("artsbir_conv1x1_dgrad_fold_wg", d, gd.data_ptr(), xd.data_ptr(), wout.data_ptr(), bias.data_ptr(),
+              dx.data_ptr(), desc, G, 4 * Ci, P.data_ptr(), gram.data_ptr(), _hip.stream())
+    torch.cuda.synchronize()
+    name = _hip.lib().artsbir_last_kernel().decode()
+    one_kernel = dtype == torch.bfloat16 and Ci == 64 and Co == 256
+    if one_kernel:
+        assert name == ("pstream_kernel<64,bnbk,fold,wg>" if fused else "pstream_kernel<64,fold,wg>"), name
+    xs, gs = x.reshape(G, -1, Ci), gr.reshape(G, -1, Co)
+    refP = torch.einsum("gpc,gpi->gci", gs, xs)
+    refG = torch.einsum("gpk,gpi->gki", xs, xs)
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert _rel(P.double().cpu() - p0.double(), refP) < tol
+    assert _rel(gram.double().cpu() - q0.double(), refG) < tol
+    ref = dxr
+    if fused:
+        y2, bnp, slots = aux[:3]
+        m = ((y2.reshape(G, -1, Ci) - bnp[:, 0].double()[:, None]) * bnp[:, 2].double()[:, None]
+             + bnp[:, 3].double()[:, None]) > 0
+        ref = (dxr.reshape(G, -1, Ci) * m).reshape(B, H, W, Ci)
+        rg = ref.reshape(G, -1, Ci)
+        s = slots.double().cpu().sum(1)
+        assert _rel(s[:, 0], rg.sum(1)) < 2e-2
+    out = dx.double().cpu()
+    assert torch.isfinite(out).all()
+    assert _rel(out, ref) < (1e-5 if dtype == torch.float32 else 1.5e-2)
