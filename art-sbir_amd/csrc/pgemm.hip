@@ -252,9 +252,30 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
   }
   if constexpr (GLB) {
     const int slot = (int)(blockIdx.x % ARTSBIR_NSLOT);
-    EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
-    pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true, X2>(a, acc, bpx, bch, wpx,
-                                                                                              wch, fr, fq, red, sgg);
+#ifndef PG_GLB_OLD
+#define PG_GLB_OLD 0
+#endif
+    if constexpr (PG_GLB_OLD || NW >= 8) {  // channel pairs outside (the 8-wave tile: 128 VGPRs)
+      EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
+      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true, X2>(a, acc, bpx, bch, wpx,
+                                                                                                wch, fr, fq, red, sgg);
+    } else {
+      // the 8-wave 256 x 128 tile runs at 128 VGPRs (two workgroups per CU):
+      // statistics reduced per (tile, pair) there, carried in registers otherwise
+      // statistics carried in registers across the pixel tiles; the BN constants
+      // from an LDS table where the registers allow (4 waves: 168 VGPRs), else
+      // from the L1-resident parameter vectors (8 waves: 128 VGPRs)
+      constexpr bool SP = true, TBL = NW < 8;
+      float* tprm = reinterpret_cast<float*>(smem);  // the stage ring is free after the main loop
+      if constexpr (BNB && TBL) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave is done reading the stages
+        pg_prm_fill<BCH, 64 * NW>(a, tprm, bpx, bch, seg0);
+        __syncthreads();
+      }
+      pg_epilogue_glb<BK, TWO, BCH, MTC, NTP, WTPX, WTCH, X2, SP, TBL>(a, acc, bpx, bch, wpx, wch, fr, fq, red,
+                                                                       tprm, seg0);
+    }
     if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
     return;
   }

@@ -9,6 +9,9 @@
 namespace artsbir {
 
 #define PG_OOB 0x80000000u
+#ifndef PG_SNAKE
+#define PG_SNAKE 1  // GLB epilogue: odd channel pairs walk the pixel tiles backwards (pg_epilogue_k)
+#endif
 #ifndef PG_PRIO
 #define PG_PRIO 1
 #endif
@@ -625,7 +628,10 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
     constexpr bool GLOBAL_OPS = !REG && (GLB || (RESK && !S_RES) || (TWO && !S_Y1) || (BK == 2 && !S_MK) || BK == 0);
     constexpr int EJ = (GLOBAL_OPS && NTP >= EJB) ? EJB : 1;
 #pragma unroll
-    for (int j0 = 0; j0 < NTP; j0 += EJ) {
+    for (int jj = 0; jj < NTP; jj += EJ) {
+      // GLB: odd channel pairs walk the pixel tiles backwards, so the lines whose
+      // first 64-B half the previous pair read last are re-read first (still in L2)
+      const int j0 = (GLB && PG_SNAKE && (p & 1)) ? NTP - EJ - jj : jj;
       Vec16<bf16> rv[EJ], y0v[EJ], mkv[EJ], y1v[EJ];
       unsigned mbits[EJ];
 #pragma unroll
@@ -753,6 +759,190 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
           atomicAdd(rb + (ch0 - bch) + e, s1[e]);
           atomicAdd(rb + BCH + (ch0 - bch) + e, s2[e]);
           if constexpr (TWO) atomicAdd(rb + 2 * BCH + (ch0 - bch) + e, s3[e]);
+        }
+      }
+    }
+  }
+}
+
+// The global-operand (GLB) form of pg_epilogue_k with the loops turned round:
+// pixel tile j outside, channel pair p inside, so a lane reads the two 64-B
+// halves of each 128-B residual / BN-target / mask line (pairs p = 0, 1 of the
+// wave's 64 channels) one right after the other.  pg_epilogue_k walks all the
+// wave's pixel tiles for pair 0 before pair 1, and at every L2 read request
+// being 128 B the line is often evicted in between and fetched twice (the
+// 1.3x traffic of the fused BN-backward dgrads).  The per-pair
+// statistics stay in registers across the tiles (SP: both pairs) or, when the
+// register budget does not hold them, are reduced per (tile, pair).  The BN
+// constants come from the LDS table prm (pg_prm_fill, in the stage ring the
+// main loop has left) per use.
+template <int BK, bool TWO, int BCH, int MTC, int NTP, int WTPX, int WTCH, bool FB, bool SP, bool TBL>
+__device__ __forceinline__ void pg_epilogue_glb(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
+                                                int wpx, int wch, int fr, int fq, float* red, const float* prm,
+                                                long long seg0) {
+  constexpr bool BNB = BK != 0;
+  constexpr bool RESK = BK == 2 || BK == 3;
+  constexpr int NP = MTC / 2;
+  const int HoWo = a.Ho * a.Wo;
+  const long long wpx0 = bpx + wpx * WTPX;
+  float* rb = red + stats_rseg(a, bpx, wpx0) * 3 * BCH;
+  const long long wseg = a.seg_m > 0 ? (wpx0 < a.M ? wpx0 : a.M - 1) / a.seg_m : 0;
+  const bool sums = (BNB || a.stats != nullptr) && !(a.dbg & 2);
+  const bool res = RESK || (BK == 0 && a.res_mode != 0);
+  const float rsc = a.res_mode == 2 ? 0.25f : 1.f;
+  // BN constants: rows of the LDS table (TBL) or the parameter vectors; + channel
+  const long long po0 = wseg * a.bnb_pstride;
+  const float* tp = prm + (int)(wseg - seg0) * PG_PRM_ROWS * BCH - bch;
+  const float* r_is0 = TBL ? tp : a.bnb_istd[0] + po0;
+  const float* r_m0 = TBL ? tp + BCH : a.bnb_mean[0] + po0;
+  float sa[SP ? NP : 1][8], sb[SP ? NP : 1][8], sc[SP && TWO ? NP : 1][8];
+  if constexpr (SP) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { sa[p][e] = 0.f; sb[p][e] = 0.f; if constexpr (TWO) sc[p][e] = 0.f; }
+  }
+  // reduce a pair's 16 pixel lanes (DPP) and add them into the block accumulator
+  auto flush = [&](float (&s1)[8], float (&s2)[8], float (&s3)[8], int ch0, bool chok) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s1[e] = dpp_row_sum(s1[e]); s2[e] = dpp_row_sum(s2[e]); }
+    if constexpr (TWO) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s3[e] = dpp_row_sum(s3[e]);
+    }
+    if (fr == 15 && chok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        atomicAdd(rb + (ch0 - bch) + e, s1[e]);
+        atomicAdd(rb + BCH + (ch0 - bch) + e, s2[e]);
+        if constexpr (TWO) atomicAdd(rb + 2 * BCH + (ch0 - bch) + e, s3[e]);
+      }
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < NTP; ++j) {
+    const long long px = wpx0 + j * 16 + fr;
+    const long long pc = px < a.M ? px : a.M - 1;
+    long long ri = pc;
+    if (res && a.res_mode == 2) {
+      const long long img = pc / HoWo;
+      const int rem = (int)(pc - img * HoWo);
+      const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+      ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+      const bool chok = ch0 < a.Cout;
+      const int chc = chok ? ch0 : 0;
+      const bool ok = px < a.M && chok;
+      // operands of (tile j, pair p): the loads of pair p + 1 follow right after
+      Vec16<bf16> rv, y0v, mkv, y1v;
+      unsigned mbits = 0;
+      if (res) rv = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + chc);
+      if constexpr (BNB) {
+        y0v = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[0]) + pc * a.ldy + chc);
+        if constexpr (BK == 2) mkv = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_mask) + pc * a.ldy + chc);
+        if constexpr (BK == 3) mbits = reinterpret_cast<const unsigned char*>(a.bnb_mask)[pc * (a.Cout >> 3) + (chc >> 3)];
+        if constexpr (TWO) y1v = ld16<bf16>(reinterpret_cast<const bf16*>(a.bnb_y[1]) + pc * a.ldy + chc);
+      }
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+      if constexpr (FB) {
+        float fbias[8];
+        loadf8v(a.bias + wseg * a.bias_sstride + chc, fbias);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += fbias[e];
+      }
+      if (BK == 0 && a.res_mode == 3) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= pg_quickgelu_grad(to_f(rv.v[e]));
+      } else if (res) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += rsc * to_f(rv.v[e]);
+      }
+      if constexpr (BK == 0 && !FB) {
+        if (a.bias) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += a.bias[chc + e];
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+      }
+      float t1[8], t2[8], t3[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { t1[e] = 0.f; t2[e] = 0.f; t3[e] = 0.f; }
+      if constexpr (BNB) {
+        float xa0[8], m0[8];
+        loadf8v(r_is0 + chc, xa0);
+        loadf8v(r_m0 + chc, m0);
+        float mm[BK == 1 ? 8 : 1], ms[BK == 1 ? 8 : 1], mh[BK == 1 ? 8 : 1];
+        if constexpr (BK == 1) {
+          loadf8v((TBL ? tp + 4 * BCH : a.bnb_mbn + po0) + chc, mm);
+          loadf8v((TBL ? tp + 5 * BCH : a.bnb_mbn + 2 * a.Cout + po0) + chc, ms);
+          loadf8v((TBL ? tp + 6 * BCH : a.bnb_mbn + 3 * a.Cout + po0) + chc, mh);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float yv = to_f(y0v.v[e]);
+          bool keep;
+          if constexpr (BK == 1) keep = (yv - mm[e]) * ms[e] + mh[e] > 0.f;
+          else if constexpr (BK == 3) keep = ((mbits >> e) & 1u) != 0u;
+          else keep = to_f(mkv.v[e]) > 0.f;
+          v[e] = (keep && ok) ? v[e] : 0.f;  // tail rows/channels add nothing to the sums
+          t1[e] = v[e];
+          t2[e] = v[e] * ((yv - m0[e]) * xa0[e]);
+        }
+        if constexpr (TWO) {
+          float xa1[8], m1[8];
+          loadf8v((TBL ? tp + 2 * BCH : a.bnb_istd[1] + po0) + chc, xa1);
+          loadf8v((TBL ? tp + 3 * BCH : a.bnb_mean[1] + po0) + chc, m1);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) t3[e] = v[e] * ((to_f(y1v.v[e]) - m1[e]) * xa1[e]);
+        }
+      } else if (a.stats) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float w = ok ? v[e] : 0.f;
+          t1[e] = w;
+          t2[e] = w * w;
+        }
+      }
+      if (ok) {
+        Vec16<bf16> o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+        typedef __attribute__((ext_vector_type(4))) unsigned pg_u4;
+        __builtin_nontemporal_store(*reinterpret_cast<const pg_u4*>(&o),
+                                    reinterpret_cast<pg_u4*>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0));
+      }
+      if (sums) {
+        if constexpr (SP) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sa[p][e] += t1[e];
+            sb[p][e] += t2[e];
+            if constexpr (TWO) sc[p][e] += t3[e];
+          }
+        } else {
+          flush(t1, t2, t3, ch0, chok);
+        }
+      }
+    }
+  }
+  if constexpr (SP) {
+    if (sums) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
+        if constexpr (TWO) {
+          flush(sa[p], sb[p], sc[p], ch0, ch0 < a.Cout);
+        } else {
+          float unused[8];
+          flush(sa[p], sb[p], unused, ch0, ch0 < a.Cout);
         }
       }
     }
