@@ -324,6 +324,19 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
   if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, slot, lane, bpx, BPX);
 }
 
+#ifndef PG_NOL
+#define PG_NOL 0  // 1: normalize-on-load cost probe of a diagnostic build only (pstream_kernel)
+#endif
+// Cost probe (round 5, tools/gpu/r5_nol.sh) for a consumer-side BatchNorm + ReLU
+// on pstream_kernel's pixel fragments: relu(s * x + b) per input channel in f32,
+// repacked to bf16, with coefficients read from LDS per 32-k step.  Wrong
+// results by design (the coefficients are scratch); only the time matters.
+__device__ __forceinline__ unsigned pg_nol2(unsigned w, float s0, float s1, float b0, float b1) {
+  const float lo = fmaxf(fmaf(__uint_as_float(w << 16), s0, b0), 0.f);
+  const float hi = fmaxf(fmaf(__uint_as_float(w & 0xffff0000u), s1, b1), 0.f);
+  return (__float_as_uint(lo) >> 16) | (__float_as_uint(hi) & 0xffff0000u);
+}
+
 // ---------------------------------------------------------------------------
 // Persistent producer/consumer variant for layers with many 256-pixel tiles
 // (stem, layer1-3, low K).  4 loader waves only issue LDS-DMA, so their vmcnt
@@ -531,6 +544,21 @@ __global__ void __launch_bounds__(768) pstream_kernel(PgArgs a, int ntiles) {
 #pragma unroll
         for (int j = 0; j < NTP; ++j)
           bv[j] = *reinterpret_cast<const uint4*>(pxs + (wpx * WTPX + j * 16 + fr) * ROWB + so);
+#if PG_NOL
+        {
+          const char* cbase = reinterpret_cast<const char*>(red) + fq * 32;
+          const f32x4 cs0 = *reinterpret_cast<const f32x4*>(cbase), cs1 = *reinterpret_cast<const f32x4*>(cbase + 16);
+          const f32x4 cb0 = *reinterpret_cast<const f32x4*>(cbase + 128);
+          const f32x4 cb1 = *reinterpret_cast<const f32x4*>(cbase + 144);
+#pragma unroll
+          for (int j = 0; j < NTP; ++j) {
+            bv[j].x = pg_nol2(bv[j].x, cs0[0], cs0[1], cb0[0], cb0[1]);
+            bv[j].y = pg_nol2(bv[j].y, cs0[2], cs0[3], cb0[2], cb0[3]);
+            bv[j].z = pg_nol2(bv[j].z, cs1[0], cs1[1], cb1[0], cb1[1]);
+            bv[j].w = pg_nol2(bv[j].w, cs1[2], cs1[3], cb1[2], cb1[3]);
+          }
+        }
+#endif
         PG_PRIO_ON();
 #pragma unroll
         for (int i = 0; i < MTC; ++i)
