@@ -1431,6 +1431,20 @@ static bool pg_fold_launch(const PgArgs& a, int c, hipStream_t st) {
       set_last_kernel(k1 ? "pstream_kernel<64,bnbk,fold>" : bch == 64 ? "pstream_kernel<64,fold>" : "pstream_kernel<128,fold>");
       return true;
     }
+    case 17: {  // the persistent streaming kernel with 32-channel blocks (four tiles per pixel panel)
+      if (!pg_fold_ok(a, 256, 64) || a.Cout < 32 || a.Cout % 32) return false;
+      const long long nt = ntl(256, 32);
+      if (nt > 0x7fffffffLL) return false;
+      const int grid = (int)(nt < 256 ? nt : 256);
+      if (k1)
+        hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, false, true, false, 1, false, 64, true>), dim3(grid), dim3(768), 0,
+                           st, a, (int)nt);
+      else
+        hipLaunchKernelGGL((pstream_kernel<32, 8, 1, 4, false, false, false, 0, false, 64, true>), dim3(grid), dim3(768),
+                           0, st, a, (int)nt);
+      set_last_kernel(k1 ? "pstream_kernel<32,bnbk,fold>" : "pstream_kernel<32,fold>");
+      return true;
+    }
     default:
       return false;
   }

@@ -83,8 +83,11 @@ def short(name):
             return f"{k}<{t[0]},{t[1]}{f',w{t[2]}x{t[3]}' if t[0] == t[1] == '256' else ''}>"
         if k == "hwgrad_kernel":  # <CT, OT, TR, NWC>: the 4-wave 64 x 64 variant is named w4
             return f"{k}<{t[0]},{t[1]}{',w4' if t[0] == t[1] == '64' and t[3] == '4' else ''}>"
-        if k == "pstream_kernel":  # <BCH, WPX, WCH, NSTAGE, MULTI, BNB, FWDS, BK, TWO, KS, X2>
+        if k == "pw256_kernel":  # <DENSE>
+            return f"{k}<{'dense' if t[0] == 'true' else 'conv'}>"
+        if k == "pstream_kernel":  # <BCH, WPX, WCH, NSTAGE, MULTI, BNB, FWDS, BK, TWO, KS, X2, WGK>
             fold = ",fold" if len(t) > 10 and t[10] == "true" else ""
+            fold += ",wg" if len(t) > 11 and t[11] not in ("0", "") else ""
             if len(t) > 9 and t[9] == "32":
                 return f"{k}<{t[0]},k32>"
             if t[5] == "true":
