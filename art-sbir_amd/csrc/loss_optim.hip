@@ -7,31 +7,40 @@
 
 namespace artsbir {
 
-// one wave per triplet row; dist[2*B] saved for the backward
-__global__ void __launch_bounds__(256) triplet_fwd_kernel(const float* __restrict__ a, const float* __restrict__ p,
-                                                          const float* __restrict__ n, int B, int D, float margin,
-                                                          float eps, float* __restrict__ dist, float* __restrict__ loss) {
-  __shared__ float part[4];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  float total = 0.f;
-  for (int r = wid; r < B; r += 4) {
-    float sp = 0.f, sn = 0.f;
-    for (int d = lane; d < D; d += 64) {
-      const float av = a[(long long)r * D + d];
-      const float dpv = av - p[(long long)r * D + d] + eps;
-      const float dnv = av - n[(long long)r * D + d] + eps;
-      sp += dpv * dpv;
-      sn += dnv * dnv;
-    }
-    sp = warp_sum(sp);
-    sn = warp_sum(sn);
-    const float dap = sqrtf(sp), dan = sqrtf(sn);
-    if (lane == 0) { dist[2 * r] = dap; dist[2 * r + 1] = dan; }
-    total += fmaxf(margin + dap - dan, 0.f);
+// one wave per triplet row, B/4 workgroups; dist[2*B] saved for the backward
+// (the per-row arithmetic of the single-workgroup form this replaced: one
+// workgroup walked all rows, ~0.5 ms at B = 512)
+__global__ void __launch_bounds__(256) triplet_rows_kernel(const float* __restrict__ a, const float* __restrict__ p,
+                                                           const float* __restrict__ n, int B, int D, float eps,
+                                                           float* __restrict__ dist) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float sp = 0.f, sn = 0.f;
+  for (int d = lane; d < D; d += 64) {
+    const float av = a[(long long)r * D + d];
+    const float dpv = av - p[(long long)r * D + d] + eps;
+    const float dnv = av - n[(long long)r * D + d] + eps;
+    sp += dpv * dpv;
+    sn += dnv * dnv;
   }
-  if (lane == 0) part[wid] = total;
+  sp = warp_sum(sp);
+  sn = warp_sum(sn);
+  if (lane == 0) { dist[2 * r] = sqrtf(sp); dist[2 * r + 1] = sqrtf(sn); }
+}
+
+// mean of the hinge over the rows in a fixed order: four partial sums over rows
+// w, w + 4, ... then their sum (the single-workgroup form's order, bit for bit)
+__global__ void triplet_mean_kernel(const float* __restrict__ dist, int B, float margin, float* __restrict__ loss) {
+  __shared__ float part[4];
+  const int w = threadIdx.x;
+  if (w < 4) {
+    float total = 0.f;
+    for (int r = w; r < B; r += 4) total += fmaxf(margin + dist[2 * r] - dist[2 * r + 1], 0.f);
+    part[w] = total;
+  }
   __syncthreads();
-  if (threadIdx.x == 0) loss[0] = (part[0] + part[1] + part[2] + part[3]) / (float)B;
+  if (w == 0) loss[0] = (part[0] + part[1] + part[2] + part[3]) / (float)B;
 }
 
 __global__ void triplet_bwd_kernel(const float* __restrict__ a, const float* __restrict__ p, const float* __restrict__ n,
@@ -99,7 +108,9 @@ using namespace artsbir;
 extern "C" int artsbir_triplet_fwd(const float* a, const float* p, const float* n, int B, int D, float margin, float eps,
                                    float* dist, float* loss, void* stream) {
   if (B <= 0) { set_error("triplet_fwd: empty batch"); return -1; }
-  hipLaunchKernelGGL(triplet_fwd_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, a, p, n, B, D, margin, eps, dist, loss);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(triplet_rows_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, a, p, n, B, D, eps, dist);
+  hipLaunchKernelGGL(triplet_mean_kernel, dim3(1), dim3(64), 0, st, dist, B, margin, loss);
   ARTSBIR_CHECK_LAUNCH("triplet_fwd");
   return 0;
 }

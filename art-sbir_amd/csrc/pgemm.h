@@ -55,6 +55,9 @@ struct PgArgs {
   // wg_gram[seg][k - C1][Cout] += sum_m x2[m][k - C1] x2[m][co] (f32, atomics)
   float* wg_p = nullptr;
   float* wg_gram = nullptr;
+  // forward with BN statistics (pg_epilogue_fwd): store the output non-temporally
+  // (candidates 24 / 25: the persistent kernels 10 / 15 with this set)
+  int nts = 0;
 };
 
 // Weight gradient dW[co][k] += sum_m dY[m][co] * Xcol[m][k] (pwgrad.hip).

@@ -22,9 +22,11 @@
 //    zeros written to LDS.
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "common.h"
 #include "pgemm.h"
+#include "../../include/artsbir.h"
 
 #include "pgemm_dev.h"
 
@@ -1496,6 +1498,22 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (c >= 11 && c <= 13) return pg_pf_launch(c, a, multi, st);
   if (c == 14) return pstream_bnb_launch(a, multi, st);
   if (c == 15) return pstream_k32_launch(a, multi, st);
+  if (c == 24 || c == 25) {  // 10 / 15 with the forward-statistics epilogue's stores non-temporal
+    if (!a.stats || a.bnb || a.bias || a.relu) return false;
+    PgArgs b = a;
+    b.nts = 1;
+    if (!pgemm_launch_cfg(b, c == 24 ? 10 : 15, st)) return false;
+    const std::string base = artsbir_last_kernel();
+    static const char* nt_names[] = {"pstream_kernel<32,nt>", "pstream_kernel<64,nt>", "pstream_kernel<128,nt>",
+                                     "pstream_kernel<64,k32,nt>", "pstream_kernel<128,k32,nt>"};
+    const char* nm = base == "pstream_kernel<32>"       ? nt_names[0]
+                     : base == "pstream_kernel<64>"     ? nt_names[1]
+                     : base == "pstream_kernel<128>"    ? nt_names[2]
+                     : base == "pstream_kernel<64,k32>" ? nt_names[3]
+                                                        : nt_names[4];
+    set_last_kernel(nm);
+    return true;
+  }
   if (c == 16) return pg_glb_launch(a, multi, st);
   if (c == 18) return pg_glb2_launch(a, multi, st);
   if (c == 19) return pg_k32w8_launch(a, multi, st);

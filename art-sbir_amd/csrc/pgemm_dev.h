@@ -1004,27 +1004,36 @@ __device__ __forceinline__ void pg_epilogue_fwd(const PgArgs& a, const f32x4 (&a
     w.seg = seg;
     w.bch = bch;
   }
+  // a.nts: non-temporal stores (no L2 allocation for the output lines); they
+  // pay on the 28^2 .. 7^2 1x1 forwards (-10..-20 %), not at 56^2 (+8 %), so
+  // the autotuner picks per shape (candidates 24 / 25, profiles/r5_fwd_stores.txt)
+  constexpr int NP = MTC / 2;
+  const bool nts = a.nts != 0;
 #pragma unroll
-  for (int p = 0; p < MTC / 2; ++p) {
+  for (int it = 0; it < NP * NTP; ++it) {
+    const int p = it / NTP, j = it % NTP;
     const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
     const bool chok = ch0 < a.Cout;
+    const long long px = wpx0 + j * 16 + fr;
+    const bool ok = px < a.M && chok;
+    float v[8];
 #pragma unroll
-    for (int j = 0; j < NTP; ++j) {
-      const long long px = wpx0 + j * 16 + fr;
-      const bool ok = px < a.M && chok;
-      float v[8];
+    for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j][r]; v[4 + r] = acc[2 * p + 1][j][r]; }
+    for (int e = 0; e < 8; ++e) {
+      const float u = ok ? v[e] : 0.f;
+      w.s1[p][e] += u;
+      w.s2[p][e] += u * u;
+    }
+    if (ok) {
+      Vec16<bf16> o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float u = ok ? v[e] : 0.f;
-        w.s1[p][e] += u;
-        w.s2[p][e] += u * u;
-      }
-      if (ok) {
-        Vec16<bf16> o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+      for (int e = 0; e < 8; ++e) o.v[e] = from_f<bf16>(v[e]);
+      if (nts) {
+        typedef __attribute__((ext_vector_type(4))) unsigned pg_u4;
+        __builtin_nontemporal_store(*reinterpret_cast<const pg_u4*>(&o),
+                                    reinterpret_cast<pg_u4*>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0));
+      } else {
         st16<bf16>(reinterpret_cast<bf16*>(a.y) + px * a.ldy + ch0, o);
       }
     }

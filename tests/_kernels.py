@@ -30,6 +30,8 @@ CONV = {
     "20": r"sconv_kernel<",
     "21": r"hconv_kernel<",
     "22": r"pp256_kernel(<bnb>)?$",
+    "24": r"pstream_kernel<(32|64|128),nt>$",
+    "25": r"pstream_kernel<(64|128),k32,nt>$",
 }
 
 

@@ -29,7 +29,7 @@ CASES = [
     (2, 32, 16, 32, 64, 3, 3, 1, 1),    # halo-tiled, 16 x 16 tiles, 32 -> 64 channels
     (3, 17, 23, 64, 32, 3, 3, 1, 1),    # halo-tiled, 8 x 16 tiles with row and column tails
 ]
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21", "22"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "15", "16", "19", "20", "21", "22", "24", "25"]
 
 
 @pytest.fixture
