@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 
 import torch  # noqa: F401  (must be imported before the library is dlopen'ed)
 
@@ -228,12 +229,15 @@ class HipError(RuntimeError):
 # that declares its algorithmic work is bracketed by two timing events on the
 # current stream and (kernel, flops, bytes, start, end, tag, stream) is appended.
 PROFILE = None
+HOST_TS = None  # list: host time of every profiled launch (diagnostics)
 
 
 def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes: float = 0.0,
          tag: str | None = None) -> None:
     """Invoke a status-returning entry point; map a non-zero status to HipError."""
     prof = PROFILE
+    if HOST_TS is not None and prof is not None and kernel is not None:
+        HOST_TS.append(time.perf_counter())  # host enqueue time of this launch (tools/step_gaps.py --host)
     if prof is not None and kernel is not None:
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)

@@ -364,6 +364,21 @@ class Engine:
         call("artsbir_gemm_tn", self.dt, M, N, K, ptr(dy), ldd, ptr(x), ldx, ptr(dw), _s(),
              kernel="auto", flops=2.0 * M * N * K, tag=f"gemm_tn {M}x{N}x{K}")
 
+    def _side_gemm_tn(self, M, N, K, dy, ldd, x, ldx, dw):
+        """_gemm_tn of a weight gradient on the side stream (as _wgrad), its
+        operands held until the backward's stream join"""
+        if not OVERLAP_WGRAD or SKIP_WGRAD[0]:
+            if not SKIP_WGRAD[0]:
+                self._gemm_tn(M, N, K, dy, ldd, x, ldx, dw)
+            return
+        main = torch.cuda.current_stream()
+        side = self._side_stream(dy.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self._gemm_tn(M, N, K, dy, ldd, x, ldx, dw)
+        self._side_keep.append(dy)
+        self._side_keep.append(x)
+
     def _conv(self, a: Act, fw, cout, R, S, stride, pad, stats_buf=None):
         B, H, W, C = a.shape
         Ho = (H + 2 * pad - R) // stride + 1
@@ -714,7 +729,10 @@ class Engine:
         else:
             doutT = self._empty(B, D, device=dev)
             call("artsbir_cast", _hip.DT_F32, ptr(dout), self.dt, ptr(doutT), B * D, _s())
-        self._gemm_tn(B, D, C, doutT, D, o, C, grads[ap.c_proj.weight])
+        # the head's weight gradients (c_proj, then q and k|v below) on the side
+        # stream, idle at this point of the backward: the k|v one (B*Tk rows) is
+        # ~0.65 ms that the main stream's data-gradient chain no longer waits for
+        self._side_gemm_tn(B, D, C, doutT, D, o, C, grads[ap.c_proj.weight])
         _, wcT, _ = pk["c"]
         do = torch.empty(B, C, dtype=torch.float32, device=dev)
         self._gemm_nt(B, C, D, doutT, D, wcT, do, C, 1, 0, None)
@@ -724,8 +742,8 @@ class Engine:
              _s())
         call("artsbir_colsum", self.dt, ptr(dq), B, C, C, ptr(grads[ap.q_proj.bias]), _s())
         call("artsbir_colsum", self.dt, ptr(dkv), B * Tk, 2 * C, 2 * C, ptr(grads[ap.k_proj.bias]), _s())
-        self._gemm_tn(B, C, C, dq, C, tok, Tk * C, grads[ap.q_proj.weight])
-        self._gemm_tn(B * Tk, 2 * C, C, dkv, 2 * C, tok, C, grads[ap.k_proj.weight])
+        self._side_gemm_tn(B, C, C, dq, C, tok, Tk * C, grads[ap.q_proj.weight])
+        self._side_gemm_tn(B * Tk, 2 * C, C, dkv, 2 * C, tok, C, grads[ap.k_proj.weight])
         _, wkvT, _ = pk["kv"]
         _, wqT, _ = pk["q"]
         Hs, Ws = c["hw"]

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--mode", default="overlap", choices=["overlap", "skip", "serial"])
     ap.add_argument("--side-tail", type=int, default=25, help="side-stream launches listed after main's last one")
     ap.add_argument("--by-tag", type=int, default=0, help="also list the N largest (kernel, tag) groups")
+    ap.add_argument("--pre", type=int, default=0, help="steps enqueued (no sync) before the profiled one")
+    ap.add_argument("--host", action="store_true", help="main-stream launches the GPU reached before the host issued them")
     args = ap.parse_args()
     import _hip
     import bench
@@ -67,8 +69,12 @@ def main():
     torch.cuda.synchronize()
     wall_plain = (time.perf_counter() - t0) * 1e3
     prof = []
+    hts = [] if args.host else None
+    _hip.HOST_TS = hts
     ref = torch.cuda.Event(enable_timing=True)
     ref.record()
+    for _ in range(args.pre):  # the GPU is still busy with these when the profiled step is issued
+        step()
     _hip.PROFILE = prof
     t0 = time.perf_counter()
     step()
@@ -77,6 +83,7 @@ def main():
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) * 1e3
     _hip.PROFILE = None
+    _hip.HOST_TS = None
     main_id = main.cuda_stream
     rows = []
     for kname, fl, nb, e0, e1, tag, sid in prof:
@@ -111,6 +118,21 @@ def main():
             print(f"    {s:8.2f} - {e:8.2f} ms  {k:40s} {t}")
     if args.by_tag:
         _by_tag(rows, args.by_tag)
+    if hts is not None and len(hts) == len(prof):
+        # host issue time (ms from the step's start) vs the GPU start of the same
+        # launch: where the GPU start is within 30 us after the host issue, the
+        # stream was idle waiting for the host (host-bound stretch)
+        t_host = [(h - t0) * 1e3 for h in hts]
+        bound = []
+        for (kname, fl, nb, e0, e1, tag, sid), th in zip(prof, t_host):
+            if sid != main_id:
+                continue
+            tg = ref.elapsed_time(e0)
+            if tg - th < 0.03:
+                bound.append((th, tg, kname, tag or ""))
+        print(f"  main-stream launches started within 30 us of their host issue: {len(bound)}")
+        for th, tg, k, t in bound[:40]:
+            print(f"    host {th:8.2f} ms  gpu {tg:8.2f} ms  {k:40s} {t}")
 
 
 def _by_tag(rows, n):
