@@ -418,14 +418,22 @@ class _PatchFunction(torch.autograd.Function):
     """conv1 (patch x patch, stride patch, no bias) as patchify + GEMM: [B,3,R,R] -> [B*P, E]"""
 
     @staticmethod
-    def forward(ctx, img, weight, dtype, patch):
-        B, _, R, _ = img.shape
+    def forward(ctx, img, weight, dtype, patch, more=()):
+        """img, then any further image batches of the same shape (the other
+        branches of forward_branches): their patch rows follow in one buffer,
+        so the branches are never concatenated as images"""
+        imgs = (img,) + tuple(more)
+        Bi, _, R, _ = img.shape
+        B = Bi * len(imgs)
         E = weight.shape[0]
         K = 3 * patch * patch
         P = (R // patch) ** 2
         rows = torch.empty(B * P, K, dtype=dtype, device=img.device)
-        call("artsbir_vit_patchify", _hip.dtype_code(dtype), img.contiguous().float().data_ptr(), B, R, patch,
-             rows.data_ptr(), _st())
+        for i, im in enumerate(imgs):
+            if im.shape != img.shape:
+                raise ValueError(f"branch {i}: image batch {tuple(im.shape)} != {tuple(img.shape)}")
+            call("artsbir_vit_patchify", _hip.dtype_code(dtype), im.contiguous().float().data_ptr(), Bi, R, patch,
+                 rows[i * Bi * P:].data_ptr(), _st())
         out = _gemm(rows, _as(weight.view(E, K), dtype), B * P, E, K)
         ctx.save_for_backward(rows)
         ctx.wshape = weight.shape
@@ -436,7 +444,7 @@ class _PatchFunction(torch.autograd.Function):
         rows, = ctx.saved_tensors
         dw = torch.zeros(ctx.wshape, dtype=torch.float32, device=rows.device)
         _wgrad(dout.contiguous().to(rows.dtype), rows, dw.view(ctx.wshape[0], -1))
-        return None, dw, None, None
+        return None, dw, None, None, None
 
 
 class _TokensFunction(torch.autograd.Function):
@@ -527,13 +535,13 @@ class VisionTransformer(nn.Module):
     def freeze_layers(self):
         self.trained_layers.append('all')
 
-    def forward(self, x):
+    def forward(self, x, more=()):
         fp8 = self.compute_dtype == "fp8"
         dtype = torch.bfloat16 if fp8 else self.compute_dtype
         for blk in self.transformer.resblocks:
             blk.fp8 = fp8
-        B = x.shape[0]
-        t = _PatchFunction.apply(x, self.conv1.weight, dtype, self.patch_size)
+        B = x.shape[0] * (1 + len(more))
+        t = _PatchFunction.apply(x, self.conv1.weight, dtype, self.patch_size, tuple(more))
         t = _TokensFunction.apply(t, self.class_embedding, self.positional_embedding, B)
         t = self.ln_pre(t)
         t = self.transformer(t)
@@ -542,5 +550,9 @@ class VisionTransformer(nn.Module):
 
     def forward_branches(self, xs):
         """the three branch calls of train.py:28-30 (no BatchNorm here: one batched call is exact)"""
-        out = self.forward(torch.cat(list(xs)))
+        xs = list(xs)
+        if all(x.shape == xs[0].shape for x in xs):
+            out = self.forward(xs[0], tuple(xs[1:]))
+        else:
+            out = self.forward(torch.cat(xs))
         return list(out.chunk(len(xs)))
