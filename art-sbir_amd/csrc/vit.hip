@@ -312,6 +312,169 @@ __global__ void __launch_bounds__(256) layernorm_bwd_v_kernel(const T* __restric
   }
 }
 
+// LayerNorm backward for bf16 rows of C = 256 NC columns (ViT-B: 768): lane l
+// owns the 4-column chunks l + 64 u, u < NC (8-B loads and stores, every lane
+// busy; the 8-column form leaves half the lanes idle in its second chunk at
+// C = 768 and holds 232-248 VGPRs, so one row in flight per wave: ~36 KB of
+// loads in flight per CU, ~3 TB/s).  At ~150 VGPRs this one keeps PF = 2 rows
+// in flight per wave at the same two waves per SIMD.  Same arithmetic as
+// ln_bwd_row (row sums in another order); dgamma / dbeta (and with SUMS the
+// column sums of dres and dx) reduced over the block's 4 waves in LDS, then
+// one atomic per column per block
+template <int NC>
+struct Ln4Row {
+  uint2 x[NC], g[NC], r[NC];
+};
+__device__ __forceinline__ void ln4_cvt(uint2 v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+template <int NC, bool RES>
+__device__ __forceinline__ void ln4_fetch(const bf16* __restrict__ x, const bf16* __restrict__ dy, const bf16* dres,
+                                          long long row, int lane, Ln4Row<NC>& R) {
+  constexpr int C = 256 * NC;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const long long o = row * C + 4 * (lane + 64 * u);
+    R.x[u] = *reinterpret_cast<const uint2*>(x + o);
+    R.g[u] = *reinterpret_cast<const uint2*>(dy + o);
+    if (RES) R.r[u] = *reinterpret_cast<const uint2*>(dres + o);
+  }
+}
+template <int NC, bool SUMS, bool RES>
+__device__ __forceinline__ void ln4_row(const Ln4Row<NC>& R, bf16* __restrict__ dx, long long row, float eps, int lane,
+                                        const float (&gm)[NC][4], float (&pg)[NC][4], float (&pb)[NC][4],
+                                        float (&pr)[NC][4], float (&po)[NC][4]) {
+  constexpr int C = 256 * NC;
+  float xv[NC][4], gv[NC][4], res[NC][4];
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    ln4_cvt(R.x[u], xv[u]);
+    ln4_cvt(R.g[u], gv[u]);
+    if (RES) ln4_cvt(R.r[u], res[u]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (!RES) res[u][e] = 0.f;
+      s += xv[u][e];
+    }
+  }
+  const float mean = warp_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int u = 0; u < NC; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += (xv[u][e] - mean) * (xv[u][e] - mean);
+  const float istd = rsqrtf(warp_sum(q) / (float)C + eps);
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int u = 0; u < NC; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (xv[u][e] - mean) * istd;
+      const float g = gv[u][e] * gm[u][e];
+      a += g;
+      b += g * xh;
+      pg[u][e] += gv[u][e] * xh;
+      pb[u][e] += gv[u][e];
+      xv[u][e] = xh;
+      gv[u][e] = g;
+    }
+  a = warp_sum(a) / (float)C;
+  b = warp_sum(b) / (float)C;
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    float out[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) out[e] = istd * (gv[u][e] - a - xv[u][e] * b) + res[u][e];
+    uint2 h;
+    h.x = (unsigned)__builtin_bit_cast(unsigned short, (bf16)out[0]) |
+          ((unsigned)__builtin_bit_cast(unsigned short, (bf16)out[1]) << 16);
+    h.y = (unsigned)__builtin_bit_cast(unsigned short, (bf16)out[2]) |
+          ((unsigned)__builtin_bit_cast(unsigned short, (bf16)out[3]) << 16);
+    *reinterpret_cast<uint2*>(dx + row * C + 4 * (lane + 64 * u)) = h;
+    if constexpr (SUMS) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { pr[u][e] += res[u][e]; po[u][e] += out[e]; }
+    }
+  }
+}
+template <int NC, bool SUMS, int PF>
+__global__ void __launch_bounds__(256) layernorm_bwd_c4_kernel(const bf16* __restrict__ x,
+                                                               const float* __restrict__ gamma,
+                                                               const bf16* __restrict__ dy, long long rows, float eps,
+                                                               const bf16* dres, bf16* dx, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta, float* __restrict__ dres_sum,
+                                                               float* __restrict__ dx_sum) {
+  constexpr int NR = SUMS ? 4 : 2;
+  constexpr int C = 256 * NC;
+  __shared__ float red[NR][3][C];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float pg[NC][4], pb[NC][4], gm[NC][4], pr[NC][4], po[NC][4];
+#pragma unroll
+  for (int u = 0; u < NC; ++u) {
+    const float4 g4 = *reinterpret_cast<const float4*>(gamma + 4 * (lane + 64 * u));
+    gm[u][0] = g4.x; gm[u][1] = g4.y; gm[u][2] = g4.z; gm[u][3] = g4.w;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { pg[u][e] = 0.f; pb[u][e] = 0.f; pr[u][e] = 0.f; po[u][e] = 0.f; }
+  }
+  const long long stride = gridDim.x * 4LL;
+  long long row = blockIdx.x * 4LL + w;
+  if (row < rows) {
+    // rows PF strides ahead in flight (past the end the last row is re-fetched:
+    // no branch around the loads)
+    Ln4Row<NC> cur, n1, n2;
+    if (dres) {
+      ln4_fetch<NC, true>(x, dy, dres, row, lane, cur);
+      if (PF == 2) ln4_fetch<NC, true>(x, dy, dres, min(row + stride, rows - 1), lane, n1);
+    } else {
+      ln4_fetch<NC, false>(x, dy, dres, row, lane, cur);
+      if (PF == 2) ln4_fetch<NC, false>(x, dy, dres, min(row + stride, rows - 1), lane, n1);
+    }
+    for (; row < rows; row += stride) {
+      const long long rn = min(row + PF * stride, rows - 1);
+      if (dres) {
+        ln4_fetch<NC, true>(x, dy, dres, rn, lane, PF == 2 ? n2 : n1);
+        ln4_row<NC, SUMS, true>(cur, dx, row, eps, lane, gm, pg, pb, pr, po);
+      } else {
+        ln4_fetch<NC, false>(x, dy, dres, rn, lane, PF == 2 ? n2 : n1);
+        ln4_row<NC, SUMS, false>(cur, dx, row, eps, lane, gm, pg, pb, pr, po);
+      }
+      cur = n1;
+      if (PF == 2) n1 = n2;
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int u = 0; u < NC; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * (lane + 64 * u) + e;
+        red[0][w - 1][i] = pg[u][e];
+        red[1][w - 1][i] = pb[u][e];
+        if constexpr (SUMS) {
+          red[NR - 2][w - 1][i] = pr[u][e];
+          red[NR - 1][w - 1][i] = po[u][e];
+        }
+      }
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int u = 0; u < NC; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * (lane + 64 * u) + e;
+        atomicAdd(dgamma + i, pg[u][e] + red[0][0][i] + red[0][1][i] + red[0][2][i]);
+        atomicAdd(dbeta + i, pb[u][e] + red[1][0][i] + red[1][1][i] + red[1][2][i]);
+        if constexpr (SUMS) {
+          if (dres_sum) atomicAdd(dres_sum + i, pr[u][e] + red[NR - 2][0][i] + red[NR - 2][1][i] + red[NR - 2][2][i]);
+          if (dx_sum) atomicAdd(dx_sum + i, po[u][e] + red[NR - 1][0][i] + red[NR - 1][1][i] + red[NR - 1][2][i]);
+        }
+      }
+  }
+}
+
 // y = (x - mean) / sqrt(var + eps) * gamma + beta per row, in fp32 whatever
 // the storage dtype (models.py:382-388); one wave per row
 template <typename T>
@@ -846,6 +1009,26 @@ static int layernorm_bwd_impl(int dtype, const void* x, const float* gamma, cons
   if (vec) {  // 8-column chunks per lane; 512 blocks: few atomics per column
     long long gv = (rows + 3) / 4;
     const unsigned gridv = (unsigned)(gv > 512 ? 512 : gv);
+    // bf16 rows of 256 / 512 / 768 / 1024 columns: the 4-column form with two
+    // rows in flight per wave (ARTSBIR_LN_C4=0: the 8-column form, timing comparison)
+    static const bool c4 = [] { const char* e = getenv("ARTSBIR_LN_C4"); return !e || atoi(e) != 0; }();
+    if (c4 && dtype == ARTSBIR_DT_BF16 && C % 256 == 0 && C <= 1024) {
+      hipStream_t st = (hipStream_t)stream;
+#define LNB4(N, S) hipLaunchKernelGGL((layernorm_bwd_c4_kernel<N, S, 2>), dim3(gridv), dim3(256), 0, st, (const bf16*)x, \
+                                      gamma, (const bf16*)dy, rows, eps, (const bf16*)dres, (bf16*)dx, dgamma, dbeta,     \
+                                      dres_sum, dx_sum)
+#define LNB4S(N) do { if (sums) LNB4(N, true); else LNB4(N, false); } while (0)
+      switch (C / 256) {
+        case 1: LNB4S(1); break;
+        case 2: LNB4S(2); break;
+        case 3: LNB4S(3); break;
+        default: LNB4S(4); break;
+      }
+#undef LNB4S
+#undef LNB4
+      ARTSBIR_CHECK_LAUNCH("layernorm_bwd");
+      return 0;
+    }
 #define LNBV(N, S) VIT_DISPATCH(dtype, hipLaunchKernelGGL((layernorm_bwd_v_kernel<T, N, S>), dim3(gridv), dim3(256), 0, \
                                                          (hipStream_t)stream, (const T*)x, gamma, (const T*)dy, rows,  \
                                                          C, eps, (const T*)dres, (T*)dx, dgamma, dbeta, dres_sum,      \

@@ -451,3 +451,46 @@ def test_fp8_gemm_gelu_matches_gemm_then_quickgelu(M, N, K, dev):
     q1, s1 = vit._fp8(gg, pm)
     q2, s2 = vit._fp8(g_ref)
     assert torch.equal(q1, q2) and torch.equal(s1, s2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [256, 768, 1024, 520])
+@pytest.mark.parametrize("rows", [37, 2500])
+@pytest.mark.parametrize("sums", [False, True])
+def test_layernorm_bwd_bf16_forms(dev, C, rows, sums):
+    """artsbir_layernorm_bwd(_sums) on bf16 rows against float64 autograd of the
+    oracle LayerNorm on the same (bf16-rounded) inputs: the 4-column form
+    (C % 256 == 0, two rows in flight per wave) and the 8-column form (C = 520).
+    dx is stored in bf16 (tolerance 1e-2 relative); dgamma / dbeta and the
+    column sums of dres and dx are f32 sums over the rows (1e-4)"""
+    import _hip
+    g = torch.Generator().manual_seed(C + rows)
+    x = torch.randn(rows, C, generator=g).bfloat16()
+    gam, bet = 1 + 0.1 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    dy = torch.randn(rows, C, generator=g).bfloat16()
+    res = torch.randn(rows, C, generator=g).bfloat16()
+    xr = x.double().requires_grad_(True)
+    gr, br = gam.double().requires_grad_(True), bet.double().requires_grad_(True)
+    (oenc.layernorm_fp32(xr, gr, br) * dy.double()).sum().backward()
+    want_dx = xr.grad + res.double()
+    X, G, Dy, Rs = (t.to(dev) for t in (x, gam, dy, res))
+    dx = torch.empty_like(X)
+    dg = torch.zeros(C, device=dev)
+    db = torch.zeros(C, device=dev)
+    st = _hip.stream()
+    if sums:
+        rsum = torch.zeros(C, device=dev)
+        xsum = torch.zeros(C, device=dev)
+        _hip.call("artsbir_layernorm_bwd_sums", _hip.DT_BF16, X.data_ptr(), G.data_ptr(), Dy.data_ptr(), rows, C,
+                  1e-5, Rs.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), rsum.data_ptr(), xsum.data_ptr(),
+                  st)
+    else:
+        _hip.call("artsbir_layernorm_bwd", _hip.DT_BF16, X.data_ptr(), G.data_ptr(), Dy.data_ptr(), rows, C, 1e-5,
+                  Rs.data_ptr(), dx.data_ptr(), dg.data_ptr(), db.data_ptr(), st)
+    torch.cuda.synchronize()
+    rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(dx, want_dx) < 1e-2
+    assert rel(dg, gr.grad) < 1e-4 and rel(db, br.grad) < 1e-4
+    if sums:
+        assert rel(rsum, res.double().sum(0)) < 1e-4
+        assert rel(xsum, want_dx.sum(0)) < 1e-4  # the f32 values before dx's rounding to bf16
