@@ -424,8 +424,18 @@ __device__ __forceinline__ void f8_gelu_row4(T* __restrict__ C, bf16* __restrict
 // stores alike, so a load issued after a store waits for that store too: RD 1
 // issues pass p + 1's loads before pass p's stores, and no load waits behind
 // the output traffic.
-template <typename T, int RD, int BN>
-__global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
+//
+// BM 128 (with BN 128, tile code 2, forced only): a 128 x 128 tile of 4 waves
+// (2 x 2 of 64 x 64) on a 2-stage ring of 32 KB stages, two workgroups per CU,
+// so one workgroup's prologue and epilogue run beside the other's k-loop (the
+// 256-row tiles are one workgroup per CU: their epilogue, 0.34 of out_proj's
+// 0.58 ms, leaves the matrix pipe idle).  Slower on all four C5 shapes all the
+// same (qkv 0.98 vs 0.85 ms, out_proj 0.64 vs 0.57, c_fc 1.10 vs 0.98, c_proj
+// 0.91 vs 0.84; without the epilogue's traffic 2.88 vs 2.59 ms per block;
+// C5 210.8 vs 205.3 ms/step, profiles/r5_fp8_tile128.txt)
+template <typename T, int RD, int BN, int BM = 256>
+__global__ void __launch_bounds__(BM == 256 ? 512 : 256, BM == 256 ? 1 : 2)
+    gemm_fp8_v2_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
                                                           const unsigned char* __restrict__ B,
                                                           const float* __restrict__ sa, const float* __restrict__ sb,
                                                           const float* __restrict__ bias, T* __restrict__ C,
@@ -437,11 +447,14 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   // 3-stage ring of 48 KB stages, two in flight: at ~1 us of MFMA per stage the
   // single stage in flight of the 256-wide tile leaves every k-step waiting on
   // its L2/HBM round trip
-  constexpr int NST = BN == 256 ? 2 : 3;
+  static_assert(BM == 256 || BN == 128, "the 128-row tile is 128 wide");
+  constexpr int NW = BM == 256 ? 8 : 4;             // waves
+  constexpr int NST = (BN == 256 || BM == 128) ? 2 : 3;
   constexpr int MI = BN == 256 ? 8 : 4;             // 16-row MFMA tiles per wave
-  constexpr int SB = 256 * 128 + BN * 128;          // stage bytes: A [256][128] | B [BN][128]
-  constexpr int NPB = BN / 64;                      // B pieces per wave
-  constexpr int PER_STAGE = 4 + NPB;                // LDS-DMA instructions per wave per stage
+  constexpr int SB = BM * 128 + BN * 128;           // stage bytes: A [BM][128] | B [BN][128]
+  constexpr int NPA = BM / 8 / NW;                  // A pieces (1 KB, 8 rows) per wave
+  constexpr int NPB = BN / 8 / NW;                  // B pieces per wave
+  constexpr int PER_STAGE = NPA + NPB;              // LDS-DMA instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char smem[NST][SB];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -452,7 +465,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
     const long long q = G / 8, r = G % 8, x = lid % 8;
     lid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + lid / 8;
   }
-  const int m0 = (int)(lid / tiles_n) * 256, n0 = (int)(lid % tiles_n) * BN;
+  const int m0 = (int)(lid / tiles_n) * BM, n0 = (int)(lid % tiles_n) * BN;
   const int wm = BN == 256 ? (wid >> 2) * 128 : (wid >> 1) * 64;
   const int wn = BN == 256 ? (wid & 3) * 64 : (wid & 1) * 64;
   const int nk = K / 128;
@@ -464,16 +477,16 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   const int lrow = lane >> 3, lslot = lane & 7;
   auto issue = [&](int kt, int buf) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int piece = wid + 8 * u, row = piece * 8 + lrow;
+    for (int u = 0; u < NPA; ++u) {
+      const int piece = wid + NW * u, row = piece * 8 + lrow;
       const unsigned off = (unsigned)(row * K + kt * 128 + ((lslot ^ (row & 7)) << 4));
       f8_glds16(ra, &smem[buf][piece * 1024], off);
     }
 #pragma unroll
     for (int u = 0; u < NPB; ++u) {
-      const int piece = wid + 8 * u, row = piece * 8 + lrow;
+      const int piece = wid + NW * u, row = piece * 8 + lrow;
       const unsigned off = (unsigned)(row * K + kt * 128 + ((lslot ^ (row & 7)) << 4));
-      f8_glds16(rb, &smem[buf][256 * 128 + piece * 1024], off);
+      f8_glds16(rb, &smem[buf][BM * 128 + piece * 1024], off);
     }
   };
   f32x4 acc[MI][4];
@@ -499,7 +512,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
       if (kt + 2 < nk) issue(kt + 2, (kt + 2) % 3);  // the stage consumed at kt - 1: every wave is past it
     }
     const char* ai = &smem[buf][0];
-    const char* bi = &smem[buf][256 * 128];
+    const char* bi = &smem[buf][BM * 128];
     i32x8 bfr[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) bfr[j] = f8_frag(bi, wn + 16 * j + fr, kq);
@@ -517,7 +530,7 @@ __global__ void __launch_bounds__(512) gemm_fp8_v2_kernel(int M, int N, int K, c
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
   constexpr int EP = 68;  // f32 row pitch of a wave's block
-  static_assert(8 * 32 * EP * 4 <= NST * SB, "epilogue blocks fit the ring");
+  static_assert(NW * 32 * EP * 4 <= NST * SB, "epilogue blocks fit the ring");
   float* eb = reinterpret_cast<float*>(&smem[0][0]) + wid * 32 * EP;
   const float s = sa[0] * sb[0];
   const int ec = (lane & 15) * 4, er = lane >> 4;  // this lane's 4 columns, row phase
@@ -663,9 +676,36 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
 // in flight, epilogue from the registers by buffer stores) ran 12-29 % slower
 // on all four shapes (qkv 1.06 vs 0.93, out_proj 0.76 vs 0.59, c_fc 1.34 vs
 // 1.14, c_proj 0.96 vs 0.83 ms; profiles/r4_fp8_attn.txt) and was dropped
-static int fp8_bn(int N) {
-  static const int forced = [] { const char* e = getenv("ARTSBIR_FP8_BN"); return e ? atoi(e) : 0; }();
-  return forced == 128 ? 128 : 256;
+//
+// tile codes: 0 the 256 x 256 tile, 1 256 x 128 (ARTSBIR_FP8_BN=128), 2 the
+// 128 x 128 tile at two workgroups per CU; ARTSBIR_FP8_TILE forces one
+static int fp8_tile(int M, int N, int K) {
+  static const int forced = [] {
+    const char* e = getenv("ARTSBIR_FP8_TILE");
+    if (e) return atoi(e);
+    const char* b = getenv("ARTSBIR_FP8_BN");
+    return b && atoi(b) == 128 ? 1 : -1;
+  }();
+  (void)M; (void)N; (void)K;
+  return forced >= 0 && forced <= 2 ? forced : 0;
+}
+template <typename T, int RD>
+static void fp8_v2_launch(int tile, int M, int N, int K, const unsigned char* a, const unsigned char* b,
+                          const float* sa, const float* sb, const float* bias, T* c, int accumulate, const bf16* res,
+                          bf16* out2, int skip_c, unsigned* pmax, hipStream_t st) {
+  if (tile == 2) {
+    const unsigned g = (unsigned)((long long)((M + 127) / 128) * ((N + 127) / 128));
+    hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, RD, 128, 128>), dim3(g), dim3(256), 0, st, M, N, K, a, b, sa, sb, bias,
+                       c, accumulate, res, out2, skip_c, pmax);
+  } else if (tile == 1) {
+    const unsigned g = (unsigned)((long long)((M + 255) / 256) * ((N + 127) / 128));
+    hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, RD, 128>), dim3(g), dim3(512), 0, st, M, N, K, a, b, sa, sb, bias, c,
+                       accumulate, res, out2, skip_c, pmax);
+  } else {
+    const unsigned g = (unsigned)((long long)((M + 255) / 256) * ((N + 255) / 256));
+    hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, RD, 256>), dim3(g), dim3(512), 0, st, M, N, K, a, b, sa, sb, bias, c,
+                       accumulate, res, out2, skip_c, pmax);
+  }
 }
 
 extern "C" int artsbir_gemm_nt_fp8(int M, int N, int K, const unsigned char* a, const unsigned char* b,
@@ -689,9 +729,7 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
   if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8: too many tiles"); return -1; }
   hipStream_t st = (hipStream_t)stream;
   const char* old = getenv("ARTSBIR_FP8_V1");
-  if (M >= 256 && N >= 256 && !(old && atoi(old))) {  // 256 x BN LDS-DMA kernel
-    const int bn = fp8_bn(N);
-    const long long t2 = (long long)((M + 255) / 256) * ((N + bn - 1) / bn);
+  if (M >= 256 && N >= 256 && !(old && atoi(old))) {  // the LDS-DMA kernel
     if ((long long)M * K > 0x7fffffffLL || (long long)N * K > 0x7fffffffLL) {
       set_error("gemm_nt_fp8: operand larger than 2 GiB");
       return -1;
@@ -701,35 +739,17 @@ extern "C" int artsbir_gemm_nt_fp8_ex(int M, int N, int K, const unsigned char* 
       accumulate = 0; res = nullptr; out2 = nullptr; skip_c = 1;
     }
     const int nrd = (accumulate ? 1 : 0) + (res ? 1 : 0);
-    set_last_kernel("gemm_fp8_v2_kernel");
-    if (nrd == 0) {
-      if (bn == 128)
-        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0, 128>), dim3((unsigned)t2), dim3(512), 0,
-                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                                 (bf16*)out2, skip_c, nullptr));
-      else
-        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 0, 256>), dim3((unsigned)t2), dim3(512), 0,
-                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                                 (bf16*)out2, skip_c, nullptr));
-    } else if (nrd == 1) {
-      if (bn == 128)
-        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1, 128>), dim3((unsigned)t2), dim3(512), 0,
-                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                                 (bf16*)out2, skip_c, nullptr));
-      else
-        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 1, 256>), dim3((unsigned)t2), dim3(512), 0,
-                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                                 (bf16*)out2, skip_c, nullptr));
-    } else {
-      if (bn == 128)
-        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2, 128>), dim3((unsigned)t2), dim3(512), 0,
-                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                                 (bf16*)out2, skip_c, nullptr));
-      else
-        FP8_DISPATCH(out_dtype, hipLaunchKernelGGL((gemm_fp8_v2_kernel<T, 2, 256>), dim3((unsigned)t2), dim3(512), 0,
-                                                 st, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate, (const bf16*)res,
-                                                 (bf16*)out2, skip_c, nullptr));
-    }
+    const int tile = fp8_tile(M, N, K);
+    set_last_kernel(tile == 2 ? "gemm_fp8_v2_kernel<128x128>" : "gemm_fp8_v2_kernel");
+    if (nrd == 0)
+      FP8_DISPATCH(out_dtype, fp8_v2_launch<T, 0>(tile, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate,
+                                                  (const bf16*)res, (bf16*)out2, skip_c, nullptr, st));
+    else if (nrd == 1)
+      FP8_DISPATCH(out_dtype, fp8_v2_launch<T, 1>(tile, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate,
+                                                  (const bf16*)res, (bf16*)out2, skip_c, nullptr, st));
+    else
+      FP8_DISPATCH(out_dtype, fp8_v2_launch<T, 2>(tile, M, N, K, a, b, sa, sb, bias, (T*)c, accumulate,
+                                                  (const bf16*)res, (bf16*)out2, skip_c, nullptr, st));
   } else {
     set_last_kernel("gemm_fp8_kernel");
     FP8_DISPATCH(out_dtype, hipLaunchKernelGGL(gemm_fp8_kernel<T>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K,
@@ -754,19 +774,13 @@ extern "C" int artsbir_gemm_nt_fp8_gelu(int M, int N, int K, const unsigned char
   if (tiles > 0x7fffffffLL) { set_error("gemm_nt_fp8_gelu: too many tiles"); return -1; }
   hipStream_t st = (hipStream_t)stream;
   if (M >= 256 && N >= 256) {
-    const int bn = fp8_bn(N);
-    const long long t2 = (long long)((M + 255) / 256) * ((N + bn - 1) / bn);
     if ((long long)M * K > 0x7fffffffLL || (long long)N * K > 0x7fffffffLL) {
       set_error("gemm_nt_fp8_gelu: operand larger than 2 GiB");
       return -1;
     }
-    set_last_kernel("gemm_fp8_v2_kernel");
-    if (bn == 128)
-      hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0, 128>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa,
-                         sb, bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
-    else
-      hipLaunchKernelGGL((gemm_fp8_v2_kernel<bf16, 0, 256>), dim3((unsigned)t2), dim3(512), 0, st, M, N, K, a, b, sa,
-                         sb, bias, (bf16*)c, 0, (const bf16*)nullptr, (bf16*)out2, 0, pmax);
+    const int tile = fp8_tile(M, N, K);
+    set_last_kernel(tile == 2 ? "gemm_fp8_v2_kernel<128x128>" : "gemm_fp8_v2_kernel");
+    fp8_v2_launch<bf16, 0>(tile, M, N, K, a, b, sa, sb, bias, (bf16*)c, 0, nullptr, (bf16*)out2, 0, pmax, st);
   } else {
     set_last_kernel("gemm_fp8_kernel");
     hipLaunchKernelGGL(gemm_fp8_kernel<bf16>, dim3((unsigned)tiles), dim3(256), 0, st, M, N, K, a, b, sa, sb, bias,
