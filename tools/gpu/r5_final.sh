@@ -8,6 +8,6 @@ timeout -k 10 900 python -u bench.py > gpurun_out/r5_bench.json 2> gpurun_out/r5
 tail -c 600 gpurun_out/r5_bench.json; echo
 cd /tmp && export TMPDIR=/tmp
 rm -rf $R/gpurun_out/r5_prof
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/r5_prof -o run -- python3 $R/bench.py --no-cpu-baseline --no-c5 --no-embed --no-retrieval --no-preprocess --steps 5 --warmup 2 > $R/gpurun_out/r5_prof.log 2>&1 || { echo PROF_FAILED; tail -5 $R/gpurun_out/r5_prof.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/r5_prof -o run -- python3 $R/bench.py --no-cpu-baseline --no-c5 --no-embed --no-retrieval --no-preprocess --steps 5 --warmup 2 > $R/gpurun_out/r5_prof.log 2>&1 || { echo PROF_FAILED; tail -5 $R/gpurun_out/r5_prof.log; exit 1; }
 find $R/gpurun_out/r5_prof -name "*kernel_stats.csv" | head -3
 cd $R && timeout -k 10 300 python3 -u tools/fold_bench.py > gpurun_out/r5_fold_bench.txt 2>&1; tail -60 gpurun_out/r5_fold_bench.txt
