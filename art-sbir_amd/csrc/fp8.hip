@@ -432,7 +432,12 @@ __device__ __forceinline__ void f8_gelu_row4(T* __restrict__ C, bf16* __restrict
 // 0.58 ms, leaves the matrix pipe idle).  Slower on all four C5 shapes all the
 // same (qkv 0.98 vs 0.85 ms, out_proj 0.64 vs 0.57, c_fc 1.10 vs 0.98, c_proj
 // 0.91 vs 0.84; without the epilogue's traffic 2.88 vs 2.59 ms per block;
-// C5 210.8 vs 205.3 ms/step, profiles/r5_fp8_tile128.txt)
+// C5 210.8 vs 205.3 ms/step, profiles/r5_fp8_tile128.txt).  Two more schedules
+// of the 256 x 256 tile measured and dropped (profiles/r5_fp8_kloop.txt): 64-k
+// half-stages on v_mfma_scale_f32_32x32x64 with three of four 32 KB buffers in
+// flight (+4 %: the ring depth does not bound the k-loop), and the next
+// stage's eight LDS-DMA pieces issued one per row tile between the MFMAs
+// instead of after the barrier (-2 % standalone, C5 step unchanged)
 template <typename T, int RD, int BN, int BM = 256>
 __global__ void __launch_bounds__(BM == 256 ? 512 : 256, BM == 256 ? 1 : 2)
     gemm_fp8_v2_kernel(int M, int N, int K, const unsigned char* __restrict__ A,
