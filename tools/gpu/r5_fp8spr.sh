@@ -1,5 +1,6 @@
 #!/bin/bash
 # round 5: the fp8 256x256 kernel with its stage loads spread over the MFMAs (ARTSBIR_FP8_TILE=4)
+# (the kernels this compared were removed after the run: results in profiles/r5_fp8_kloop.txt)
 # against the 256 x 256 tile: parity with the tile forced, per-shape timings
 # (tools/fp8_bench.py), C5 bench legs
 set -o pipefail
