@@ -1725,6 +1725,27 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   if (tiles / need < tpc) tpc = tiles / need > 0 ? tiles / need : 1;
   const long long maxch = 60000 / (KT * 12);          // knn_merge's shared memory
   if ((tiles + tpc - 1) / tpc > maxch) tpc = (tiles + maxch - 1) / maxch;
+  static const bool balance = [] { const char* e = getenv("ARTSBIR_KNN_BALANCE"); return !e || atoi(e) != 0; }();
+  if (tpc_req <= 0 && p.v2 && Q > 0 && balance) {
+    // the v2 scan runs ceil(Q / 256) query tiles x nchunks workgroups, one per CU
+    // (140 KB of LDS): take the chunk length (at most 1/4 shorter) whose grid
+    // fills its last round of workgroups.  C4 (10k x 1M): 31 chunks of 256
+    // tiles = 1240 workgroups, 4.84 rounds on 256 CUs, the last chunk half
+    // full; 32 chunks of 245 tiles = 1280 = 5.00 rounds of 245 tiles
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0) {
+      const long long ntq = (Q + 255) / 256;
+      long long best = tpc, bestc = -1;
+      for (long long t = tpc; t >= (tpc * 3 + 3) / 4 && t >= 1; --t) {
+        const long long nch = (tiles + t - 1) / t;
+        if (nch > maxch || tiles / need < t) continue;
+        const long long cost = (ntq * nch + ncu - 1) / ncu * t;  // rounds x tiles per workgroup
+        if (bestc < 0 || cost < bestc) { bestc = cost; best = t; }
+      }
+      tpc = best;
+    }
+  }
   p.tpc = (int)tpc;
   p.nchunks = (int)((tiles + tpc - 1) / tpc);
   p.ncand = p.nchunks * KT;
