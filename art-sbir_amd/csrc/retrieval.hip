@@ -614,11 +614,18 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
 
   const __amdgpu_buffer_rsrc_t gr =
       rrsrc(reinterpret_cast<const char*>(a.g) + (long long)g0 * C::RB, (long long)(a.Ng - g0) * C::RB);
-  const int my_ni = wid < C::NI ? (C::NI - wid + V2_WAVES - 1) / V2_WAVES : 0;
+  // a tile is NI (33 at D = 512) 1-KB pieces over 8 waves: the wave issuing
+  // the odd piece rotates with the tile (KNN_ROT), so no wave is the one every
+  // barrier waits for
+#ifndef KNN_ROT
+#define KNN_ROT 1
+#endif
+  auto w_of = [&](int t) { return KNN_ROT ? (wid + t) & (V2_WAVES - 1) : wid; };
+  auto ni_of = [&](int t) { const int w2 = w_of(t); return w2 < C::NI ? (C::NI - w2 + V2_WAVES - 1) / V2_WAVES : 0; };
   auto issue_tile = [&](int t) {
     char* st = smem + (t % C::NST) * C::STAGE;
     const unsigned gb = (unsigned)(t * V2_ROWS * C::RB);
-    for (int i = wid; i < C::NI; i += V2_WAVES) rdma16(gr, st + i * 1024, gb + (unsigned)((i * 64 + lane) * 16));
+    for (int i = w_of(t); i < C::NI; i += V2_WAVES) rdma16(gr, st + i * 1024, gb + (unsigned)((i * 64 + lane) * 16));
   };
   issue_tile(0);
   if (ntiles > 1) issue_tile(1);
@@ -689,7 +696,13 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     // B fragments PF reads ahead of their MFMA, pinned in that order (left
     // alone, the scheduler either hoists all KB reads and runs out of registers
     // or issues each read just one MFMA before its use and exposes the LDS latency)
-    constexpr int PF = KB < 6 ? KB : 6;
+    // (KNN_PF: at 6 the kernel needs 256 VGPRs plus a 16-B spill whose reload
+    // before the first MFMA of every tile carried s_waitcnt vmcnt(0), draining
+    // the DMA ring each tile; 4 spills nothing)
+#ifndef KNN_PF
+#define KNN_PF 4
+#endif
+    constexpr int PF = KB < KNN_PF ? KB : KNN_PF;
     f32x16 acc = {};
     uint4 bq[KB];
 #ifndef KNN_ABL
@@ -718,7 +731,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     // wave's LDS.  An atomic of the previous epilogue forces the full wait.
     if (t + 1 < ntiles) {
       if (t + 2 < ntiles && !__builtin_amdgcn_ballot_w64(atom))
-        rvm_wait_n(my_ni);
+        rvm_wait_n(ni_of(t + 2));
       else
         rvm_wait<0>();
     }
