@@ -495,6 +495,11 @@ __device__ __forceinline__ void rvm_wait_n(int n) {
     case 3: rvm_wait<3>(); break;
     case 4: rvm_wait<4>(); break;
     case 5: rvm_wait<5>(); break;
+    case 6: rvm_wait<6>(); break;
+    case 7: rvm_wait<7>(); break;
+    case 8: rvm_wait<8>(); break;
+    case 9: rvm_wait<9>(); break;
+    case 10: rvm_wait<10>(); break;
     default: rvm_wait<0>(); break;
   }
 }
@@ -565,11 +570,22 @@ struct V2 {
   static constexpr int SLOTS = V2_ROWS * RB / 16;       // 16-B slots per tile
   static constexpr int NI = (SLOTS + 63) / 64;          // DMA instructions per tile
   static constexpr int STAGE = NI * 1024;
-  static constexpr int NST = 3;
+  // KNN_NST 4: three tiles in flight instead of two; the LDS it takes comes
+  // from the slow path's staging, which then holds half a wave's rows per pass.
+  // Measured slower again once the per-tile drain was gone (scan 11.2 -> 12.0 ms,
+  // profiles/r5_knn_nst4.txt; round 4's 4-stage build ran under that drain), so
+  // the DMA ring's depth does not bound the scan: 3 stays
+#ifndef KNN_NST
+#define KNN_NST 3
+#endif
+  static constexpr int NST = KNN_NST;
+  static constexpr int SROWS = NST == 4 ? 16 : 32;       // staged rows per slow-path pass
   static constexpr int SP = 33;                          // staging pitch (floats)
-  static constexpr int STG = V2_WAVES * 32 * SP * 4;
+  static constexpr int WSTG = SROWS * SP + (SROWS == 32 ? 0 : 32);  // + the 32 columns' |g|^2 (in the row padding at 32 rows)
+  static constexpr int STG = V2_WAVES * WSTG * 4;
   static constexpr int ROWS = V2_WAVES * 32;
   static constexpr int LDS = NST * STAGE + STG + 5 * ROWS * 4;
+  static_assert(LDS <= 163840, "LDS");
   static_assert((NI + V2_WAVES - 1) / V2_WAVES <= 5, "rvm_wait_n covers at most 5 DMA per wave");
 };
 
@@ -587,7 +603,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   using C = V2<KB>;
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   float* s_stage = reinterpret_cast<float*>(smem + C::NST * C::STAGE);
-  float* s_thr = s_stage + V2_WAVES * 32 * C::SP;  // [256] 16th smallest so far (-INF: row unused)
+  float* s_thr = s_stage + V2_WAVES * C::WSTG;     // [256] 16th smallest so far (-INF: row unused)
   float* s_crit = s_thr + C::ROWS;                 // [256] max(thr, band hi)
   float* s_lo = s_crit + C::ROWS;                  // [256] rank band (hi < 0: no band)
   float* s_hi = s_lo + C::ROWS;
@@ -629,6 +645,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   };
   issue_tile(0);
   if (ntiles > 1) issue_tile(1);
+  if (C::NST == 4 && ntiles > 2) issue_tile(2);
 
   const float* band_lo = a.lo;
   const float* band_hi = a.hi;
@@ -680,7 +697,9 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     }
   };
   load_crit();
-  float* stg = s_stage + wid * 32 * C::SP;
+  float* stg = s_stage + wid * C::WSTG;
+  float* sg = stg + (C::SROWS == 32 ? 32 : C::SROWS * C::SP);  // column c's |g|^2 at sg[c * gstr]
+  constexpr int gstr = C::SROWS == 32 ? C::SP : 1;
   const int q_own = qb + R_own;
   const float eps_own = q_own < a.Nq ? a.rel * sqrtf(a.qsq[q_own] * gmax) * 1.001f + 1e-3f : 0.f;
   float thr_g = s_thr[R_own];  // best shared bound seen (with thr0)
@@ -690,7 +709,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   bool atom = false;  // this wave issued a global atomic since its last DMA wait
   unsigned st_entries = 0, st_ins = 0;
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 2 < ntiles) issue_tile(t + 2);
+    if (t + C::NST - 1 < ntiles) issue_tile(t + C::NST - 1);
     const char* st = smem + (t % C::NST) * C::STAGE;
     const char* bp = st + r32 * C::RB + h * 16;
     // B fragments PF reads ahead of their MFMA, pinned in that order (left
@@ -730,10 +749,14 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     // tile t+3): the epilogue reads no stage, only gsq (saved above) and its own
     // wave's LDS.  An atomic of the previous epilogue forces the full wait.
     if (t + 1 < ntiles) {
-      if (t + 2 < ntiles && !__builtin_amdgcn_ballot_w64(atom))
-        rvm_wait_n(ni_of(t + 2));
-      else
+      if (t + 2 < ntiles && !__builtin_amdgcn_ballot_w64(atom)) {
+        if (C::NST == 4 && t + 3 < ntiles)
+          rvm_wait_n(ni_of(t + 2) + ni_of(t + 3));
+        else
+          rvm_wait_n(ni_of(t + 2));
+      } else {
         rvm_wait<0>();
+      }
     }
     atom = false;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage t (gsq) are done
@@ -751,29 +774,43 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
       // of each row re-evaluates its hits exactly (d2 with the same formula as
       // knn_scan_kernel): list insertion, certainly-closer count, uncertain queue
       unsigned mymask = 0;
-      if (lane < 32) stg[r32 * C::SP + 32] = gsq;  // column r32's |g|^2 (INF past Ng), in the row padding
+      if (lane < 32) sg[r32 * gstr] = gsq;  // column r32's |g|^2 (INF past Ng)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const unsigned long long m = __builtin_amdgcn_ballot_w64(fmaf(-2.f, acc[e], gsq) <= critp[e]);
         if (m) {
-          stg[((e & 3) + 8 * (e >> 2) + 4 * h) * C::SP + r32] = acc[e];
+          if (C::SROWS == 32) stg[((e & 3) + 8 * (e >> 2) + 4 * h) * C::SP + r32] = acc[e];
           if (oe == e) mymask = oh ? (unsigned)(m >> 32) : (unsigned)m;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
       bool changed = false;
       // every lane reads its (owner) row's state: lanes >= 32 mirror row lane - 32
       const float qs = s_qsq[R_own], hi = s_hi[R_own];
       float thr = s_thr[R_own];
-      if (lane < 32 && mymask) {
+      // SROWS 16: two passes, the rows of lane half hp (h == hp) staged at
+      // (e & 3) + 4 (e >> 2), their owners (oh == hp) evaluating in between
+#pragma unroll
+      for (int hp = 0; hp < (C::SROWS == 32 ? 1 : 2); ++hp) {
+      if (C::SROWS == 16) {
+        if (hp) {  // pass 0's owners are done with the staging
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+        if (h == hp) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) stg[((e & 3) + 4 * (e >> 2)) * C::SP + r32] = acc[e];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < 32 && mymask && (C::SROWS == 32 || oh == hp)) {
         const float lo = s_lo[R_own];
-        const float* srow = stg + orow * C::SP;
+        const float* srow = stg + (C::SROWS == 32 ? orow : oe) * C::SP;
         while (mymask) {
           const int c = __builtin_ctz(mymask);
           mymask &= mymask - 1;
           const bool valid = bn + c < a.Ng;
-          const float g2 = stg[c * C::SP + 32];
+          const float g2 = sg[c * gstr];
           const float d2 = fmaf(-2.f, srow[c], qs + g2);
           if (d2 < thr) {
             ++st_ins;
@@ -810,6 +847,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
           s_thr[R_own] = thr;
           s_crit[R_own] = fmaxf(thr, hi);
         }
+      }
       }
       if (__builtin_amdgcn_ballot_w64(changed)) {
         // refresh the prefilter bounds from the owner lanes' registers (readlane:
