@@ -28,5 +28,5 @@ for leg in ${LEGS:-train}; do
 done
 cd $R
 case " ${LEGS:-train} " in *" retr "*) P="gpurun_out/pmc_train gpurun_out/pmc_retr" ;; *) P="gpurun_out/pmc_train" ;; esac
-python3 profiles/summarize_pmc.py $P gpurun_out/r5_pmc_traffic.json || exit 1
+case " ${LEGS:-train} " in *" train "*) python3 profiles/summarize_pmc.py $P gpurun_out/r5_pmc_traffic.json ;; esac || exit 1
 echo summaries done
