@@ -559,7 +559,7 @@ constexpr int V2_ROWS = 32;  // gallery rows per tile
 // tiles between two exchanges of the shared per-query bound (power of two; env
 // ARTSBIR_KNN_KB=0 turns the exchange off in the one-call path)
 #ifndef KB_SYNC_TILES
-#define KB_SYNC_TILES 64
+#define KB_SYNC_TILES 128  // round 5, after the prefetch fix: 32 / 64 / 128 -> 11.44 / 11.20 / 11.14 ms (profiles/r5_knn_kb.txt)
 #endif
 constexpr int KB_SYNC = KB_SYNC_TILES;
 constexpr int V2_WAVES = 8;  // 8 x 32 = 256 queries per workgroup
