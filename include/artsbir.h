@@ -475,7 +475,10 @@ int artsbir_knn_exact_all(const float* q, const float* g, int D, int n, double* 
  *   positive (-1 if none).  dpos_in (nullable): for a shard call, the positive's
  *   key when it lives in another shard (artsbir_positive_key + a MAX all-reduce).
  * dtype: ARTSBIR_DT_BF16 (bf16 MFMA scan) or ARTSBIR_DT_F32 (f32 MFMA scan); the
- * result is exact either way.  1 <= k <= 64, N < 2^31.  tiles_per_chunk 0 = auto.
+ * result is exact either way.  1 <= k <= 64, N < 2^31.  tiles_per_chunk 0 = auto
+ * (bf16: up to 256 tiles of 128 rows, shortened so the scan's ceil(Q/256) x
+ * chunks workgroups fill whole rounds of the current device's CUs; the same
+ * choice in the workspace query and the call on one device).
  * workspace: device memory of artsbir_pairwise_l2_topk_workspace() bytes.  No
  * host synchronisation; the rare fallbacks (uncertain-queue overflow, a chunk
  * list that may have hidden a top-k item) run as device kernels. */
