@@ -1750,6 +1750,7 @@ std::vector<std::pair<hipEvent_t, hipEvent_t>> g_scan_ev;
 
 struct TopkPlan {
   int dtype, v2, Dp, tpc, nchunks, ncand, unc_cap;
+  int ncand_alloc;  // candidate slots the workspace holds per query (>= ncand)
   size_t off[20];
   size_t total;
 };
@@ -1777,6 +1778,15 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   const long long maxch = 60000 / (KT * 12);          // knn_merge's shared memory
   if ((tiles + tpc - 1) / tpc > maxch) tpc = (tiles + maxch - 1) / maxch;
   static const bool balance = [] { const char* e = getenv("ARTSBIR_KNN_BALANCE"); return !e || atoi(e) != 0; }();
+  // the workspace is laid out for the most chunks the balancing below may pick,
+  // whatever the device it finds (or none, as in a host-side workspace query):
+  // the layout depends on the arguments alone
+  long long nch_alloc = (tiles + tpc - 1) / tpc;
+  if (tpc_req <= 0 && p.v2) {
+    const long long tmin = (tpc * 3 + 3) / 4 > 0 ? (tpc * 3 + 3) / 4 : 1;
+    const long long nmax = (tiles + tmin - 1) / tmin;
+    nch_alloc = std::max(nch_alloc, std::min(nmax, maxch));
+  }
   if (tpc_req <= 0 && p.v2 && Q > 0 && balance) {
     // the v2 scan runs ceil(Q / 256) query tiles x nchunks workgroups, one per CU
     // (140 KB of LDS): take the chunk length (at most 1/4 shorter) whose grid
@@ -1800,6 +1810,7 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   p.tpc = (int)tpc;
   p.nchunks = (int)((tiles + tpc - 1) / tpc);
   p.ncand = p.nchunks * KT;
+  p.ncand_alloc = (int)std::max<long long>(p.nchunks, nch_alloc) * KT;
   p.unc_cap = g_topk_unc_cap;
   const size_t es = dtype == ARTSBIR_DT_BF16 ? 2 : 4;
   const size_t W = KNN_XB * 4;
@@ -1814,7 +1825,7 @@ int topk_plan(int dtype, int Q, long long N, int D, int k, int tpc_req, TopkPlan
   sz[W_DPOS] = 8 * (size_t)Q;
   sz[W_CNT] = 4 * (size_t)Q;
   sz[W_UNC] = 4 * (2 * (size_t)p.unc_cap + 1);
-  sz[W_CD] = sz[W_CI] = 4 * (size_t)Q * p.ncand;
+  sz[W_CD] = sz[W_CI] = 4 * (size_t)Q * p.ncand_alloc;
   sz[W_FLAG] = 4 * (size_t)Q;
   sz[W_PK] = sz[W_PI] = 8 * (size_t)Q * W * k;
   sz[W_KB] = 4 * (size_t)Q;
