@@ -528,7 +528,7 @@ def cpu_embed_baseline(batch=48, reps=2):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=384, help="triplets per GPU per step")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
