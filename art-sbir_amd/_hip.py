@@ -230,6 +230,11 @@ class HipError(RuntimeError):
 # current stream and (kernel, flops, bytes, start, end, tag, stream) is appended.
 PROFILE = None
 HOST_TS = None  # list: host time of every profiled launch (diagnostics)
+# Optional call trace (tests): when TRACE is a list, every successful call appends
+# (entry point, kernel, tag) — kernel is the variant the library launched for a
+# kernel="auto" call (artsbir_last_kernel), the declared name otherwise — so a
+# test can assert which kernels a whole forward / backward actually ran
+TRACE = None
 
 
 def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes: float = 0.0,
@@ -252,6 +257,11 @@ def call(name: str, *args, kernel: str | None = None, flops: float = 0.0, nbytes
     if rc != 0:
         msg = lib().artsbir_last_error().decode(errors="replace")
         raise HipError(f"{name} failed ({rc}): {msg}")
+    tr = TRACE
+    if tr is not None:
+        if kernel == "auto":
+            kernel = lib().artsbir_last_kernel().decode()
+        tr.append((name, kernel, tag))
 
 
 def ptr(t) -> int | None:

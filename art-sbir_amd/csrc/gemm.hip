@@ -1091,8 +1091,9 @@ __global__ void __launch_bounds__(256) fold_concat_kernel(const T* __restrict__ 
   }
 }
 
-static void* g_fold_ws = nullptr;  // the concatenated operand of the fallback path
-static size_t g_fold_ws_n = 0;
+static int fold_concat_gemms(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                             const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                             long long param_stride, const ConvArgs& a, void* ws, hipStream_t st);
 
 // the segment s slice of a fused BN-backward descriptor (kind 1: the BN before the ReLU)
 static artsbir_bn_bwd_desc bnb_segment(const artsbir_bn_bwd_desc* bd, int s, long long seg_m, int C, long long pstride) {
@@ -1160,7 +1161,10 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
   if (bf) {
     int rc = launch_conv<bf16>(a, st);
     if (rc <= 0) return rc;
-    for (int s = 0; s < nseg && rc == 0; ++s) {
+    // no kernel took the whole batch (a tile would straddle two segments): one
+    // launch per segment; segment 0 decides, a refusal there drops to the
+    // concatenated form below (every segment has the same shape)
+    for (int s = 0; s < nseg; ++s) {
       ConvArgs p = a;
       artsbir_bn_bwd_desc bs;
       if (bnb) { bs = bnb_segment(bnb, s, seg_m, Ci, param_stride); p.bnb_desc = &bs; }
@@ -1172,29 +1176,45 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
       p.y = reinterpret_cast<bf16*>(dx) + s * seg_m * Ci;
       rc = launch_conv<bf16>(p, st);
       if (rc < 0) return rc;
-      if (rc > 0 && s > 0) { set_error("conv1x1_dgrad_fold: segment %d has no kernel", s); return -1; }
+      if (rc > 0) {
+        if (s > 0) { set_error("conv1x1_dgrad_fold: segment %d has no kernel", s); return -1; }
+        break;
+      }
     }
     if (rc == 0) return 0;
   }
   // f32 (the parity mode) and shapes the pipelined kernels do not take: the two
-  // operands concatenated per pixel, then one plain GEMM per segment
+  // operands concatenated per pixel, then one plain GEMM per segment.  The
+  // concatenated operand is stream-ordered scratch (hipMallocAsync / hipFreeAsync
+  // on the caller's stream): no process-wide buffer shared across devices or
+  // threads, no device-synchronous hipFree in the middle of a step
   const size_t need = (size_t)(M * K * es);
-  if (need > g_fold_ws_n) {
-    if (g_fold_ws) (void)hipFree(g_fold_ws);
-    g_fold_ws = nullptr;
-    g_fold_ws_n = 0;
-    if (hipMalloc(&g_fold_ws, need) != hipSuccess) { set_error("conv1x1_dgrad_fold: workspace of %zu bytes", need); return -1; }
-    g_fold_ws_n = need;
+  void* ws = nullptr;
+  if (hipMallocAsync(&ws, need, st) != hipSuccess) {
+    set_error("conv1x1_dgrad_fold: workspace of %zu bytes", need);
+    return -1;
   }
+  const int rc = fold_concat_gemms(d, g, x, w, bias, dx, bnb, nseg, param_stride, a, ws, st);
+  (void)hipFreeAsync(ws, st);
+  return rc;
+}
+
+static int fold_concat_gemms(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                             const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                             long long param_stride, const ConvArgs& a, void* ws, hipStream_t st) {
+  const int Co = d->Cout, Ci = d->C, K = Co + Ci;
+  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
+  const bool bf = d->dtype == ARTSBIR_DT_BF16;
+  const long long es = bf ? 2 : 4;
   {
     const long long n = M * (K * es / 16);
     const unsigned grid = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
     if (bf)
       hipLaunchKernelGGL(fold_concat_kernel<bf16>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const bf16*>(g),
-                         reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(g_fold_ws), M, Co, Ci);
+                         reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(ws), M, Co, Ci);
     else
       hipLaunchKernelGGL(fold_concat_kernel<float>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(g),
-                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(g_fold_ws), M, Co, Ci);
+                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(ws), M, Co, Ci);
     ARTSBIR_CHECK_LAUNCH("fold_concat");
   }
   for (int s = 0; s < nseg; ++s) {
@@ -1203,7 +1223,7 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
     if (bnb) { bs = bnb_segment(bnb, s, seg_m, Ci, param_stride); p.bnb_desc = &bs; }
     p.x2 = nullptr; p.C1 = 0; p.w_sstride = 0; p.bias_sstride = 0;
     p.nseg = 1; p.M = seg_m;
-    p.x = reinterpret_cast<const char*>(g_fold_ws) + s * seg_m * K * es; p.x_elems = seg_m * K;
+    p.x = reinterpret_cast<const char*>(ws) + s * seg_m * K * es; p.x_elems = seg_m * K;
     p.sW = K; p.sH = (long long)d->W * K; p.sN = (long long)d->H * d->W * K;
     p.w = reinterpret_cast<const char*>(w) + s * a.w_sstride * es;
     p.bias = bias + s * Ci;

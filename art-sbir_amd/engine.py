@@ -595,8 +595,12 @@ class Engine:
 
     def _fold_on(self):
         """whether the backward folds the block-output BN through conv3 / the
-        downsample conv (it needs the column sums of their inputs from the forward)"""
-        return FOLD_BN[0] and _fuse_bnb() and type(self) is Engine
+        downsample conv (it needs the column sums of their inputs from the
+        forward).  Every block folds, in every mode: where the block-output BN
+        reduction is not fused into the next block's data gradient (the
+        encoder's last block; the deterministic mode, which reduces in a fixed
+        order) a reduce-only pass supplies g and the reduction (_bn_reduce_g)"""
+        return FOLD_BN[0] and type(self) is Engine
 
     def _block_fwd(self, blk, bp, h, train, stats, fold=False, h_cs=None):
         B, H, W, Cin = h.shape
@@ -816,6 +820,28 @@ class Engine:
                                                                  + (1 if gout is not None else 0))),
              tag=f"bn_bwd_apply k{kind} {B}x{H}x{W}x{C} t{len(targets)}")
         return dys
+
+    def _bn_reduce_g(self, d, targets, ws, mask):
+        """the reduce half of _bn_bwd for the block output (kind 0): g = d * relu
+        mask is written and Σg, Σg·x̂ of every target and segment go to the slots
+        (fixed-order f64 in the deterministic mode), no apply pass — the BN
+        backward is then folded through the 1x1 convs.  Returns (g, fused) in
+        the form of a fused data gradient's hand-over (_bnb_fused_desc)."""
+        y0 = targets[0][0]
+        B, H, W, C = y0.shape
+        G = self._G
+        g = torch.empty_like(d)
+        slots = [ws.take(C * G) for _ in targets]
+        desc = self._seg_desc(0, 0, targets, B // G, H, W, C)
+        desc.d = ptr(d)
+        desc.mask = ptr(mask)
+        desc.gout = ptr(g)
+        for i in range(len(targets)):
+            desc.slots[i] = ptr(slots[i])
+        call("artsbir_bn_bwd_reduce", desc, _s(), kernel="bn_bwd_reduce_kernel<0>",
+             nbytes=float(y0.element_size() * B * H * W * C * (3 + len(targets))),
+             tag=f"bn_bwd_reduce k0 {B}x{H}x{W}x{C} t{len(targets)} +g")
+        return g, (None, slots, targets)
 
     def _bn_coefs(self, targets, bnmods, slots, grads, count):
         """parameter gradients (+=) and apply coefficients [G][3][C] of every
@@ -1100,6 +1126,12 @@ class Engine:
         # (csrc/fold.hip): no dy3 / dyd tensors, their apply pass and re-reads gone
         fold = fused_res is not None and FOLD_BN[0]
         dys = coefs = None
+        if fused_res is None and self._fold_on():
+            # no data gradient reduced this BN for us (the last block; the
+            # deterministic mode): a reduce-only pass, then the same fold
+            targets = [(y3, b3)] + ([(yd, bd)] if has_ds else [])
+            dout, fused_res = self._bn_reduce_g(dout, targets, ws, out)
+            fold = True
         if fold:
             _, slots, targets = fused_res
             B3, H3, W3, _ = y3.shape
@@ -1120,15 +1152,15 @@ class Engine:
             wargs = (blk.conv3, bp["conv3"][0], coefs[0], b3, grads, c.get("cs2"))
             if not wg3:
                 self._wgrad_fold(dout, p2, *wargs)
-            f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2) if s == 1 else None
+            f2 = self._bnb_fused_desc(1, [(y2, b2)], ws, mask_bn=b2) if s == 1 and _fuse_bnb() else None
             if wg3:
                 g2 = self._dgrad_fold_wg(dout, p2, fw3, *wargs, fused=f2)
             else:
                 g2 = self._dgrad_fold(dout, p2, fw3, blk.conv3, fused=f2)
-            if s == 1:
+            if f2 is not None:
                 dy2, = self._bn_finish(g2, f2, [blk.bn2], grads)
             else:
-                dy2, = self._bn_bwd(1, g2, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s)
+                dy2, = self._bn_bwd(1, g2, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
         else:
             dy3 = dys[0]
             held = self._wgrad_pre(dy3, c3in, blk.conv3, 1, 0, grads)

@@ -525,9 +525,54 @@ def cpu_embed_baseline(batch=48, reps=2):
                                           f"{reps}, ModifiedResNet((3,4,6,3),512) fp32 224^2"}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(n: int, argv, port: int):
+    """the command that runs this benchmark as n ranks, one process per GPU
+    (torch.distributed.run on 127.0.0.1: RANK / LOCAL_RANK / WORLD_SIZE in each
+    child's environment, so the children do not launch again)"""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` outside a launcher: start the N ranks as child
+    processes and return their exit status.  Nothing in this process has
+    touched the GPU (no HIP call, no torch.cuda query), and it never execs —
+    it waits for the children and passes their status on."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_command(n, argv, free_port()), env=env)
+
+
+def launch_check(world, rank):
+    """--launch-check: the rank protocol alone (no GPU work): every rank joins the
+    process group, the ranks agree on the world size by an all-reduce, rank 0
+    prints one JSON line — tests/test_bench_launch.py runs it on the CPU (gloo)"""
+    import ddp
+    ddp.init_distributed()
+    t = torch.ones(1)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"n_gpus": dist.get_world_size(), "world_size": dist.get_world_size(),
+                          "all_reduce": float(t.item()), "backend": dist.get_backend()}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE, else 1); without a launcher's WORLD_SIZE, "
+                         "N > 1 starts the N ranks itself under torch.distributed.run")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=384, help="triplets per GPU per step")
@@ -553,6 +598,16 @@ def main():
                     help="write the autotuner's choices after every leg has run (shapes of all legs)")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world or 1)
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} under a launcher of {env_world} ranks")
+    if args.launch_check:
+        return launch_check(int(env_world or 1), int(os.environ.get("RANK", "0")))
+
     import _hip
     import ddp
     import losses
@@ -562,10 +617,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
     if world > 1:
         # RCCL ("nccl") over xGMI, one GPU per rank; ARTSBIR_DIST_BACKEND=gloo lets
         # several ranks share one device (a rehearsal of the N > 1 code path)
         ddp.init_distributed()
+        backend = dist.get_backend()
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group of {dist.get_world_size()} ranks for --gpus {args.gpus}")
     dev = torch.device("cuda", torch.cuda.current_device())
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 
@@ -683,7 +742,8 @@ def main():
         step_flops = train_flops_per_triplet() * B
         line = {
             "metric": "triplet-images/sec embedded @224² bf16, 1→8 GPU; gallery kNN QPS @1M×512",
-            "value": round(value, 2), "unit": "triplet-images/s", "n_gpus": world, "steps": args.steps,
+            "value": round(value, 2), "unit": "triplet-images/s", "n_gpus": world, "world_size": world,
+            "backend": backend, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
             "config": {"workload": "triplet training step (train.py:59-70): 3x encoder fwd + TripletMarginLoss "

@@ -12,6 +12,15 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "art-sbir_amd", "build_asan", "capi_asan")
+# written by __graft_entry__.build() when `make asan` fails (removed when it succeeds)
+FAILED = os.path.join(ROOT, "art-sbir_amd", "build_asan", "BUILD_FAILED")
+
+
+def test_asan_build_did_not_fail():
+    """a failed sanitizer build must not pass as a skip"""
+    if os.path.exists(FAILED):
+        with open(FAILED) as f:
+            pytest.fail("the AddressSanitizer build failed:\n" + f.read()[-3000:])
 
 
 @pytest.mark.skipif(not os.path.exists(EXE), reason="ASan build absent: make -C art-sbir_amd asan")

@@ -1,7 +1,7 @@
 """The drop-in boundary without a GPU: the C-ABI library loads and exports every
 entry point include/artsbir.h declares, rejects bad shapes with a status and a
 message, and the Python mirror of models.py has the reference's constructor
-signatures, parameter names and counts (models.py:93-151 of the reference)."""
+signatures, parameter names and counts (models.py:191-379 of the reference)."""
 import ctypes
 import os
 import re

@@ -147,6 +147,25 @@ def test_c2_f32_step_matches_oracle(oracle_c2, dev):
     check_f32_step(oracle_c2, dev, "C2")
 
 
+FOLD_ENTRIES = ("artsbir_conv1x1_dgrad_fold", "artsbir_conv1x1_dgrad_fold_wg")
+
+
+def assert_folded(m, trace):
+    """one folded data gradient and one weight-gradient combine per conv3 and
+    per downsample conv of every Bottleneck, and no apply pass of a
+    block-output BatchNorm (kind 0 / the residual targets) left in the trace
+    (_hip.TRACE entries: entry point, kernel, tag); returns the fold calls"""
+    blocks = list(m.blocks())
+    want = len(blocks) + sum(1 for b in blocks if b.downsample is not None)
+    folds = [t for t in trace if t[0] in FOLD_ENTRIES]
+    combines = [t for t in trace if t[0] == "artsbir_bn_fold_wgrad_combine"]
+    assert len(folds) == want, (len(folds), want)
+    assert len(combines) == want, (len(combines), want)
+    applies = [t for t in trace if t[0] == "artsbir_bn_bwd_apply"]
+    assert not [t for t in applies if (t[2] or "").startswith("bn_bwd_apply k0") or " t2" in (t[2] or "")], applies
+    return folds
+
+
 def check_f32_step(oracle, dev, tag):
     """f32 mode, deterministic.  Unconditioned: embeddings within 1e-3 of the
     float64 oracle, loss and the whole gradient vector (relative L2) as accurate
@@ -156,15 +175,23 @@ def check_f32_step(oracle, dev, tag):
     ReLU decisions): every parameter's gradient within max(2e-4, 4x the float32
     oracle's error) of the float64 one, relative to its largest entry — no
     outliers; the HIP and float64 ReLU decisions differ only at |x| < 1e-5 max|x|."""
+    import _hip
     import engine
     elements, cfg = oracle["elements"], oracle["cfg"]
     old = engine.set_deterministic(True)
+    trace = []
     try:
         m = _mine(dev, torch.float32, cfg=cfg)
         masks = hip_relu_masks(m, elements, dev)
+        _hip.TRACE = trace
         loss, embs, grads = _step(m, elements, dev)
     finally:
+        _hip.TRACE = None
         engine.set_deterministic(old)
+    # the gradients checked below come out of the folded BatchNorm backward
+    # (artsbir_conv1x1_dgrad_fold + artsbir_bn_fold_wgrad_combine) of every
+    # block's conv3 and downsample conv: the arithmetic bench.py times
+    assert_folded(m, trace)
     o64, o32 = oracle["64"], oracle["32"]
     for e, e64 in zip(embs, o64["emb"]):
         assert torch.allclose(e, e64, atol=1e-3, rtol=1e-3), (e - e64).abs().max().item()
@@ -255,6 +282,8 @@ def test_c2_deterministic_forward_is_bit_identical(dev):
 # absolute floors; measured values are printed (-s) and quoted in DESIGN.md §2
 BF16_FACTOR = 1.5
 BF16_EMB_FLOOR, BF16_LOSS_FLOOR, BF16_GRAD_FLOOR = 2e-2, 2e-2, 1e-1
+# per folded weight gradient (conv3 / downsample conv): rel-L2 <= max(floor, factor x autocast's)
+BF16_FOLD_FACTOR, BF16_FOLD_FLOOR = 2.0, 5e-2
 
 
 @pytest.mark.parametrize("deterministic", [False, True], ids=["atomic", "det"])
@@ -263,13 +292,18 @@ def test_c2_bf16_step_accuracy(oracle_c2, dev, deterministic):
 
 
 def check_bf16_step(oracle, dev, deterministic, tag):
+    import _hip
     import engine
     old = engine.set_deterministic(deterministic)
+    trace = []
     try:
         m = _mine(dev, torch.bfloat16, cfg=oracle["cfg"])
+        _hip.TRACE = trace
         loss, embs, grads = _step(m, oracle["elements"], dev)
     finally:
+        _hip.TRACE = None
         engine.set_deterministic(old)
+    assert_folded(m, trace)
     o64, oac = oracle["64"], oracle["ac"]
     g64 = o64["grad"]
     flat64 = torch.cat([g.flatten() for g in g64.values()])
@@ -290,6 +324,19 @@ def check_bf16_step(oracle, dev, deterministic, tag):
     assert l_err < max(BF16_LOSS_FLOOR if deterministic else 5e-2, BF16_FACTOR * a_loss), (l_err, a_loss)
     assert g_err < max(BF16_GRAD_FLOOR, BF16_FACTOR * a_grad), (g_err, a_grad)
     assert g_cos > min(0.95, a_cos - 0.03), (g_cos, a_cos)
+    # the folded weight gradients (conv3 and downsample conv of every block,
+    # c1 g^T x + b' W Gram + k colsum in the kernels) each on their own: relative
+    # L2 against float64 no worse than autocast-bf16's error on that parameter
+    bad, rows = [], []
+    for k in g64:
+        if not (k.endswith("conv3.weight") or k.endswith("downsample.0.weight")):
+            continue
+        e, a = _rel_l2(grads[k], g64[k]), _rel_l2(oac["grad"][k], g64[k])
+        rows.append(f"{k} {e:.3f} ({a:.3f})")
+        if e > max(BF16_FOLD_FLOOR, BF16_FOLD_FACTOR * a):
+            bad.append((k, e, a))
+    print(f"{tag} bf16 folded weight gradients rel-L2 (autocast): " + ", ".join(rows))
+    assert not bad, bad
 
 
 def test_c2_bf16_eval_embedding(dev):
@@ -314,3 +361,82 @@ def test_c2_bf16_eval_embedding(dev):
     err, a_err = _rel_l2(e, e64), _rel_l2(eac, e64)
     print(f"\nC2 bf16 eval embedding vs float64: rel-L2 {err:.3e} (autocast {a_err:.3e})")
     assert err < max(BF16_EMB_FLOOR, BF16_FACTOR * a_err), (err, a_err)
+
+
+def _det_step(dev, dtype, elements, fold, fold_wg=True, cfg=C2, trace=None):
+    """one deterministic-mode step of the damped model with the block-output BN
+    backward folded through the 1x1 convs (fold) or as its own apply pass"""
+    import _hip
+    import engine
+    old = engine.set_deterministic(True)
+    oldf, oldw = engine.FOLD_BN[0], engine.FOLD_WG[0]
+    engine.FOLD_BN[0], engine.FOLD_WG[0] = fold, fold_wg
+    try:
+        m = _mine(dev, dtype, cfg=cfg)
+        _hip.TRACE = trace
+        out = _step(m, elements, dev)
+    finally:
+        _hip.TRACE = None
+        engine.FOLD_BN[0], engine.FOLD_WG[0] = oldf, oldw
+        engine.set_deterministic(old)
+    return m, out
+
+
+def test_c2_bf16_det_fold_matches_unfolded(oracle_c2, dev):
+    """bf16, deterministic mode (identical forward bits and ReLU decisions in
+    both runs): the step with the block-output BatchNorm backward folded through
+    every conv3 / downsample conv (the layer-1 ones on the one-pass dgrad+wgrad
+    kernel pstream_kernel<64,fold,wg>, asserted by name) against the same step
+    with dy formed by the apply pass.  Reference chain: models.py:219-220,
+    226-229 (conv3 -> bn3, downsample conv -> BN).
+
+    Both are scored against the float64 oracle evaluated on the bf16 forward's
+    own ReLU decisions (mask-conditioned, tests/_parity.py): per parameter the
+    folded path's relative L2 error may exceed the apply path's by at most
+    FOLD_BF16_FACTOR (+ FOLD_BF16_SLACK), and the whole gradient vector by 10 %.
+    The two bf16 paths round at different places — the apply path rounds dy
+    per element, the fold rounds its per-segment weights diag(c1) W and
+    W^T diag(b') W once — so they differ from each other by about the bf16
+    forward's own error (a few 1e-2 on the stem, which sits behind 16 blocks);
+    what must hold is that the fold is no less accurate."""
+    elements = oracle_c2["elements"]
+    trace = []
+    m1, (l1, e1, g1) = _det_step(dev, torch.bfloat16, elements, True, trace=trace)
+    _, (l0, e0, g0) = _det_step(dev, torch.bfloat16, elements, False)
+    folds = assert_folded(m1, trace)
+    wg = [t for t in folds if t[0] == "artsbir_conv1x1_dgrad_fold_wg"]
+    # layer 1: three conv3 (Ci 64 -> Co 256) and the stride-1 downsample conv (64 -> 256)
+    assert len(wg) == 4, wg
+    assert all(t[1] == "pstream_kernel<64,fold,wg>" for t in wg), wg
+    for a, b in zip(e1, e0):
+        assert torch.equal(a, b)
+    assert l1 == l0
+    import engine
+    old = engine.set_deterministic(True)
+    try:
+        masks = hip_relu_masks(_mine(dev, torch.bfloat16), elements, dev)
+    finally:
+        engine.set_deterministic(old)
+    c64, _ = _conditioned(DAMP, elements, torch.float64, masks)
+    ref = c64["grad"]
+    floor = 1e-4 * max(g.norm().item() for g in ref.values())
+    bad, worst_diff, rows = [], 0.0, []
+    for k, g in ref.items():
+        den = max(g.norm().item(), floor)
+        ef, eu = (g1[k] - g).norm().item() / den, (g0[k] - g).norm().item() / den
+        worst_diff = max(worst_diff, (g1[k] - g0[k]).norm().item() / den)
+        if k == "conv1.weight" or k.endswith(("conv3.weight", "downsample.0.weight")):
+            rows.append(f"{k} {ef:.2e}/{eu:.2e}")
+        if ef > FOLD_BF16_FACTOR * eu + FOLD_BF16_SLACK:
+            bad.append((k, ef, eu))
+    fl = lambda gr: torch.cat([gr[k].flatten() for k in ref])  # noqa: E731
+    e_all_f, e_all_u = _rel_l2(fl(g1), fl(ref)), _rel_l2(fl(g0), fl(ref))
+    print(f"\nC2 bf16 det vs mask-conditioned float64, fold / apply path: whole vector {e_all_f:.3e} / {e_all_u:.3e}; "
+          f"largest fold-vs-apply difference {worst_diff:.2e}; " + ", ".join(rows[:12]))
+    assert e_all_f <= 1.1 * e_all_u, (e_all_f, e_all_u)
+    assert not bad, bad
+
+
+# per parameter: folded-path error <= factor x apply-path error + slack (relative L2
+# against the mask-conditioned float64 oracle)
+FOLD_BF16_FACTOR, FOLD_BF16_SLACK = 1.5, 2e-3
