@@ -105,6 +105,9 @@ SIGNATURES = {
     "artsbir_conv2d_dgrad_bnb": [_P, _vp, _vp, _vp, _vp, _c_int, _PB, _c_int, _c_ll, _vp],
     "artsbir_conv1x1_dgrad_fold": [_P, _vp, _vp, _vp, _vp, _vp, _PB, _c_int, _c_ll, _vp],
     "artsbir_conv1x1_dgrad_fold_wg": [_P, _vp, _vp, _vp, _vp, _vp, _PB, _c_int, _c_ll, _vp, _vp, _vp],
+    "artsbir_conv1x1_dgrad_fold_y": [_P, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _PB, _c_int, _c_ll, _vp],
+    "artsbir_bn_fold_bwd_prep_y": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp],
+    "artsbir_bn_fold_wgrad_combine_y": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _c_ll, _vp, _vp],
     "artsbir_bn_fold_bwd_prep": [_c_int, _c_int, _c_int, _vp, _vp, _vp, _c_ll, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_bn_fold_wgrad_combine": [_c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_ll, _vp,
                                       _vp, _vp],
@@ -122,6 +125,7 @@ SIGNATURES = {
     "artsbir_act_pool": [_c_int, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp],
     "artsbir_block_out": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp],
     "artsbir_block_out_mask": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp],
+    "artsbir_block_out_colsum": [_c_int, _vp, _vp, _vp, _vp, _vp, _c_ll, _c_int, _c_int, _vp, _vp, _vp, _vp],
     "artsbir_layernorm_fwd": [_c_int, _vp, _vp, _vp, _c_ll, _c_int, ctypes.c_float, _vp, _vp],
     "artsbir_quickgelu": [_c_int, _vp, _c_ll, _vp, _vp],
     "artsbir_mha_fwd": [_c_int, _vp, _c_int, _c_int, _c_int, _vp, _vp, _vp],

@@ -432,16 +432,25 @@ __global__ void block_out_kernel(const T* __restrict__ y3, const float* __restri
 // block_out with each lane owning one 8-channel group (parameters loaded once),
 // segment = blockIdx.y (seg_rows rows each), 2 rows per trip with all loads
 // issued before the stores.  C / 8 <= 256.
-template <typename T>
+// CS: also the column sums of the stored output per segment into one of
+// ARTSBIR_NSLOT replica rows of colsum[s][slot][C] — the 1^T x of the next
+// block's folded conv1 weight gradient (csrc/fold.hip, the y-side fold)
+template <typename T, bool CS = false>
 __global__ void __launch_bounds__(256) block_out_cg_kernel(const T* __restrict__ y3, const float* __restrict__ bn3,
                                                            const T* __restrict__ yd, const float* __restrict__ bnd,
                                                            const T* __restrict__ idn, int seg_rows, int C,
                                                            int rows_per_block, T* __restrict__ out,
-                                                           unsigned char* __restrict__ bits) {
+                                                           unsigned char* __restrict__ bits,
+                                                           float* __restrict__ colsum = nullptr) {
   const int s = blockIdx.y;
   const int CG = C / 8, RL = 256 / CG;
   const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
-  if (rl >= RL) return;
+  float csum[CS ? 8 : 1];
+  if constexpr (CS) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  }
+  if (!CS && rl >= RL) return;
   const long long po = (long long)s * 4 * C;
   float m[8], sc[8], h[8], m2[8], s2[8], h2[8];
   load_bn8(bn3 + po, C, cg * 8, m, sc, h);
@@ -451,7 +460,7 @@ __global__ void __launch_bounds__(256) block_out_cg_kernel(const T* __restrict__
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(r0 + rows_per_block, seg_rows);
   constexpr int UN = 2;
-  for (int rb = r0 + rl; rb < r1; rb += RL * UN) {
+  for (int rb = r0 + rl; rl < RL && rb < r1; rb += RL * UN) {
     float a[UN][8], r[UN][8];
 #pragma unroll
     for (int i = 0; i < UN; ++i) {
@@ -476,6 +485,22 @@ __global__ void __launch_bounds__(256) block_out_cg_kernel(const T* __restrict__
         for (int e = 0; e < 8; ++e) mk |= (to_f(from_f<T>(a[i][e])) > 0.f ? 1u : 0u) << e;
         bits[row * CG + cg] = (unsigned char)mk;
       }
+      if constexpr (CS) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += to_f(from_f<T>(a[i][e]));  // the stored values
+      }
+    }
+  }
+  if constexpr (CS) {  // the RL lanes of each channel group, then one atomic per channel
+    __shared__ float red[256][9];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[threadIdx.x][e] = rl < RL ? csum[e] : 0.f;
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      const int g = c >> 3, e = c & 7;
+      float t = 0.f;
+      for (int r = 0; r < RL; ++r) t += red[r * CG + g][e];
+      atomicAdd(colsum + ((long long)s * ARTSBIR_NSLOT + blockIdx.x % ARTSBIR_NSLOT) * C + c, t);
     }
   }
 }
@@ -1200,9 +1225,9 @@ extern "C" int artsbir_act_pool(int dtype, const void* x, const float* bn, int r
   return artsbir_act_pool_colsum(dtype, x, bn, relu, pool, B, H, W, C, nseg, out, nullptr, stream);
 }
 
-extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
-                                      const void* identity, long long rows, int C, int nseg, void* out,
-                                      unsigned char* mask_bits, void* stream) {
+extern "C" int artsbir_block_out_colsum(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                                        const void* identity, long long rows, int C, int nseg, void* out,
+                                        unsigned char* mask_bits, float* colsum, void* stream) {
   if (C % 8) { set_error("block_out: C %% 8 != 0"); return -1; }
   if (nseg < 1 || rows % nseg) { set_error("block_out: %d segments do not split %lld rows", nseg, rows); return -1; }
   if (!yd && !identity) { set_error("block_out: need downsample or identity input"); return -1; }
@@ -1212,9 +1237,14 @@ extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn
   if (C / 8 <= 256 && seg_rows < 0x7fffffffLL) {
     const int rpb = cg_units_per_block(seg_rows, nseg, C);
     const dim3 g((unsigned)((seg_rows + rpb - 1) / rpb), (unsigned)nseg);
-    DISPATCH_T(dtype, hipLaunchKernelGGL(block_out_cg_kernel<T>, g, dim3(256), 0, (hipStream_t)stream, (const T*)y3, bn3,
-                                         (const T*)yd, bnd, (const T*)identity, (int)seg_rows, C, rpb, (T*)out,
-                                         mask_bits));
+    if (colsum)
+      DISPATCH_T(dtype, hipLaunchKernelGGL((block_out_cg_kernel<T, true>), g, dim3(256), 0, (hipStream_t)stream,
+                                           (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, (int)seg_rows, C,
+                                           rpb, (T*)out, mask_bits, colsum));
+    else
+      DISPATCH_T(dtype, hipLaunchKernelGGL((block_out_cg_kernel<T, false>), g, dim3(256), 0, (hipStream_t)stream,
+                                           (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, (int)seg_rows, C,
+                                           rpb, (T*)out, mask_bits, nullptr));
     ARTSBIR_CHECK_LAUNCH("block_out");
     return 0;
   }
@@ -1222,7 +1252,20 @@ extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn
                                        (const T*)y3, bn3, (const T*)yd, bnd, (const T*)identity, rows, C, nseg,
                                        (T*)out, mask_bits));
   ARTSBIR_CHECK_LAUNCH("block_out");
+  if (colsum) {  // the generic kernel's shapes: a column-sum pass per segment into replica row 0
+    const long long es = dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+    for (int s = 0; s < nseg; ++s)
+      if (artsbir_colsum(dtype, reinterpret_cast<const char*>(out) + s * seg_rows * C * es, seg_rows, C, C,
+                         colsum + (long long)s * ARTSBIR_NSLOT * C, stream))
+        return -1;
+  }
   return 0;
+}
+
+extern "C" int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                                      const void* identity, long long rows, int C, int nseg, void* out,
+                                      unsigned char* mask_bits, void* stream) {
+  return artsbir_block_out_colsum(dtype, y3, bn3, yd, bnd, identity, rows, C, nseg, out, mask_bits, nullptr, stream);
 }
 
 extern "C" int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,

@@ -55,13 +55,51 @@ __global__ void __launch_bounds__(256) fold_prep_kernel(const T* __restrict__ wt
   if (threadIdx.x == 0) bias[(long long)s * Ci + ci] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// The y-side fold (artsbir_bn_fold_bwd_prep_y): the BatchNorm right after the
+// conv is folded with its own input y (the conv output, kept for the BN backward)
+// instead of the conv input x — dy = c1 g + b' y + k, so
+//   dx = g (diag(c1) W) + y (diag(b') W) + k W
+// needs no Gram-side GEMM: row ci of segment s is wout[s][ci][co] = c1 W^T[ci][co],
+// wout[s][ci][Co + co] = b' W^T[ci][co], bias[s][ci] = sum_co W^T[ci][co] k[co]
+template <typename T>
+__global__ void __launch_bounds__(256) fold_prep_y_kernel(const T* __restrict__ wt, int Co, int Ci,
+                                                          const float* __restrict__ coef, const float* __restrict__ prm,
+                                                          long long pstride, T* __restrict__ wout,
+                                                          float* __restrict__ bias) {
+  const int ci = blockIdx.x, s = blockIdx.y;
+  const float* c1 = coef + (long long)s * 3 * Co;
+  const float* c2 = c1 + Co;
+  const float* c3 = c2 + Co;
+  const float* mean = prm + s * pstride;
+  const float* istd = mean + Co;
+  const T* wr = wt + (long long)ci * Co;
+  T* bo = wout + ((long long)s * Ci + ci) * (2 * Co);
+  float acc = 0.f;
+  for (int c = threadIdx.x; c < Co; c += 256) {
+    const float w = to_f(wr[c]);
+    const float a1 = c1[c], is = istd[c];
+    const float bp = -a1 * c3[c] * is;
+    const float k = -a1 * (c2[c] - c3[c] * is * mean[c]);
+    bo[c] = from_f<T>(a1 * w);
+    bo[Co + c] = from_f<T>(bp * w);
+    acc += w * k;
+  }
+  __shared__ float red[4];
+  acc = warp_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) bias[(long long)s * Ci + ci] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // dW[co][ci] += sum_s c1_s[co] P_s[co][ci] + b'_s[co] T[co][s Ci + ci] + k_s[co] cs_s[ci]
-// with T = W [Gram_0 | Gram_1 | ...] (an f32 GEMM before it): elementwise, 4
-// values of one dW row per thread
+// with T = W [Gram_0 | Gram_1 | ...] (an f32 GEMM before it) — or, for the y-side
+// fold, T_s = y_s^T x_s straight from artsbir_gemm_tn2 (t_co / t_s: the strides of
+// T's rows and segments): elementwise, 4 values of one dW row per thread
 __global__ void __launch_bounds__(256) fold_wgrad_combine_kernel(const float* __restrict__ P,
-                                                                 const float* __restrict__ T,
-                                                                 const float* __restrict__ cs, int cs_slots, int Co,
-                                                                 int Ci, int nseg, const float* __restrict__ coef,
+                                                                 const float* __restrict__ T, long long t_co,
+                                                                 long long t_s, const float* __restrict__ cs,
+                                                                 int cs_slots, int Co, int Ci, int nseg,
+                                                                 const float* __restrict__ coef,
                                                                  const float* __restrict__ prm, long long pstride,
                                                                  float* __restrict__ dw) {
   const int cq = Ci / 4;
@@ -75,7 +113,7 @@ __global__ void __launch_bounds__(256) fold_wgrad_combine_kernel(const float* __
     const float c1 = c[co], c2 = c[Co + co], c3 = c[2 * Co + co], mean = mp[co], istd = mp[Co + co];
     const float bp = -c1 * c3 * istd, k = -c1 * (c2 - c3 * istd * mean);
     const float4 p = *reinterpret_cast<const float4*>(P + ((long long)s * Co + co) * Ci + ci);
-    const float4 t = *reinterpret_cast<const float4*>(T + (long long)co * nseg * Ci + (long long)s * Ci + ci);
+    const float4 t = *reinterpret_cast<const float4*>(T + co * t_co + s * t_s + ci);
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);  // the column sums' replica rows of segment s
     for (int r = 0; r < cs_slots; ++r) {
       const float4 v = *reinterpret_cast<const float4*>(cs + ((long long)s * cs_slots + r) * Ci + ci);
@@ -267,8 +305,42 @@ extern "C" int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg
     return -1;
   }
   const long long n = (long long)Co * (Ci / 4);
-  hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, T, colsums,
-                     cs_slots < 1 ? 1 : cs_slots, Co, Ci, nseg, coef, prm, pstride, dw);
+  hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, T,
+                     (long long)nseg * Ci, (long long)Ci, colsums, cs_slots < 1 ? 1 : cs_slots, Co, Ci, nseg, coef, prm,
+                     pstride, dw);
   ARTSBIR_CHECK_LAUNCH("fold_wgrad_combine");
+  return 0;
+}
+
+extern "C" int artsbir_bn_fold_bwd_prep_y(int dtype, int Co, int Ci, const void* wt, const float* coef,
+                                          const float* prm, long long pstride, int nseg, void* wout, float* bias,
+                                          void* stream) {
+  if (Co <= 0 || Ci <= 0 || Co % 8 || Ci % 8 || nseg < 1) {
+    set_error("bn_fold_bwd_prep_y: bad shape Co=%d Ci=%d nseg=%d", Co, Ci, nseg);
+    return -1;
+  }
+  if (!wt || !coef || !prm || !wout || !bias) { set_error("bn_fold_bwd_prep_y: null operand"); return -1; }
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((unsigned)Ci, (unsigned)nseg);
+  if (dtype == ARTSBIR_DT_BF16)
+    hipLaunchKernelGGL(fold_prep_y_kernel<bf16>, g, dim3(256), 0, st, reinterpret_cast<const bf16*>(wt), Co, Ci, coef,
+                       prm, pstride, reinterpret_cast<bf16*>(wout), bias);
+  else
+    hipLaunchKernelGGL(fold_prep_y_kernel<float>, g, dim3(256), 0, st, reinterpret_cast<const float*>(wt), Co, Ci,
+                       coef, prm, pstride, reinterpret_cast<float*>(wout), bias);
+  ARTSBIR_CHECK_LAUNCH("fold_prep_y");
+  return 0;
+}
+
+extern "C" int artsbir_bn_fold_wgrad_combine_y(int Co, int Ci, int nseg, const float* P, const float* Q,
+                                               const float* colsums, int cs_slots, const float* coef,
+                                               const float* prm, long long pstride, float* dw, void* stream) {
+  if (Co <= 0 || Ci <= 0 || Co % 8 || Ci % 8 || nseg < 1) { set_error("bn_fold_wgrad_combine_y: bad shape"); return -1; }
+  if (!P || !Q || !colsums || !coef || !prm || !dw) { set_error("bn_fold_wgrad_combine_y: null operand"); return -1; }
+  const long long n = (long long)Co * (Ci / 4);
+  hipLaunchKernelGGL(fold_wgrad_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     P, Q, (long long)Ci, (long long)Co * Ci, colsums, cs_slots < 1 ? 1 : cs_slots, Co, Ci, nseg, coef,
+                     prm, pstride, dw);
+  ARTSBIR_CHECK_LAUNCH("fold_wgrad_combine_y");
   return 0;
 }

@@ -1078,29 +1078,50 @@ static int dgrad_common(const artsbir_conv_desc* d, const void* dy, const void* 
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ void __launch_bounds__(256) fold_concat_kernel(const T* __restrict__ g, const T* __restrict__ x, T* out,
-                                                          long long M, int Co, int Ci) {
+                                                          long long M, int Co, int C2) {
   constexpr int EPC = 16 / sizeof(T);
-  const int cg = (Co + Ci) / EPC;  // 16-B chunks per output row
+  const int cg = (Co + C2) / EPC;  // 16-B chunks per output row
   const long long n = M * cg;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const long long m = i / cg;
     const int c = (int)(i - m * cg) * EPC;
     const uint4 v = c < Co ? *reinterpret_cast<const uint4*>(g + m * Co + c)
-                           : *reinterpret_cast<const uint4*>(x + m * Ci + (c - Co));
-    *reinterpret_cast<uint4*>(out + m * (Co + Ci) + c) = v;
+                           : *reinterpret_cast<const uint4*>(x + m * C2 + (c - Co));
+    *reinterpret_cast<uint4*>(out + m * (Co + C2) + c) = v;
   }
 }
 
-static int fold_concat_gemms(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
-                             const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
-                             long long param_stride, const ConvArgs& a, void* ws, hipStream_t st);
+// One fold launch: dx [N][H][W][Ci] = [g | x2] w_s^T + bias_s (+ residual) for
+// the pixels of BN segment s, g with Co channels, x2 with C2 (the conv input x,
+// C2 = Ci: artsbir_conv1x1_dgrad_fold; the BN input y, C2 = Co:
+// artsbir_conv1x1_dgrad_fold_y), an optional fused BN-backward reduction of the
+// gradient it produces
+struct FoldOp {
+  const artsbir_conv_desc* d;
+  const void* g;
+  const void* x2;
+  int C2;
+  const void* w;
+  const float* bias;
+  void* dx;
+  const void* res;
+  int res_mode;
+  const artsbir_bn_bwd_desc* bnb;
+  int nseg;
+  long long pstride;
+};
 
-// the segment s slice of a fused BN-backward descriptor (kind 1: the BN before the ReLU)
+static int fold_concat_gemms(const FoldOp& f, const ConvArgs& a, void* ws, hipStream_t st);
+
+// the segment s slice of a fused BN-backward descriptor (its tensors, mask and
+// BN parameters advanced by whole segments)
 static artsbir_bn_bwd_desc bnb_segment(const artsbir_bn_bwd_desc* bd, int s, long long seg_m, int C, long long pstride) {
   artsbir_bn_bwd_desc d = *bd;
   const long long es = bd->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
   d.nseg = 1;
   if (bd->mask_bn) d.mask_bn = bd->mask_bn + s * pstride;
+  if (bd->mask)  // kind 3: one mask byte per 8 channels; kind 0: the block output
+    d.mask = reinterpret_cast<const char*>(bd->mask) + (bd->kind == 3 ? s * seg_m * (C / 8) : s * seg_m * C * es);
   for (int t = 0; t < bd->ntarget; ++t) {
     d.y[t] = reinterpret_cast<const char*>(bd->y[t]) + s * seg_m * C * es;
     d.mean[t] = bd->mean[t] + s * pstride;
@@ -1110,52 +1131,83 @@ static artsbir_bn_bwd_desc bnb_segment(const artsbir_bn_bwd_desc* bd, int s, lon
   return d;
 }
 
-static int fold_check(const artsbir_conv_desc* d, const void* g, const void* x, const void* w, const float* bias,
-                      void* dx, const artsbir_bn_bwd_desc* bnb, int nseg) {
+static int fold_check(const FoldOp& f) {
+  const artsbir_conv_desc* d = f.d;
   if (check_conv(d)) return -1;
   if (d->R != 1 || d->S != 1 || d->stride != 1 || d->pad != 0) { set_error("conv1x1_dgrad_fold: 1x1 stride-1 convolutions only"); return -1; }
-  if (!g || !x || !w || !bias || !dx) { set_error("conv1x1_dgrad_fold: null operand"); return -1; }
-  if (d->Cout % 8 || d->C % 8) { set_error("conv1x1_dgrad_fold: channels must be multiples of 8"); return -1; }
-  if (nseg < 1 || d->N % nseg) { set_error("conv1x1_dgrad_fold: %d segments do not divide batch %d", nseg, d->N); return -1; }
-  if (bnb && (bnb->kind != 1 || bnb->ntarget != 1 || !bnb->mask_bn || bnb->pool > 1 || bnb->dtype != d->dtype)) {
-    set_error("conv1x1_dgrad_fold: the fused BN backward must be kind 1 with one target");
-    return -1;
+  if (!f.g || !f.x2 || !f.w || !f.bias || !f.dx) { set_error("conv1x1_dgrad_fold: null operand"); return -1; }
+  if (d->Cout % 8 || d->C % 8 || f.C2 % 8 || f.C2 <= 0) { set_error("conv1x1_dgrad_fold: channels must be multiples of 8"); return -1; }
+  if (f.nseg < 1 || d->N % f.nseg) { set_error("conv1x1_dgrad_fold: %d segments do not divide batch %d", f.nseg, d->N); return -1; }
+  if (f.res_mode < 0 || f.res_mode > 2 || (f.res_mode && !f.res)) { set_error("conv1x1_dgrad_fold: bad residual"); return -1; }
+  if (f.res_mode == 2 && (d->H % 2 || d->W % 2)) { set_error("conv1x1_dgrad_fold: unpool residual needs even H, W"); return -1; }
+  if (f.res_mode == 2 && (d->N / f.nseg) * d->H * d->W % 4) { set_error("conv1x1_dgrad_fold: unpool residual segments"); return -1; }
+  if (const artsbir_bn_bwd_desc* b = f.bnb) {
+    if (b->dtype != d->dtype || b->pool > 1) { set_error("conv1x1_dgrad_fold: bad fused BN backward"); return -1; }
+    if (b->kind == 1) {
+      if (b->ntarget != 1 || !b->mask_bn || f.res_mode) {
+        set_error("conv1x1_dgrad_fold: a kind-1 fused BN backward takes one target and no residual");
+        return -1;
+      }
+    } else if (b->kind == 0 || b->kind == 3) {
+      if (b->ntarget < 1 || b->ntarget > 2 || !b->mask || !f.res_mode) {
+        set_error("conv1x1_dgrad_fold: a kind-0/3 fused BN backward takes 1-2 targets, a mask and a residual");
+        return -1;
+      }
+      if (b->kind == 3 && (d->dtype != ARTSBIR_DT_BF16 || d->C % 8)) { set_error("conv1x1_dgrad_fold: bit masks need bf16"); return -1; }
+    } else {
+      set_error("conv1x1_dgrad_fold: fused BN-backward kind %d", b->kind);
+      return -1;
+    }
   }
   return 0;
 }
 
 // the two-operand / per-segment-weight launch arguments of the fold
-static ConvArgs fold_conv_args(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
-                               const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
-                               long long param_stride) {
-  const int Co = d->Cout, Ci = d->C, K = Co + Ci;
+static ConvArgs fold_conv_args(const FoldOp& f) {
+  const artsbir_conv_desc* d = f.d;
+  const int Co = d->Cout, Ci = d->C, K = Co + f.C2;
   const long long M = (long long)d->N * d->H * d->W;
   ConvArgs a;
-  a.x = g; a.sW = Co; a.sH = (long long)d->W * Co; a.sN = (long long)d->H * d->W * Co; a.x_elems = M * Co;
-  a.x2 = x; a.sW2 = Ci; a.sH2 = (long long)d->W * Ci; a.sN2 = (long long)d->H * d->W * Ci; a.x2_elems = M * Ci;
+  a.x = f.g; a.sW = Co; a.sH = (long long)d->W * Co; a.sN = (long long)d->H * d->W * Co; a.x_elems = M * Co;
+  a.x2 = f.x2; a.sW2 = f.C2; a.sH2 = (long long)d->W * f.C2; a.sN2 = (long long)d->H * d->W * f.C2; a.x2_elems = M * f.C2;
   a.C1 = Co;
   a.H = d->H; a.W = d->W; a.C = K;
   a.R = 1; a.S = 1; a.stride = 1; a.pad = 0; a.Ho = d->H; a.Wo = d->W;
   a.in_scale = nullptr; a.in_shift = nullptr; a.in_relu = 0;
-  a.w = w; a.Cout = Ci; a.K = K; a.M = M;
-  a.y = dx; a.ldy = Ci;
-  a.out_f32 = 0; a.accumulate = 0; a.bias = bias; a.stats = nullptr;
-  a.res = nullptr; a.res_mode = 0; a.relu = 0;
-  a.nseg = nseg; a.bnb_desc = bnb; a.bnb_pstride = param_stride;
+  a.w = f.w; a.Cout = Ci; a.K = K; a.M = M;
+  a.y = f.dx; a.ldy = Ci;
+  a.out_f32 = 0; a.accumulate = 0; a.bias = f.bias; a.stats = nullptr;
+  a.res = f.res; a.res_mode = f.res_mode; a.relu = 0;
+  a.nseg = f.nseg; a.bnb_desc = f.bnb; a.bnb_pstride = f.pstride;
   a.w_sstride = (long long)Ci * K; a.bias_sstride = Ci;
   return a;
 }
 
-extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
-                                          const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
-                                          long long param_stride, void* stream) {
-  if (fold_check(d, g, x, w, bias, dx, bnb, nseg)) return -1;
-  const int Co = d->Cout, Ci = d->C, K = Co + Ci;
-  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
+// segment s's slice of a fold launch (one BN segment, its weights and bias)
+static ConvArgs fold_segment(const FoldOp& f, const ConvArgs& a, int s, artsbir_bn_bwd_desc* bs) {
+  const int Co = f.d->Cout, Ci = f.d->C;
+  const long long seg_m = a.M / f.nseg;
+  const long long es = f.d->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
+  ConvArgs p = a;
+  if (f.bnb) { *bs = bnb_segment(f.bnb, s, seg_m, Ci, f.pstride); p.bnb_desc = bs; }
+  p.nseg = 1; p.M = seg_m;
+  p.x = reinterpret_cast<const char*>(f.g) + s * seg_m * Co * es; p.x_elems = seg_m * Co;
+  p.x2 = reinterpret_cast<const char*>(f.x2) + s * seg_m * f.C2 * es; p.x2_elems = seg_m * f.C2;
+  p.w = reinterpret_cast<const char*>(f.w) + s * a.w_sstride * es;
+  p.bias = f.bias + s * Ci;
+  p.y = reinterpret_cast<char*>(f.dx) + s * seg_m * Ci * es;
+  if (f.res_mode) p.res = reinterpret_cast<const char*>(f.res) + s * (f.res_mode == 2 ? seg_m / 4 : seg_m) * Ci * es;
+  return p;
+}
+
+static int fold_dgrad(const FoldOp& f, hipStream_t st) {
+  if (fold_check(f)) return -1;
+  const artsbir_conv_desc* d = f.d;
+  const int K = d->Cout + f.C2;
+  const long long M = (long long)d->N * d->H * d->W;
   const bool bf = d->dtype == ARTSBIR_DT_BF16;
   const long long es = bf ? 2 : 4;
-  hipStream_t st = (hipStream_t)stream;
-  const ConvArgs a = fold_conv_args(d, g, x, w, bias, dx, bnb, nseg, param_stride);
+  const ConvArgs a = fold_conv_args(f);
   // one launch over every segment, else one per segment (the tiles of a
   // launch then never straddle two), on the two-operand pipelined kernels
   if (bf) {
@@ -1164,16 +1216,9 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
     // no kernel took the whole batch (a tile would straddle two segments): one
     // launch per segment; segment 0 decides, a refusal there drops to the
     // concatenated form below (every segment has the same shape)
-    for (int s = 0; s < nseg; ++s) {
-      ConvArgs p = a;
+    for (int s = 0; s < f.nseg; ++s) {
       artsbir_bn_bwd_desc bs;
-      if (bnb) { bs = bnb_segment(bnb, s, seg_m, Ci, param_stride); p.bnb_desc = &bs; }
-      p.nseg = 1; p.M = seg_m;
-      p.x = reinterpret_cast<const bf16*>(g) + s * seg_m * Co; p.x_elems = seg_m * Co;
-      p.x2 = reinterpret_cast<const bf16*>(x) + s * seg_m * Ci; p.x2_elems = seg_m * Ci;
-      p.w = reinterpret_cast<const bf16*>(w) + s * a.w_sstride;
-      p.bias = bias + s * Ci;
-      p.y = reinterpret_cast<bf16*>(dx) + s * seg_m * Ci;
+      const ConvArgs p = fold_segment(f, a, s, &bs);
       rc = launch_conv<bf16>(p, st);
       if (rc < 0) return rc;
       if (rc > 0) {
@@ -1194,40 +1239,50 @@ extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void
     set_error("conv1x1_dgrad_fold: workspace of %zu bytes", need);
     return -1;
   }
-  const int rc = fold_concat_gemms(d, g, x, w, bias, dx, bnb, nseg, param_stride, a, ws, st);
+  const int rc = fold_concat_gemms(f, a, ws, st);
   (void)hipFreeAsync(ws, st);
   return rc;
 }
 
-static int fold_concat_gemms(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
-                             const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
-                             long long param_stride, const ConvArgs& a, void* ws, hipStream_t st) {
-  const int Co = d->Cout, Ci = d->C, K = Co + Ci;
-  const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
+extern "C" int artsbir_conv1x1_dgrad_fold(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
+                                          const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
+                                          long long param_stride, void* stream) {
+  if (bnb && bnb->kind != 1) { set_error("conv1x1_dgrad_fold: the fused BN backward must be kind 1 with one target"); return -1; }
+  const FoldOp f{d, g, x, d ? d->C : 0, w, bias, dx, nullptr, 0, bnb, nseg, param_stride};
+  return fold_dgrad(f, (hipStream_t)stream);
+}
+
+extern "C" int artsbir_conv1x1_dgrad_fold_y(const artsbir_conv_desc* d, const void* g, const void* y, const void* w,
+                                            const float* bias, void* dx, const void* res, int res_mode,
+                                            const artsbir_bn_bwd_desc* bnb, int nseg, long long param_stride,
+                                            void* stream) {
+  const FoldOp f{d, g, y, d ? d->Cout : 0, w, bias, dx, res, res_mode, bnb, nseg, param_stride};
+  return fold_dgrad(f, (hipStream_t)stream);
+}
+
+static int fold_concat_gemms(const FoldOp& f, const ConvArgs& a, void* ws, hipStream_t st) {
+  const artsbir_conv_desc* d = f.d;
+  const int Co = d->Cout, K = Co + f.C2;
+  const long long M = (long long)d->N * d->H * d->W, seg_m = M / f.nseg;
   const bool bf = d->dtype == ARTSBIR_DT_BF16;
   const long long es = bf ? 2 : 4;
   {
     const long long n = M * (K * es / 16);
     const unsigned grid = (unsigned)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
     if (bf)
-      hipLaunchKernelGGL(fold_concat_kernel<bf16>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const bf16*>(g),
-                         reinterpret_cast<const bf16*>(x), reinterpret_cast<bf16*>(ws), M, Co, Ci);
+      hipLaunchKernelGGL(fold_concat_kernel<bf16>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const bf16*>(f.g),
+                         reinterpret_cast<const bf16*>(f.x2), reinterpret_cast<bf16*>(ws), M, Co, f.C2);
     else
-      hipLaunchKernelGGL(fold_concat_kernel<float>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(g),
-                         reinterpret_cast<const float*>(x), reinterpret_cast<float*>(ws), M, Co, Ci);
+      hipLaunchKernelGGL(fold_concat_kernel<float>, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float*>(f.g),
+                         reinterpret_cast<const float*>(f.x2), reinterpret_cast<float*>(ws), M, Co, f.C2);
     ARTSBIR_CHECK_LAUNCH("fold_concat");
   }
-  for (int s = 0; s < nseg; ++s) {
-    ConvArgs p = a;
+  for (int s = 0; s < f.nseg; ++s) {
     artsbir_bn_bwd_desc bs;
-    if (bnb) { bs = bnb_segment(bnb, s, seg_m, Ci, param_stride); p.bnb_desc = &bs; }
+    ConvArgs p = fold_segment(f, a, s, &bs);
     p.x2 = nullptr; p.C1 = 0; p.w_sstride = 0; p.bias_sstride = 0;
-    p.nseg = 1; p.M = seg_m;
     p.x = reinterpret_cast<const char*>(ws) + s * seg_m * K * es; p.x_elems = seg_m * K;
     p.sW = K; p.sH = (long long)d->W * K; p.sN = (long long)d->H * d->W * K;
-    p.w = reinterpret_cast<const char*>(w) + s * a.w_sstride * es;
-    p.bias = bias + s * Ci;
-    p.y = reinterpret_cast<char*>(dx) + s * seg_m * Ci * es;
     const int rc = bf ? launch_conv<bf16>(p, st) : launch_conv<float>(p, st);
     if (rc) return -1;
   }
@@ -1242,14 +1297,16 @@ static int fold_concat_gemms(const artsbir_conv_desc* d, const void* g, const vo
 extern "C" int artsbir_conv1x1_dgrad_fold_wg(const artsbir_conv_desc* d, const void* g, const void* x, const void* w,
                                              const float* bias, void* dx, const artsbir_bn_bwd_desc* bnb, int nseg,
                                              long long param_stride, float* P, float* gram, void* stream) {
-  if (fold_check(d, g, x, w, bias, dx, bnb, nseg)) return -1;
+  if (bnb && bnb->kind != 1) { set_error("conv1x1_dgrad_fold_wg: the fused BN backward must be kind 1"); return -1; }
+  const FoldOp f{d, g, x, d ? d->C : 0, w, bias, dx, nullptr, 0, bnb, nseg, param_stride};
+  if (fold_check(f)) return -1;
   if (!P || !gram) { set_error("conv1x1_dgrad_fold_wg: null weight-gradient operand"); return -1; }
   const int Co = d->Cout, Ci = d->C;
   const long long M = (long long)d->N * d->H * d->W, seg_m = M / nseg;
   const long long es = d->dtype == ARTSBIR_DT_BF16 ? 2 : 4;
   static const bool off = getenv("ARTSBIR_FOLD_WG") && atoi(getenv("ARTSBIR_FOLD_WG")) == 0;  // measurement switch
   if (d->dtype == ARTSBIR_DT_BF16 && !off) {
-    ConvArgs a = fold_conv_args(d, g, x, w, bias, dx, bnb, nseg, param_stride);
+    ConvArgs a = fold_conv_args(f);
     a.wg_p = P; a.wg_gram = gram;
     const int rc = launch_conv<bf16>(a, (hipStream_t)stream);
     if (rc <= 0) return rc;

@@ -102,8 +102,20 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
   // of each 8-row wave instruction, with k-chunk csrc = slot ^ (row & 7)
   const int lrow = lane / CPR, lslot = lane % CPR;
   const int csrc = KS == 64 ? (lslot ^ lrow) : (lslot ^ ((lrow >> 2) & 2));
-  int rowoff[IPX], rowoff2[X2 ? IPX : 1];
+  int rowoff[IPX];
   unsigned rmask[IPX];
+  // X2: the row offsets into the second operand replace rowoff[] once, at the
+  // first stage past C1 (1x1, stride 1: the pixel itself) — not held beside
+  // them through the first operand's stages (the 8-wave tile's 128 VGPRs)
+  auto rowoff_x2 = [&](int u) {
+    const int row = (u * NW + wid) * RPI + lrow;
+    const long long gm = bpx + row;
+    const long long gmc = gm < a.M ? gm : bpx;
+    const long long img = gmc / HoWo;
+    const int rem = (int)(gmc - img * HoWo);
+    const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+    return (int)(((img - img0) * a.sN2 + (long long)oh * a.sH2 + (long long)ow * a.sW2) * 2);
+  };
 #pragma unroll
   for (int u = 0; u < IPX; ++u) {
     const int row = (u * NW + wid) * RPI + lrow;
@@ -115,7 +127,6 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
     const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
     const int ih0 = oh * a.stride - a.pad, iw0 = ow * a.stride - a.pad;
     rowoff[u] = (int)(((img - img0) * a.sN + (long long)ih0 * a.sH + (long long)iw0 * a.sW) * 2);
-    if constexpr (X2) rowoff2[u] = (int)(((img - img0) * a.sN2 + (long long)oh * a.sH2 + (long long)ow * a.sW2) * 2);
     unsigned msk = 0;
     for (int r = 0; r < a.R; ++r)
       for (int s = 0; s < a.S; ++s) {
@@ -134,6 +145,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
   const bool lps_hi = (ICH - 1) * NW + wid < ICH_TOT;
 
   int u_ci = 0, u_s = 0, u_r = 0;  // uniform-tap walk (C % 64 == 0)
+  bool on2 = false;                 // X2: rowoff[] holds the second operand's offsets
   auto issue = [&](int kt, int buf) {
     char* pxs = smem + buf * STAGE;
     char* chs = pxs + PXB;
@@ -145,7 +157,14 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
       int ci = u_ci;
       if constexpr (X2) {
         src2 = u_ci >= a.C1;
-        if (src2) ci -= a.C1;
+        if (src2) {
+          ci -= a.C1;
+          if (!on2) {
+            on2 = true;
+#pragma unroll
+            for (int u = 0; u < IPX; ++u) rowoff[u] = rowoff_x2(u);
+          }
+        }
       }
       tapoff = (u_r * (int)a.sH + u_s * (int)a.sW + ci + csrc * 8) * 2;
       kval = true;
@@ -167,8 +186,7 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
     for (int u = 0; u < IPX; ++u) {
       const bool ok = kval && ((rmask[u] >> (rs & 31)) & 1u);
       if constexpr (X2) {
-        if (src2) glds16(xr2, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff2[u] + tapoff) : PG_OOB);
-        else glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
+        glds16(src2 ? xr2 : xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
       } else {
         glds16(xr, pxs + (u * NW + wid) * 1024, ok ? (unsigned)(rowoff[u] + tapoff) : PG_OOB);
       }
@@ -259,8 +277,8 @@ __global__ void __launch_bounds__(64 * WPX * WCH, GLB ? (WPX * WCH == 8 ? 4 : 3)
 #endif
     if constexpr (PG_GLB_OLD || NW >= 8) {  // channel pairs outside (the 8-wave tile: 128 VGPRs)
       EpiStage sgg{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, seg0};
-      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true, X2>(a, acc, bpx, bch, wpx,
-                                                                                                wch, fr, fq, red, sgg);
+      pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, 1, true, X2, NW >= 8>(
+          a, acc, bpx, bch, wpx, wch, fr, fq, red, sgg);
     } else {
       // the 8-wave 256 x 128 tile runs at 128 VGPRs (two workgroups per CU):
       // statistics reduced per (tile, pair) there, carried in registers otherwise
@@ -1377,6 +1395,40 @@ static bool pg_k32w8_launch(const PgArgs& a, bool multi, hipStream_t st) {
   return true;
 }
 
+// The y-side fold of the block's first conv with the fused BN-backward reduction
+// of the previous block's output (artsbir_conv1x1_dgrad_fold_y: residual added,
+// kinds 2 / 3, one or two targets): candidates 16 (128 x 128 GLB), 18 (256 x 128
+// GLB, kind 3 with one target: the 8-wave tile's 128 VGPRs) and 22 (pp256)
+static bool pg_fold_res_launch(const PgArgs& a, int c, hipStream_t st) {
+  if (!a.res_mode) return false;
+  auto ntl = [&](int bpx, int bch) { return ((a.M + bpx - 1) / bpx) * ((a.Cout + bch - 1) / bch); };
+  const bool two = a.bnb_nt == 2;
+  switch (c) {
+    case 16: {
+      if (!pg_fold_ok(a, 128, 32) || ntl(128, 128) > 0x7fffffffLL) return false;
+      const dim3 g((unsigned)ntl(128, 128));
+#define PG_FGLB(BKV, TWOV) \
+  hipLaunchKernelGGL((pgemm_kernel<128, 128, 2, 2, 3, false, BKV, TWOV, false, 32, true, true>), g, dim3(256), 0, st, a)
+      if (a.bnb == 3 && two) PG_FGLB(3, true);
+      else if (a.bnb == 3) PG_FGLB(3, false);
+      else if (two) PG_FGLB(2, true);
+      else PG_FGLB(2, false);
+#undef PG_FGLB
+      set_last_kernel("pgemm_kernel<128,128,k32,glb,bnb,fold>");
+      return true;
+    }
+    case 18: {
+      if (a.bnb != 3 || two || !pg_fold_ok(a, 256, 32) || ntl(256, 128) > 0x7fffffffLL) return false;
+      hipLaunchKernelGGL((pgemm_kernel<256, 128, 4, 2, 3, false, 3, false, false, 32, true, true>),
+                         dim3((unsigned)ntl(256, 128)), dim3(512), 0, st, a);
+      set_last_kernel("pgemm_kernel<256,128,k32,glb,bnb,fold>");
+      return true;
+    }
+    default:
+      return false;
+  }
+}
+
 // The folded BatchNorm-backward data gradient (a.x2: artsbir_conv1x1_dgrad_fold):
 // the candidates instantiated with the two-operand loader — 2 (256 x 64), 16 (the
 // 128 x 128 GLB tile, plain or ACT epilogue), 19 (256 x 128 GLB, plain), 10 / 14
@@ -1384,12 +1436,13 @@ static bool pg_k32w8_launch(const PgArgs& a, bool multi, hipStream_t st) {
 // (pp256, in pp256_launch); epilogue: per-segment bias (+ the kind-1 mask and
 // BN-backward reduction of the BatchNorm before the conv's input)
 static bool pg_fold_launch(const PgArgs& a, int c, hipStream_t st) {
-  if (!a.x2 || !a.bias || a.relu || a.stats || a.res_mode) return false;
-  if (a.bnb && (a.bnb != 1 || a.bnb_nt != 1)) return false;
+  if (!a.x2 || !a.bias || a.relu || a.stats || a.res_mode == 3) return false;
+  if (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) return false;
   bool multi;
   if (!pg_supported(a, multi) || multi) return false;
-  const bool k1 = a.bnb == 1;
   auto ntl = [&](int bpx, int bch) { return ((a.M + bpx - 1) / bpx) * ((a.Cout + bch - 1) / bch); };
+  if (a.bnb == 2 || a.bnb == 3) return pg_fold_res_launch(a, c, st);
+  const bool k1 = a.bnb == 1;
   switch (c) {
     case 2: {
       if (!pg_fold_ok(a, 256, 64) || ntl(256, 64) > 0x7fffffffLL) return false;

@@ -581,8 +581,10 @@ __device__ __forceinline__ void epi_prefetch(const PgArgs& a, EpiRegs<MTC / 2, N
 // are always staged, the BN constants always come from the LDS table.
 // FB: the per-segment bias of a folded BatchNorm backward (artsbir_conv1x1_dgrad_fold)
 // is added to the accumulators first, before any mask / BN-backward reduction.
+// FBL: that bias loaded per use (L1-resident) instead of held in 8 VGPRs across
+// the pair's pixel tiles (the 8-wave 256 x 128 tile's 128-VGPR budget)
 template <int BK, bool TWO, bool S_RES, bool S_Y1, bool S_MK, int BCH, int MTC, int NTP, int WTPX, int WTCH,
-          bool REG = false, int EJB = 2, bool GLB = false, bool FB = false>
+          bool REG = false, int EJB = 2, bool GLB = false, bool FB = false, bool FBL = false>
 __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
                                               int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg,
                                               const EpiRegs<MTC / 2, NTP>* er = nullptr) {
@@ -604,8 +606,8 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
     float s1[8], s2[8], s3[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
-    float fbias[FB ? 8 : 1];
-    if constexpr (FB) loadf8v(a.bias + wseg * a.bias_sstride + chc, fbias);
+    float fbias[FB && !FBL ? 8 : 1];
+    if constexpr (FB && !FBL) loadf8v(a.bias + wseg * a.bias_sstride + chc, fbias);
     // BN constants (LDS table): xhat_t = (y - m_t) * xa_t; ACT mask (y - mm) * ms + mh > 0
     float xa0[8], m0[8], xa1[8], m1[8], mm[8], ms[8], mh[8];
     if constexpr (BNB && GLB) {  // the same rows pg_prm_fill tabulates, straight from the (L2-resident) vectors
@@ -684,7 +686,12 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
         float v[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) { v[r] = acc[2 * p][j0 + u][r]; v[4 + r] = acc[2 * p + 1][j0 + u][r]; }
-        if constexpr (FB) {
+        if constexpr (FB && FBL) {
+          float fb[8];
+          loadf8v(a.bias + wseg * a.bias_sstride + chc, fb);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += fb[e];
+        } else if constexpr (FB) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += fbias[e];
         }

@@ -336,14 +336,21 @@ bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st) {
   if (((256 + HoWo - 1) / HoWo + 2) * a.sN * 2 + 2LL * (a.pad * a.sH + a.pad * a.sW) > 0x7fffffffLL) return false;
   if (a.M > (1LL << 40)) return false;
   if (a.seg_m > 0 && (a.seg_m % 64 != 0 || a.seg_m < 256 || a.M % a.seg_m != 0)) return false;
-  if (a.x2 || a.w_sstride) {  // the folded BatchNorm-backward data gradient (plain or ACT epilogue + bias)
-    if (!a.x2 || !a.bias || !pg_fold_ok(a, PP_BPX, PP_KS) || a.relu || a.stats || a.res_mode) return false;
-    if (a.bnb && (a.bnb != 1 || a.bnb_nt != 1 || a.Cout % 8 != 0)) return false;
+  if (a.x2 || a.w_sstride) {  // the folded BatchNorm-backward data gradient (plain, ACT or RES epilogue + bias)
+    if (!a.x2 || !a.bias || !pg_fold_ok(a, PP_BPX, PP_KS) || a.relu || a.stats || a.res_mode == 3) return false;
+    if (a.bnb == 1 && (a.bnb_nt != 1 || a.res_mode)) return false;
+    if ((a.bnb == 2 || a.bnb == 3) && !a.res_mode) return false;
+    if (a.bnb && a.Cout % 8 != 0) return false;
     if (((256 + HoWo - 1) / HoWo + 2) * a.sN2 * 2 > 0x7fffffffLL) return false;
     const long long T = ((a.M + PP_BPX - 1) / PP_BPX) * ((a.Cout + PP_BCH - 1) / PP_BCH);
     if (T > 0x7fffffffLL) return false;
-    if (a.bnb) hipLaunchKernelGGL((pp256_kernel<1, false, false, true>), dim3((unsigned)T), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((pp256_kernel<0, false, false, true>), dim3((unsigned)T), dim3(512), 0, st, a);
+    const dim3 g((unsigned)T), b(512);
+    if (a.bnb == 1) hipLaunchKernelGGL((pp256_kernel<1, false, false, true>), g, b, 0, st, a);
+    else if (a.bnb == 2 && a.bnb_nt == 2) hipLaunchKernelGGL((pp256_kernel<2, true, false, true>), g, b, 0, st, a);
+    else if (a.bnb == 2) hipLaunchKernelGGL((pp256_kernel<2, false, false, true>), g, b, 0, st, a);
+    else if (a.bnb == 3 && a.bnb_nt == 2) hipLaunchKernelGGL((pp256_kernel<3, true, false, true>), g, b, 0, st, a);
+    else if (a.bnb == 3) hipLaunchKernelGGL((pp256_kernel<3, false, false, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((pp256_kernel<0, false, false, true>), g, b, 0, st, a);
     set_last_kernel(a.bnb ? "pp256_kernel<bnb,fold>" : "pp256_kernel<fold>");
     return true;
   }

@@ -71,6 +71,13 @@ FOLD_BN = [os.environ.get("ARTSBIR_FOLD_BN", "1") != "0"]
 # the layer-1 fold data gradients also accumulate their weight-gradient operands
 # (artsbir_conv1x1_dgrad_fold_wg): g and x read once for both gradients
 FOLD_WG = [os.environ.get("ARTSBIR_FOLD_WG", "1") != "0"]
+# ARTSBIR_FOLD_BN1=1 folds bn1's backward (models.py:199, conv1 -> bn1 of every
+# Bottleneck) through conv1 with bn1's input y1 (the y-side fold,
+# artsbir_conv1x1_dgrad_fold_y): dy1 is never written or read.  Off by default:
+# its weight gradient needs g1^T x and y1^T x (twice conv1's weight-gradient
+# MFMA work on the side stream), which cost the C2 step more than the apply
+# pass it removes from the main stream (94.8 vs 91.2 ms on one box)
+FOLD_BN1 = [os.environ.get("ARTSBIR_FOLD_BN1", "0") == "1"]
 
 
 def set_deterministic(on: bool = True) -> bool:
@@ -581,9 +588,11 @@ class Engine:
 
         # residual stages (models.py:354-357)
         bctx = []
-        for blk, bp in zip(m.blocks(), pk["blocks"]):
-            h, c = self._block_fwd(blk, bp, h, train, stats, fold=fold, h_cs=h_cs)
-            h_cs = None
+        blocks = m.blocks()
+        for i, (blk, bp) in enumerate(zip(blocks, pk["blocks"])):
+            # the next block's folded conv1 needs the column sums of its input
+            h, c, h_cs = self._block_fwd(blk, bp, h, train, stats, fold=fold, h_cs=h_cs,
+                                         out_cs=fold and self._fold1_on() and i + 1 < len(blocks))
             bctx.append(c if save else None)
         ctx["blocks"] = bctx
 
@@ -602,7 +611,12 @@ class Engine:
         order) a reduce-only pass supplies g and the reduction (_bn_reduce_g)"""
         return FOLD_BN[0] and type(self) is Engine
 
-    def _block_fwd(self, blk, bp, h, train, stats, fold=False, h_cs=None):
+    def _fold1_on(self):
+        """whether the backward folds bn1 through conv1 (the y-side fold; it needs
+        the column sums of the block input from the forward, like _fold_on)"""
+        return FOLD_BN1[0] and self._fold_on()
+
+    def _block_fwd(self, blk, bp, h, train, stats, fold=False, h_cs=None, out_cs=False):
         B, H, W, Cin = h.shape
         s = blk.stride
         # BN+ReLU outputs are materialised once (bf16): cheaper than re-applying
@@ -639,15 +653,16 @@ class Engine:
         bits = None
         if train and _fuse_bnb() and MASK_BITS and self.dt == _hip.DT_BF16:
             bits = torch.empty(out.numel() // 8, dtype=torch.uint8, device=out.device)
-        call("artsbir_block_out_mask", self.dt, ptr(y3), ptr(b3.block), ptr(yd), ptr(bd.block) if bd else None,
+        ocs = torch.zeros(G, NSLOT, C, dtype=torch.float32, device=out.device) if out_cs else None
+        call("artsbir_block_out_colsum", self.dt, ptr(y3), ptr(b3.block), ptr(yd), ptr(bd.block) if bd else None,
              None if yd is not None else ptr(h), rows * G, C, G, ptr(out),
-             bits.data_ptr() if bits is not None else None, _s(),
+             bits.data_ptr() if bits is not None else None, ptr(ocs), _s(),
              kernel="block_out_kernel", nbytes=float(out.element_size() * rows * G * C * 3 + (rows * G * C // 8 if bits
                                                                                                   is not None else 0)),
-             tag=f"block_out {rows * G}x{C}")
+             tag=f"block_out {rows * G}x{C}{' +colsum' if ocs is not None else ''}")
         ctx = dict(h=h, y1=y1, a1=a1, y2=y2, p2=p2, y3=y3, yd=yd, pd=pd, out=out, bits=bits, b1=b1, b2=b2, b3=b3,
-                   bd=bd, cs2=cs2, csd=csd)
-        return out, ctx
+                   bd=bd, cs2=cs2, csd=csd, h_cs=h_cs)
+        return out, ctx, ocs
 
     def _attnpool_fwd(self, ap, pk, h):
         B, Hs, Ws, C = h.shape
@@ -821,26 +836,28 @@ class Engine:
              tag=f"bn_bwd_apply k{kind} {B}x{H}x{W}x{C} t{len(targets)}")
         return dys
 
-    def _bn_reduce_g(self, d, targets, ws, mask):
-        """the reduce half of _bn_bwd for the block output (kind 0): g = d * relu
-        mask is written and Σg, Σg·x̂ of every target and segment go to the slots
-        (fixed-order f64 in the deterministic mode), no apply pass — the BN
-        backward is then folded through the 1x1 convs.  Returns (g, fused) in
-        the form of a fused data gradient's hand-over (_bnb_fused_desc)."""
+    def _bn_reduce_g(self, d, targets, ws, mask=None, kind=0, mask_bn=None):
+        """the reduce half of _bn_bwd: g = d * relu mask is written (kind 0: the
+        block output's mask; kind 1: the BN before the ReLU, mask_bn) and Σg,
+        Σg·x̂ of every target and segment go to the slots (fixed-order f64 in the
+        deterministic mode), no apply pass — the BN backward is then folded
+        through the 1x1 convs.  Returns (g, fused) in the form of a fused data
+        gradient's hand-over (_bnb_fused_desc)."""
         y0 = targets[0][0]
         B, H, W, C = y0.shape
         G = self._G
         g = torch.empty_like(d)
         slots = [ws.take(C * G) for _ in targets]
-        desc = self._seg_desc(0, 0, targets, B // G, H, W, C)
+        desc = self._seg_desc(kind, 0, targets, B // G, H, W, C)
         desc.d = ptr(d)
         desc.mask = ptr(mask)
+        desc.mask_bn = ptr(mask_bn.block) if mask_bn is not None else None
         desc.gout = ptr(g)
         for i in range(len(targets)):
             desc.slots[i] = ptr(slots[i])
-        call("artsbir_bn_bwd_reduce", desc, _s(), kernel="bn_bwd_reduce_kernel<0>",
-             nbytes=float(y0.element_size() * B * H * W * C * (3 + len(targets))),
-             tag=f"bn_bwd_reduce k0 {B}x{H}x{W}x{C} t{len(targets)} +g")
+        call("artsbir_bn_bwd_reduce", desc, _s(), kernel=f"bn_bwd_reduce_kernel<{kind}>",
+             nbytes=float(y0.element_size() * B * H * W * C * (2 + (kind == 0) + len(targets))),
+             tag=f"bn_bwd_reduce k{kind} {B}x{H}x{W}x{C} t{len(targets)} +g")
         return g, (None, slots, targets)
 
     def _bn_coefs(self, targets, bnmods, slots, grads, count):
@@ -1111,6 +1128,82 @@ class Engine:
         if side is not main:
             self._side_keep.extend([g, x, coef, st.buf, buf, wsp, cs])
 
+    # ------------------------- bn1 folded through conv1 with its own input (y-side)
+    def _fold_weights_y(self, packs, conv, coef, st: BNState):
+        """per-segment weights [G][Ci][2 Co] and bias [G][Ci] of the y-side fold
+        (artsbir_bn_fold_bwd_prep_y): the g side diag(c1) W, the y side
+        diag(b') W, the bias k W"""
+        _, wd = packs
+        co, ci = conv.weight.shape[:2]
+        G = self._G
+        wout = self._empty(G, ci, 2 * co, device=wd.device)
+        bias = torch.empty(G, ci, dtype=torch.float32, device=wd.device)
+        es = wout.element_size()
+        call("artsbir_bn_fold_bwd_prep_y", self.dt, co, ci, ptr(wd), ptr(coef), ptr(st.buf), 4 * co, G, ptr(wout),
+             ptr(bias), _s(), kernel="fold_prep_y_kernel", nbytes=float(es * ci * co * (1 + 2 * G) + 4 * G * ci),
+             tag=f"fold_prep_y {co}->{ci} x{G}")
+        return wout, bias
+
+    def _dgrad_fold_y(self, g, y, fold, conv, out_shape, res, res_mode, fused=None):
+        """dx = [g | y] w_s^T + bias_s (+ residual) (artsbir_conv1x1_dgrad_fold_y):
+        the data gradient of a 1x1 conv through the BatchNorm after it, from the
+        masked gradient g at the BN output and the BN input y (the conv output)"""
+        wout, bias = fold
+        B, H, W, ci = out_shape
+        co = conv.weight.shape[0]
+        dx = self._empty(B, H, W, ci, device=g.device)
+        d = self._desc(B, H, W, ci, co, 1, 1, 1, 0)
+        px = B * H * W
+        es = dx.element_size()
+        nb = 2 * px * co + self._G * ci * 2 * co + px * ci + (px * ci if res_mode == 1 else
+                                                                px * ci // 4 if res_mode == 2 else 0)
+        if fused is not None:
+            nb += px * ci * (fused[0].ntarget + {0: 1.0, 3: 1.0 / 16}.get(fused[0].kind, 0.0))
+        call("artsbir_conv1x1_dgrad_fold_y", d, ptr(g), ptr(y), ptr(wout), ptr(bias), ptr(dx), ptr(res), res_mode,
+             ctypes.byref(fused[0]) if fused is not None else None, self._G, 4 * ci, _s(), kernel="auto",
+             flops=2.0 * px * ci * 2 * co, nbytes=float(es * nb),
+             tag=f"dgrad_fold_y{'+bn' + str(fused[0].kind) if fused is not None else ''} {B}x{H}x{W}x{co}+{co}->{ci} "
+                 f"res{res_mode}")
+        return dx
+
+    def _wgrad_fold_y(self, g, y, x, conv, coef, st: BNState, grads, cs=None):
+        """weight gradient of a 1x1 conv through the BatchNorm after it, y-side
+        (side stream): per segment g^T x and y^T x in one launch
+        (artsbir_gemm_tn2), combined with the column sums of x (cs [G][slots][Ci]
+        from the forward's block_out, else a column-sum pass here) by
+        artsbir_bn_fold_wgrad_combine_y into the gradient buffer"""
+        if SKIP_WGRAD[0]:
+            return
+        main = torch.cuda.current_stream()
+        side = self._side_stream(g.device) if OVERLAP_WGRAD else main
+        if side is not main:
+            side.wait_stream(main)
+        G = self._G
+        B, H, W, ci = x.shape
+        co = conv.weight.shape[0]
+        Bs = B // G
+        Ms = Bs * H * W
+        es = x.element_size()
+        with torch.cuda.stream(side):
+            own_cs = cs is None
+            buf = torch.zeros(2 * G * co * ci + (G * ci if own_cs else 0), dtype=torch.float32, device=x.device)
+            P, Q = buf[:G * co * ci].view(G, co, ci), buf[G * co * ci:2 * G * co * ci].view(G, co, ci)
+            if own_cs:
+                cs = buf[2 * G * co * ci:].view(G, 1, ci)
+            for s in range(G):
+                gs, ys, xs = g[s * Bs:(s + 1) * Bs], y[s * Bs:(s + 1) * Bs], x[s * Bs:(s + 1) * Bs]
+                call("artsbir_gemm_tn2", self.dt, Ms, co, co, ci, ptr(gs), co, ptr(ys), co, ptr(xs), ci,
+                     ptr(P[s]), ptr(Q[s]), _s(), kernel="auto", flops=4.0 * Ms * co * ci,
+                     nbytes=float(es * Ms * (2 * co + ci) + 8 * co * ci), tag=f"wgrad_fold_y {Ms}x{co}+{co}x{ci}")
+                if own_cs:
+                    call("artsbir_colsum", self.dt, ptr(xs), Ms, ci, ci, ptr(cs[s]), _s(), kernel="colsum_kernel",
+                         nbytes=float(es * Ms * ci), tag=f"colsum {Ms}x{ci}")
+            call("artsbir_bn_fold_wgrad_combine_y", co, ci, G, ptr(P), ptr(Q), ptr(cs), cs.shape[1], ptr(coef),
+                 ptr(st.buf), 4 * co, ptr(grads[conv.weight]), _s(), kernel="fold_wgrad_combine_kernel",
+                 nbytes=float(4 * (2 * G * co * ci + 2 * co * ci)), tag=f"fold_combine_y {co}x{ci}")
+        if side is not main:
+            self._side_keep.extend([g, y, x, coef, st.buf, buf, cs])
+
     def _block_bwd(self, blk, bp, c, dout, grads, ws, fused_res=None, prev=None):
         """backward of one Bottleneck.  dout: gradient of the block output, or —
         when fused_res is given — g = dout * relu-mask with the block-output BN
@@ -1174,7 +1267,22 @@ class Engine:
                 self._wgrad_post(held)
                 dy2, = self._bn_bwd(1, dp, [(y2, b2)], [blk.bn2], ws, grads, mask_bn=b2, pool=s if s > 1 else 0)
         held = self._wgrad_pre(dy2, Act(c["a1"]), blk.conv2, 1, 1, grads)
-        if _fuse_bnb():
+        # bn1 folded through conv1 with its input y1 (models.py:198-199): no dy1
+        fold1 = fold and self._fold1_on()
+        held1 = None
+        if fold1:
+            if _fuse_bnb():
+                f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
+                g1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape, fused=f1)
+            else:  # deterministic: the fixed-order reduce-only pass writes g1
+                da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
+                g1, f1 = self._bn_reduce_g(da1, [(y1, b1)], ws, kind=1, mask_bn=b1)
+            self._wgrad_post(held)
+            B1, H1, W1, _ = y1.shape
+            coef1, = self._bn_coefs([(y1, b1)], [blk.bn1], f1[1], grads, float(B1 // self._G * H1 * W1))
+            fw1 = self._fold_weights_y(bp["conv1"], blk.conv1, coef1, b1)
+            self._wgrad_fold_y(g1, y1, h, blk.conv1, coef1, b1, grads, c.get("h_cs"))
+        elif _fuse_bnb():
             f1 = self._bnb_fused_desc(1, [(y1, b1)], ws, mask_bn=b1)
             g1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape, fused=f1)
             self._wgrad_post(held)
@@ -1183,7 +1291,8 @@ class Engine:
             da1 = self._dgrad(dy2, bp["conv2"][1], blk.conv2, 1, y1.shape)
             self._wgrad_post(held)
             dy1, = self._bn_bwd(1, da1, [(y1, b1)], [blk.bn1], ws, grads, mask_bn=b1)
-        held1 = self._wgrad_pre(dy1, Act(h), blk.conv1, 1, 0, grads)
+        if not fold1:
+            held1 = self._wgrad_pre(dy1, Act(h), blk.conv1, 1, 0, grads)
         if has_ds:
             din = pd if s > 1 else h
             dconv = blk.downsample[1]
@@ -1211,8 +1320,11 @@ class Engine:
                 fprev = self._bnb_fused_desc(3, ptargets, ws, mask=pc["bits"])
             else:
                 fprev = self._bnb_fused_desc(0, ptargets, ws, mask=pc["out"])
-        dh = self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=res, res_mode=res_mode, fused=fprev)
-        self._wgrad_post(held1)
+        if fold1:
+            dh = self._dgrad_fold_y(g1, y1, fw1, blk.conv1, h.shape, res, res_mode, fused=fprev)
+        else:
+            dh = self._dgrad(dy1, bp["conv1"][1], blk.conv1, 0, h.shape, res=res, res_mode=res_mode, fused=fprev)
+            self._wgrad_post(held1)
         return dh, fprev
 
     def _stem_bwd(self, m, pk, c, dh, grads, ws):
@@ -1299,7 +1411,7 @@ class ModuleEngine(Engine):
         if hasattr(m, "conv3"):
             nbn = sum(b.num_features for b in m.modules() if isinstance(b, torch.nn.BatchNorm2d))
             stats = _Arena(torch.zeros(max(2 * NSLOT * nbn, 1), dtype=torch.float32, device=x.device), NSLOT * 2)
-            out, c = self._block_fwd(m, pk, h, train, stats)
+            out, c, _ = self._block_fwd(m, pk, h, train, stats)
             return out.permute(0, 3, 1, 2).float().contiguous(), {"train": train, "c": c}
         out, c = self._attnpool_fwd(m, pk, h)
         return out.float(), {"train": train, "c": c}

@@ -169,6 +169,34 @@ int artsbir_bn_fold_wgrad_combine(int dtype, int Co, int Ci, int nseg, const flo
                                   const float* colsums, int cs_slots, const void* w, const float* coef,
                                   const float* prm, long long pstride, float* dw, float* workspace, void* stream);
 
+/* The y-side fold: the BatchNorm2d(train) right after a 1x1 Conv2d folded into
+ * that conv's data gradient with the BN's own input y (the conv output) instead of
+ * the conv input — models.py:198-199 conv1 -> bn1 of the Bottleneck, replacing
+ * artsbir_bn_bwd_apply (kind 2) + artsbir_conv2d_dgrad_bnb of conv1 (see
+ * csrc/fold.hip): dy = c1 g + b' y + k, so dx = [g | y] w_s^T + bias_s (+ the
+ * residual: res_mode 1 res[m][ci], 2 the 2x2 average-unpool of res) for the
+ * pixels of segment s.  d: the FORWARD conv (x [N][H][W][Ci], C = Ci, Cout = Co,
+ * 1x1 stride 1); g, y [N][H][W][Co]; w [nseg][Ci][2 Co] and bias [nseg][Ci] from
+ * artsbir_bn_fold_bwd_prep_y.  bnb (optional): the reduction of the BN(s) at
+ * the block input, fused as in artsbir_conv2d_dgrad_bnb — kind 0 / 3 (1-2
+ * targets, the residual required) or kind 1 (one target, no residual). */
+int artsbir_conv1x1_dgrad_fold_y(const artsbir_conv_desc* d, const void* g, const void* y, const void* w,
+                                 const float* bias, void* dx, const void* res, int res_mode,
+                                 const artsbir_bn_bwd_desc* bnb, int nseg, long long param_stride, void* stream);
+/* Weights of artsbir_conv1x1_dgrad_fold_y for every BN segment s:
+ * wout[s][ci][co] = c1_s[co] W[co][ci], wout[s][ci][Co + co] = b'_s[co] W[co][ci],
+ * bias[s][ci] = sum_co W[co][ci] k_s[co]  (b' = -c1 c3 istd, k = -c1 (c2 - c3 istd mean));
+ * wt, coef, prm as artsbir_bn_fold_bwd_prep. */
+int artsbir_bn_fold_bwd_prep_y(int dtype, int Co, int Ci, const void* wt, const float* coef, const float* prm,
+                               long long pstride, int nseg, void* wout, float* bias, void* stream);
+/* Its weight gradient: dw[co][ci] += sum_s c1_s[co] P_s[co][ci] + b'_s[co] Q_s[co][ci]
+ * + k_s[co] colsums_s[ci] with P_s = g_s^T x_s, Q_s = y_s^T x_s ([nseg][Co][Ci] f32,
+ * artsbir_gemm_tn2) and colsums [nseg][cs_slots][Ci] of the conv input x
+ * (artsbir_block_out_colsum). */
+int artsbir_bn_fold_wgrad_combine_y(int Co, int Ci, int nseg, const float* P, const float* Q, const float* colsums,
+                                    int cs_slots, const float* coef, const float* prm, long long pstride, float* dw,
+                                    void* stream);
+
 /* ---- layout / parameter packing ---------------------------------------- */
 /* x.type(weight dtype) + NCHW -> NHWC8 (models.py:352); x [B][Cin<=8][H][W] f32. */
 int artsbir_pack_input(int dtype, const float* x, int B, int Cin, int H, int W, void* out, void* stream);
@@ -241,6 +269,13 @@ int artsbir_block_out(int dtype, const void* y3, const float* bn3, const void* y
 int artsbir_block_out_mask(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
                            const void* identity, long long rows, int C, int nseg, void* out, unsigned char* mask_bits,
                            void* stream);
+/* artsbir_block_out_mask also accumulating the column sums of the stored output
+ * per segment: colsum[s][r][c] += sum over segment s's rows of out[.][c], spread
+ * over replica rows r < ARTSBIR_NSLOT (mask_bits optional) — the 1^T x of the
+ * next block's folded conv1 (artsbir_bn_fold_wgrad_combine_y). */
+int artsbir_block_out_colsum(int dtype, const void* y3, const float* bn3, const void* yd, const float* bnd,
+                             const void* identity, long long rows, int C, int nseg, void* out,
+                             unsigned char* mask_bits, float* colsum, void* stream);
 
 /* BatchNorm2d(train) backward, see elementwise.hip for the math. */
 struct artsbir_bn_bwd_desc {
