@@ -28,6 +28,10 @@ CONV = [  # H, W (input), C, Cout, R, stride
     (112, 112, 32, 64, 3, 1),    # stem conv3
 ]
 DENSE = [(75648, 2304, 768), (75648, 768, 768), (75648, 3072, 768), (75648, 768, 3072)]  # M, N(out), K(in)
+# the folded BatchNorm backward's g^T x and x^T x per BN segment (artsbir_gemm_tn2,
+# engine._wgrad_fold): M = 384 images' pixels, N1 = Co (g), N2 = K = Ci (x)
+TN2 = [(301056, 512, 128), (301056, 512, 256), (75264, 1024, 256), (75264, 1024, 512), (18816, 2048, 512),
+       (18816, 2048, 1024)]
 
 
 def timeit(fn, reps=3):
@@ -85,6 +89,17 @@ def main():
                   lambda: _hip.call("artsbir_conv2d_wgrad", d, dy.data_ptr(), x.data_ptr(), None, None, 0,
                                     dw.data_ptr(), st), ncand)
             del x, dy, dw
+    if "tn2" in which:
+        for (M, N1, K) in TN2:
+            dy = torch.randn(M, N1, device=dev).bfloat16()
+            x = torch.randn(M, K, device=dev).bfloat16()
+            dw = torch.zeros(N1, K, device=dev)
+            dw2 = torch.zeros(K, K, device=dev)
+            fl = 2.0 * M * (N1 + K) * K
+            sweep(f"tn2 M={M} {N1}+{K}x{K} ({M * (N1 + K) * 2 / 1e6:.0f} MB)", fl,
+                  lambda: _hip.call("artsbir_gemm_tn2", _hip.DT_BF16, M, N1, K, K, dy.data_ptr(), N1, x.data_ptr(), K,
+                                    x.data_ptr(), K, dw.data_ptr(), dw2.data_ptr(), st), ncand)
+            del dy, x, dw, dw2
     if "dense" in which:
         for (M, N, K) in DENSE:
             dy = torch.randn(M, N, device=dev).bfloat16()
