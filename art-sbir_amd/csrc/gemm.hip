@@ -819,7 +819,7 @@ static int tune_conv(const ConvArgs& a, const PgArgs& p, hipStream_t st) {
   // caller's overlapped weight gradients) would otherwise share the chip with
   // some trials and not others and make the choice noisy
   (void)hipDeviceSynchronize();
-  static const int cands[] = {-2, 0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 18, 19, 20, 21, 22, 24, 25};
+  static const int cands[] = {-2, 0, 1, 2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 18, 19, 20, 21, 22, 24, 25, 26};
   int best = -2;
   float best_ms = 1e30f;
   for (int c : cands) {

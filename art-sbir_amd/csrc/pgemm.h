@@ -104,6 +104,9 @@ bool pgemm_launch_cfg(const PgArgs& a, int cfg, hipStream_t st);
 // workgroup / persistent over 256 workgroups; false when the shape or epilogue
 // is outside it (C % 32 != 0, LDS-staged operands).
 bool pp256_launch(const PgArgs& a, bool persistent, hipStream_t st);
+// Candidate 26 (rstream.hip): the streaming 1x1 data gradient with a RES-kind
+// fused BN-backward epilogue (K 64 / 128, C % 256 == 0); false outside it
+bool rstream_launch(const PgArgs& a, hipStream_t st);
 // whether a launch with a two-operand reduction / per-segment weights can be
 // taken by a tile of BPX pixels (1x1 only, C1 a whole number of KS-k stages,
 // segments a whole number of tiles)

@@ -1541,6 +1541,7 @@ bool pgemm_launch_cfg(const PgArgs& a, int c, hipStream_t st) {
   if (act && (a.stats || a.bnb)) return false;
   // res_mode 3 (gated data gradient, pg_epilogue_k only): the plain pgemm_kernel tiles
   if (c == 22 || c == 23) return pp256_launch(a, c == 23, st);  // pp256.hip: every epilogue it supports
+  if (c == 26) return rstream_launch(a, st);                      // rstream.hip: RES-kind 1x1 dgrads
   if (a.res_mode == 3 && (c < 0 || (c >= kNumCfg && c != 16 && (c < 11 || c > 13)) || a.bnb || a.R * a.S != 1))
     return false;
   if (c == 20) return !act && sconv_launch(a, st);

@@ -32,6 +32,7 @@ CONV = {
     "22": r"pp256_kernel(<bnb>)?$",
     "24": r"pstream_kernel<(32|64|128),nt>$",
     "25": r"pstream_kernel<(64|128),k32,nt>$",
+    "26": r"rstream_kernel<bnb(,two)?>$",
 }
 
 

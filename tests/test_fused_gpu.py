@@ -15,7 +15,8 @@ import _kernels
 
 pytestmark = pytest.mark.gpu
 
-CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "22", "-2"]
+CFGS = ["auto", "0", "1", "2", "3", "4", "5", "10", "11", "12", "13", "14", "15", "16", "18", "19", "20", "21", "22", "26",
+        "-2"]
 
 
 @pytest.fixture
@@ -87,6 +88,8 @@ BNB_CASES = [
     (4, 2, 16, 16, 32, 64, 3, 1, 1, 1, 0),     # stem-like: 64-ch dY -> 32-ch dX
     (6, 3, 16, 16, 32, 32, 3, 1, 1, 1, 0),     # stem conv2 data gradient, segments
     (3, 1, 9, 13, 64, 64, 3, 1, 1, 1, 0),      # layer-1 3x3, image-crossing tiles
+    (4, 2, 16, 16, 512, 128, 1, 0, 0, 2, 1),   # RES, K 128 (layer-2 conv1 family), two targets
+    (6, 3, 8, 8, 256, 128, 1, 0, 0, 1, 2),     # RES, K 128, avg-unpool residual
 ]
 
 

@@ -1,4 +1,4 @@
-"""Every entry of the committed autotuner table (profiles/tune_r5.txt, the table
+"""Every entry of the committed autotuner table (profiles/tune_r6.txt, the table
 bench.py loads, so every bench / profiling run launches these kernels) at its
 exact shape: the entry's candidate forced (ARTSBIR_PGEMM_CFG / ARTSBIR_WGRAD_CFG),
 the kernel that ran asserted by name — a candidate that does not take its own
@@ -31,7 +31,7 @@ import _kernels
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TABLE = os.path.join(ROOT, "profiles", "tune_r5.txt")
+TABLE = os.path.join(ROOT, "profiles", "tune_r6.txt")
 BF = torch.bfloat16
 NSAMPLE = 48
 
