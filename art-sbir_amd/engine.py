@@ -96,6 +96,9 @@ SIDE_CONTIGUOUS = [False]  # measurement switch: those K CUs are mask bits 0..K-
 # only after that layer's data gradient has run on the main stream (instead of
 # beside it), so the two GEMMs of one layer never compete for the same CUs
 WGRAD_DEFER = [os.environ.get("ARTSBIR_WGRAD_DEFER", "")]
+# the stem conv's weight gradient on the main stream (ARTSBIR_STEM_WGRAD_MAIN=0:
+# on the side stream like the others)
+STEM_WGRAD_MAIN = os.environ.get("ARTSBIR_STEM_WGRAD_MAIN", "1") != "0"
 # measurement switch (never set in a real step): leave the weight gradients out
 SKIP_WGRAD = [False]
 _MASKED_STREAMS = {}
@@ -1351,7 +1354,14 @@ class Engine:
             da1 = self._dgrad(dy2, dw2, m.conv2, 1, y1.shape)
             self._wgrad_post(held)
             dy1, = self._bn_bwd(1, da1, [(y1, b1)], [m.bn1], ws, grads, mask_bn=b1)
-        self._wgrad(dy1, Act(x0), m.conv1, 2, 1, grads)
+        # the stem conv (models.py:310) has no data gradient, so the main stream
+        # has nothing left to do: its weight gradient runs there, beside the side
+        # stream's last ones, instead of queued behind them while main idles
+        # (0.6 ms at the end of the C2 step, profiles/r6_trace_gaps.txt)
+        if not STEM_WGRAD_MAIN:
+            self._wgrad(dy1, Act(x0), m.conv1, 2, 1, grads)
+        elif not SKIP_WGRAD[0]:
+            self._wgrad_sync(dy1, Act(x0), m.conv1, 2, 1, grads)
 
 
 class _Arena:
