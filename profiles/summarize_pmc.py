@@ -97,6 +97,8 @@ def short(name):
             return f"{k}<{t[0]},{t[1]},{t[2]}x{t[3]}{',bnb' if t[4] == 'true' else ''}>"
         if k == "sconv_kernel":
             return f"{k}<{t[0]},{t[1]}{',s2' if t[2] == '2' else ''}{fb}>"
+        if k == "rstream_kernel":  # <K, BK, TWO>
+            return f"{k}<bnb{',two' if len(t) > 2 and t[2] == 'true' else ''}>"
         return k
     return name.split("(")[0].replace("artsbir::", "").replace("void ", "")
 
