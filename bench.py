@@ -39,10 +39,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md; ~6.3 TB/s measu
 # files below were measured with it loaded, so a kernel name stands for the
 # same launches in both
 TUNE_CACHE = os.path.join(ROOT, "profiles", "tune_r6.txt")
-PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r5_pmc_traffic.json"))
+PMC_TRAFFIC = os.environ.get("ARTSBIR_PMC_TRAFFIC", os.path.join(ROOT, "profiles", "r6_pmc_traffic.json"))
 PMC_TRAFFIC_EMBED = os.environ.get("ARTSBIR_PMC_TRAFFIC_EMBED",
-                                   os.path.join(ROOT, "profiles", "r5_embed_pmc_traffic.json"))
-PMC_TRAFFIC_C5 = os.environ.get("ARTSBIR_PMC_TRAFFIC_C5", os.path.join(ROOT, "profiles", "r5_c5_pmc_traffic.json"))
+                                   os.path.join(ROOT, "profiles", "r6_embed_pmc_traffic.json"))
+PMC_TRAFFIC_C5 = os.environ.get("ARTSBIR_PMC_TRAFFIC_C5", os.path.join(ROOT, "profiles", "r6_c5_pmc_traffic.json"))
 
 
 def pmc_traffic(kernel, path=None):
