@@ -295,7 +295,10 @@ bool pw256_launch(PwArgs a, int level, hipStream_t st) {
   if (!a.dense && (a.C % 8 || a.R * a.S > 32 || (long long)a.Ho * a.Wo < PW_KS)) return false;
   const int ntiles = ((a.Cout + PW_BT - 1) / PW_BT) * ((a.K + PW_BT - 1) / PW_BT);
   const long long ksteps = (a.M + PW_KS - 1) / PW_KS;
-  const long long target = 256LL << level;
+  // ARTSBIR_PW256_SPLITX=f (measurement switch): f times the workgroups, each a
+  // 1/f share of the m reduction (shorter-lived workgroups beside the main stream)
+  static const int splitx = getenv("ARTSBIR_PW256_SPLITX") ? atoi(getenv("ARTSBIR_PW256_SPLITX")) : 1;
+  const long long target = (256LL << level) * (splitx > 1 ? splitx : 1);
   long long splits = target / ntiles;
   if (splits < 1) splits = 1;
   long long per = (ksteps + splits - 1) / splits;

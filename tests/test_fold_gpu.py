@@ -95,11 +95,17 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16], ids=["f32", "bf16"])
-def test_fold_prep_matches_formula(dtype, dev):
-    case = (2, 3, 8, 8, 256, 64)
+@pytest.mark.parametrize("Co,Ci", [(256, 64), (1024, 256), (2048, 512)])
+def test_fold_prep_matches_formula(Co, Ci, dtype, dev):
+    """the folded weights [diag(c1) W | W^T diag(b') W] and bias k W per segment;
+    the layer-3/4 shapes run the split-K form of the small GEMM (its fixed-order
+    reduction: a second call gives the same bits)"""
+    case = (2, 3, 8, 8, Co, Ci)
     G = case[1]
     gr, x, w, coef, prm, y = _problem(case, 1, dtype)
     wout, bias, _ = _prep(w, coef, prm, G, dtype, dev)
+    wout2, bias2, _ = _prep(w, coef, prm, G, dtype, dev)
+    assert torch.equal(wout, wout2) and torch.equal(bias, bias2)
     c = coef.double()
     mean, istd = prm[:, 0].double(), prm[:, 1].double()
     bp = -c[:, 0] * c[:, 2] * istd                         # [G][Co]
@@ -109,8 +115,8 @@ def test_fold_prep_matches_formula(dtype, dev):
     refb = torch.einsum("ci,gc->gi", w, k)
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     out = wout.double().cpu()
-    assert _rel(out[:, :, :256], ref1) < tol
-    assert _rel(out[:, :, 256:], ref2) < tol
+    assert _rel(out[:, :, :Co], ref1) < tol
+    assert _rel(out[:, :, Co:], ref2) < tol
     assert _rel(bias.double().cpu(), refb) < 1e-5
 
 
