@@ -583,8 +583,11 @@ __device__ __forceinline__ void epi_prefetch(const PgArgs& a, EpiRegs<MTC / 2, N
 // is added to the accumulators first, before any mask / BN-backward reduction.
 // FBL: that bias loaded per use (L1-resident) instead of held in 8 VGPRs across
 // the pair's pixel tiles (the 8-wave 256 x 128 tile's 128-VGPR budget)
+// PFN (BK 0, global residual / gate operand, one operand batch per channel pair):
+// the next pair's operand loads are issued before this pair's arithmetic and
+// stores, so a wave waits out one load round trip per tile instead of one per pair
 template <int BK, bool TWO, bool S_RES, bool S_Y1, bool S_MK, int BCH, int MTC, int NTP, int WTPX, int WTCH,
-          bool REG = false, int EJB = 2, bool GLB = false, bool FB = false, bool FBL = false>
+          bool REG = false, int EJB = 2, bool GLB = false, bool FB = false, bool FBL = false, bool PFN = false>
 __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc)[MTC][NTP], long long bpx, int bch,
                                               int wpx, int wch, int fr, int fq, float* red, const EpiStage& sg,
                                               const EpiRegs<MTC / 2, NTP>* er = nullptr) {
@@ -597,6 +600,29 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
   const bool sums = BNB || a.stats != nullptr;
   const bool res = RESK || (BK == 0 && a.res_mode != 0);
   const float rsc = a.res_mode == 2 ? 0.25f : 1.f;
+  static_assert(!PFN || (BK == 0 && !REG && EJB >= NTP), "PFN: plain epilogue, one batch per pair");
+  // PFN: the residual / gate operand rows of pair pp (the loads of the u loop below)
+  auto pfn_load = [&](int pp, Vec16<bf16> (&dst)[NTP]) {
+    const int c0 = bch + wch * WTCH + 32 * pp + 8 * fq;
+    const int cc = c0 < a.Cout ? c0 : 0;
+#pragma unroll
+    for (int u = 0; u < NTP; ++u) {
+      const long long px = wpx0 + u * 16 + fr;
+      const long long pc = px < a.M ? px : a.M - 1;
+      long long ri = pc;
+      if (a.res_mode == 2) {
+        const long long img = pc / HoWo;
+        const int rem = (int)(pc - img * HoWo);
+        const int oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+        ri = (img * (a.Ho / 2) + oh / 2) * (a.Wo / 2) + ow / 2;
+      }
+      dst[u] = ld16<bf16>(reinterpret_cast<const bf16*>(a.res) + ri * a.ldy + cc);
+    }
+  };
+  Vec16<bf16> pfn_next[PFN ? NTP : 1];
+  if constexpr (PFN) {
+    if (res) pfn_load(0, pfn_next);
+  }
 #pragma unroll
   for (int p = 0; p < MTC / 2; ++p) {
     const int ch0 = bch + wch * WTCH + 32 * p + 8 * fq;
@@ -636,8 +662,16 @@ __device__ __forceinline__ void pg_epilogue_k(const PgArgs& a, const f32x4 (&acc
       const int j0 = (GLB && PG_SNAKE && (p & 1)) ? NTP - EJ - jj : jj;
       Vec16<bf16> rv[EJ], y0v[EJ], mkv[EJ], y1v[EJ];
       unsigned mbits[EJ];
+      if constexpr (PFN) {
+        if (res) {
+#pragma unroll
+          for (int u = 0; u < EJ; ++u) rv[u] = pfn_next[u];
+          if (p + 1 < MTC / 2) pfn_load(p + 1, pfn_next);
+        }
+      }
 #pragma unroll
       for (int u = 0; u < EJ; ++u) {  // operands of the batch (global loads issued together)
+        if constexpr (PFN) continue;  // taken above
         if constexpr (REG) {  // prefetched before the main loop (epi_prefetch)
           rv[u] = er->rv[p][j0 + u];
           y0v[u] = er->y0v[p][j0 + u];

@@ -240,6 +240,12 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
   unsigned nol_m = (unsigned)lane * 0x9e3779b9u;
   asm volatile("" : "+v"(nol_m));  // opaque per-lane row-validity bits
 #endif
+#ifndef PP_PFN
+#define PP_PFN 1  // BK 0: the next channel pair's residual / gate operands loaded ahead (pg_epilogue_k PFN)
+#endif
+  // (loading pair 0's operands in the last K-tiles as well, under the tail's
+  // counted waits, was slower: gate GEMM 2.45 -> 2.58 ms, profiles/r6_pfn.txt)
+  constexpr bool PFN = PP_PFN && BK == 0 && !X2 && !TAPS;  // (3x3 convs: no residual operand)
   // one K-tile in buffer SL (compile-time: every LDS offset an immediate)
   auto ktile = [&](int s, auto slc) {
     constexpr int SL = decltype(slc)::value;
@@ -320,8 +326,8 @@ __global__ void __launch_bounds__(512, 1) pp256_kernel(PgArgs a) {
 #ifndef PP_EJB
 #define PP_EJB 4  // pixel tiles whose epilogue operands are loaded together (2: 1-4 % slower fused dgrads, tools/gpu/r4_ej.sh)
 #endif
-  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, PP_EJB, true, X2>(a, acc, bpx, bch, wpx,
-                                                                                                wch, fr, fq, red, sgg);
+  pg_epilogue_k<BK, TWO, false, false, false, BCH, MTC, NTP, WTPX, WTCH, false, PP_EJB, true, X2, false, PFN>(
+      a, acc, bpx, bch, wpx, wch, fr, fq, red, sgg);
   if (sums) stats_flush<BCH>(red, red_cnt, NW - 1, a, bch, (int)(blockIdx.x % ARTSBIR_NSLOT), lane, bpx, PP_BPX);
 }
 

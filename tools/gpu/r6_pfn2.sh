@@ -1,0 +1,24 @@
+#!/bin/bash
+# round 6: pp256's next-pair residual / gate operand prefetch (pg_epilogue_k PFN)
+# vs without (build_ab/libartsbir_nopfn.so): tests, gate_bench A/B, C5 / C2 step A/B
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+OLD=$R/art-sbir_amd/build_ab/libartsbir_nopfn.so
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_vit_block.py tests/test_c5_gpu.py \
+  tests/test_pgemm_gpu.py tests/test_fused_gpu.py -k "not (test_pgemm_gpu and not 22) and not (test_fused_gpu and not 22)" \
+  > gpurun_out/r6_pfn2_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r6_pfn2_tests.log; exit 1; }
+tail -2 gpurun_out/r6_pfn2_tests.log
+for i in 1 2; do
+  echo "gate new"; timeout -k 10 120 python -u tools/gate_bench.py 2>&1 | grep run || exit 1
+  echo "gate old"; ARTSBIR_LIB=$OLD timeout -k 10 120 python -u tools/gate_bench.py 2>&1 | grep run || exit 1
+done
+C5="--no-cpu-baseline --no-embed --no-retrieval --no-preprocess --no-loss-check --no-profile --steps 5 --warmup 2"
+for i in 1 2 3; do
+  for v in new old; do
+    if [ $v = old ]; then E="ARTSBIR_LIB=$OLD"; else E=""; fi
+    env $E timeout -k 10 300 python -u bench.py $C5 > gpurun_out/r6_pfn2_$v.log 2>&1 || { echo RUN_FAILED; tail -5 gpurun_out/r6_pfn2_$v.log; exit 1; }
+    tail -1 gpurun_out/r6_pfn2_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', 'C2', d['ms_per_step'], 'C5', d['c5']['ms_per_step'], d['c5']['value'])"
+  done
+done
