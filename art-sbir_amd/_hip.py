@@ -154,6 +154,7 @@ SIGNATURES = {
                                     _vp],
     "artsbir_bn_bwd_reduce": [_PB, _vp],
     "artsbir_set_deterministic": [_c_int],
+    "artsbir_set_wgrad_cus": [_c_int],
     "artsbir_bn_bwd_finalize": [_vp, _c_int, ctypes.c_double, _vp, _vp, _vp, _vp, _vp, _vp],
     "artsbir_bn_bwd_apply": [_PB, _vp],
     "artsbir_colsum": [_c_int, _vp, _c_ll, _c_ll, _c_ll, _vp, _vp],

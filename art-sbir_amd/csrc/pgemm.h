@@ -93,6 +93,8 @@ bool pwgrad_launch(PwArgs a, int c, hipStream_t st);
 // wgrad candidates 100 + level (pw256.hip): the ping-pong 256 x 256 weight-gradient
 // tile, m-split over 256 << level workgroups; false outside its range
 bool pw256_launch(PwArgs a, int level, hipStream_t st);
+// CUs the weight-gradient grids are sized for (artsbir_set_wgrad_cus; 256 by default)
+extern int g_wgrad_cus;
 int pwgrad_num_cfgs();
 int pwgrad_level(int c);
 

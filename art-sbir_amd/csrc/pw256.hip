@@ -298,7 +298,7 @@ bool pw256_launch(PwArgs a, int level, hipStream_t st) {
   // ARTSBIR_PW256_SPLITX=f (measurement switch): f times the workgroups, each a
   // 1/f share of the m reduction (shorter-lived workgroups beside the main stream)
   static const int splitx = getenv("ARTSBIR_PW256_SPLITX") ? atoi(getenv("ARTSBIR_PW256_SPLITX")) : 1;
-  const long long target = (256LL << level) * (splitx > 1 ? splitx : 1);
+  const long long target = ((long long)g_wgrad_cus << level) * (splitx > 1 ? splitx : 1);
   long long splits = target / ntiles;
   if (splits < 1) splits = 1;
   long long per = (ksteps + splits - 1) / splits;

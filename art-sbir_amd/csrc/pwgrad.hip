@@ -522,7 +522,7 @@ static void hwgrad_go(const PwArgs& a, hipStream_t st) {
   int per_cu = (160 * 1024) / (2 * Gm::STAGE);
   if (per_cu > 2) per_cu = 2;
   // pixel-tile groups: fill the chip once, a multiple of 8 (one XCD per group)
-  int groups = (256 * per_cu / npc) / 8 * 8;
+  int groups = (g_wgrad_cus * per_cu / npc) / 8 * 8;
   if (groups < 8) groups = 8;
   const int need = (ntiles + 7) / 8 * 8;
   if (groups > need) groups = need;
@@ -633,7 +633,8 @@ static void pw_launch_c(int c, const PwArgs& a, long long blocks, hipStream_t st
 // wgrad at 1536 workgroups).  The split count rounds DOWN to the target, so a
 // 256 / 512 target fills whole rounds of the 256 CUs (one workgroup per CU)
 // instead of leaving a tail round of a few workgroups.
-static const int kSplitTarget[] = {1536, 768, 512, 256};
+static const int kSplitTarget[] = {1536, 768, 512, 256};  // for 256 CUs (scaled by g_wgrad_cus)
+int g_wgrad_cus = 256;
 static const int kSplitMinSteps[] = {8, 16, 24, 64};
 constexpr int kNumLevels = 4;
 
@@ -660,7 +661,8 @@ bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
   if (g.bkk > 128 && a.K <= g.bkk / 2) return false;
   const long long ntiles = (long long)((a.Cout + g.bco - 1) / g.bco) * ((a.K + g.bkk - 1) / g.bkk);
   const long long ksteps = (a.M + 63) / 64;
-  long long splits = kSplitTarget[level] >= ntiles ? kSplitTarget[level] / ntiles : 1;
+  const long long target = (long long)kSplitTarget[level] * g_wgrad_cus / 256;
+  long long splits = target >= ntiles ? target / ntiles : 1;
   const long long max_splits = (ksteps + kSplitMinSteps[level] - 1) / kSplitMinSteps[level];
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -696,3 +698,12 @@ bool pwgrad_launch(PwArgs a, int cand, hipStream_t st) {
 }
 
 }  // namespace artsbir
+
+// the weight-gradient grids (split-K targets, persistent halo groups) sized for
+// n CUs: the engine's side stream restricted by a CU mask (ARTSBIR_SIDE_CUS);
+// returns the previous value
+extern "C" int artsbir_set_wgrad_cus(int n) {
+  const int old = artsbir::g_wgrad_cus;
+  if (n >= 8 && n <= 4096) artsbir::g_wgrad_cus = n;
+  return old;
+}

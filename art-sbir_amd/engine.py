@@ -930,6 +930,8 @@ class Engine:
                 st = self._side = cu_masked_stream(device, SIDE_CUS[0], contiguous=SIDE_CONTIGUOUS[0])
             else:
                 st = self._side = torch.cuda.Stream(device=device)
+            # the weight-gradient grids fill the side stream's CUs in whole rounds
+            _hip.lib().artsbir_set_wgrad_cus(SIDE_CUS[0] if SIDE_CUS[0] > 0 else 256)
             self._side_cus = want
         return st
 

@@ -308,6 +308,9 @@ int artsbir_bn_bwd_reduce(const artsbir_bn_bwd_desc* d, void* stream);
  * of f32 atomics.  Pair with artsbir_bn_stats_det for the forward statistics and
  * the unfused data gradients.  Returns the previous setting. */
 int artsbir_set_deterministic(int on);
+/* Size the weight-gradient grids (split-K targets, persistent groups) for n CUs (default 256;
+ * the engine's CU-masked side stream).  Returns the previous value. */
+int artsbir_set_wgrad_cus(int n);
 /* dgamma += sum g*xhat, dbeta += sum g; coef = [gamma*istd, sum g/cnt, sum g*xhat/cnt]. */
 int artsbir_bn_bwd_finalize(const float* slots, int C, double count, const float* gamma, const float* istd,
                             float* dgamma, float* dbeta, float* coef, void* stream);
