@@ -587,6 +587,7 @@ struct V2 {
   static constexpr int LDS = NST * STAGE + STG + 5 * ROWS * 4;
   static_assert(LDS <= 163840, "LDS");
   static_assert((NI + V2_WAVES - 1) / V2_WAVES <= 5, "rvm_wait_n covers at most 5 DMA per wave");
+  static_assert((NI + V2_WAVES / 2 - 1) / (V2_WAVES / 2) <= 10, "rvm_wait_n covers at most 10 DMA per wave");
 };
 
 // scan statistics (diagnostics, ARTSBIR_KNN_STAT=1): wave-tiles, slow-path
@@ -598,9 +599,16 @@ static bool knn_stat_on() {
   return on;
 }
 
-template <int KB>
-__global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int stat) {
+// QH: query halves per wave.  1: 8 waves of 32 queries (two waves per SIMD);
+// 2: 4 waves of 64 (one wave per SIMD, the A fragments of both halves resident:
+// 2 KB registers per lane at D = 512, AGPRs included), so each B fragment read
+// from LDS feeds two MFMAs — half the LDS reads per MAC — and every lane owns a
+// query row in the list / slow path (ARTSBIR_KNN_QH, knn_qh())
+template <int KB, int QH = 1>
+__global__ void __launch_bounds__(64 * V2_WAVES / QH, 1) knn_scan_v2_kernel(KnnScanArgs a, int stat) {
   using C = V2<KB>;
+  constexpr int NWV = V2_WAVES / QH;  // waves of the workgroup
+  static_assert(QH == 1 || (QH == 2 && C::SROWS == 32), "QH 2: the 3-stage ring (full-tile staging)");
   __shared__ __attribute__((aligned(16))) char smem[C::LDS];
   float* s_stage = reinterpret_cast<float*>(smem + C::NST * C::STAGE);
   float* s_thr = s_stage + V2_WAVES * C::WSTG;     // [256] 16th smallest so far (-INF: row unused)
@@ -636,12 +644,12 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
 #ifndef KNN_ROT
 #define KNN_ROT 1
 #endif
-  auto w_of = [&](int t) { return KNN_ROT ? (wid + t) & (V2_WAVES - 1) : wid; };
-  auto ni_of = [&](int t) { const int w2 = w_of(t); return w2 < C::NI ? (C::NI - w2 + V2_WAVES - 1) / V2_WAVES : 0; };
+  auto w_of = [&](int t) { return KNN_ROT ? (wid + t) & (NWV - 1) : wid; };
+  auto ni_of = [&](int t) { const int w2 = w_of(t); return w2 < C::NI ? (C::NI - w2 + NWV - 1) / NWV : 0; };
   auto issue_tile = [&](int t) {
     char* st = smem + (t % C::NST) * C::STAGE;
     const unsigned gb = (unsigned)(t * V2_ROWS * C::RB);
-    for (int i = w_of(t); i < C::NI; i += V2_WAVES) rdma16(gr, st + i * 1024, gb + (unsigned)((i * 64 + lane) * 16));
+    for (int i = w_of(t); i < C::NI; i += NWV) rdma16(gr, st + i * 1024, gb + (unsigned)((i * 64 + lane) * 16));
   };
   issue_tile(0);
   if (ntiles > 1) issue_tile(1);
@@ -663,14 +671,19 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   const int r32 = lane & 31, h = lane >> 5;
   const __amdgpu_buffer_rsrc_t qr = rrsrc(reinterpret_cast<const bf16*>(a.q) + (long long)qb * (16 * KB),
                                           (long long)(a.Nq - qb) * (32 * KB));
-  uint4 af[KB];
+  uint4 af[QH][KB];
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb)
-    af[kb] = rload(qr, (unsigned)(((wid * 32 + r32) * 16 * KB + kb * 16 + 8 * h) * 2));
-  // owner state: lane r < 32 owns row r of the wave (its e and half in the accumulator)
+  for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+      af[qh][kb] = rload(qr, (unsigned)(((wid * 32 * QH + qh * 32 + r32) * 16 * KB + kb * 16 + 8 * h) * 2));
+  // owner state: lane r < 32 owns row r of the wave (QH 2: lane l owns row l,
+  // half l >> 5), with its e and accumulator half in the 32x32 accumulator
+  const bool owner = QH == 2 || lane < 32;
+  const int ohalf = QH == 2 ? lane >> 5 : 0;
   const int orow = lane & 31;
   const int oe = (orow & 3) + 4 * (orow >> 3), oh = (orow >> 2) & 1;
-  const int R_own = wid * 32 + orow;
+  const int R_own = wid * 32 * QH + ohalf * 32 + orow;
   float lst_d[KT];
   int lst_i[KT];
 #pragma unroll
@@ -681,24 +694,29 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
   // so that the compiler's vmcnt tracking does not wait on (our hand-counted
   // DMAs behind) their loads inside the tile loop
 #pragma unroll
-  for (int kb = 0; kb < KB; ++kb) asm volatile("" : "+v"(af[kb].x), "+v"(af[kb].y), "+v"(af[kb].z), "+v"(af[kb].w));
+  for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+    for (int kb = 0; kb < KB; ++kb)
+      asm volatile("" : "+v"(af[qh][kb].x), "+v"(af[qh][kb].y), "+v"(af[qh][kb].z), "+v"(af[qh][kb].w));
   __syncthreads();
   // prefilter: t = |g|^2 - 2 q.g <= crit - |q|^2 + slack, a superset of
   // d2 = (|q|^2 + |g|^2) - 2 q.g <= crit whatever the rounding of either form
   // (every magnitude is <= 2 (|q|^2 + gsq_max), each rounding <= 2^-24 of it)
   const float gmax = a.gsq_max_p ? *a.gsq_max_p : a.gsq_max;
-  float critp[16];
+  float critp[QH][16];
   auto load_crit = [&]() {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int R = wid * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      const float qs = s_qsq[R];
-      critp[e] = (s_crit[R] - qs) + 0x1p-18f * (qs + gmax);
-    }
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int R = wid * 32 * QH + qh * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const float qs = s_qsq[R];
+        critp[qh][e] = (s_crit[R] - qs) + 0x1p-18f * (qs + gmax);
+      }
   };
   load_crit();
-  float* stg = s_stage + wid * C::WSTG;
-  float* sg = stg + (C::SROWS == 32 ? 32 : C::SROWS * C::SP);  // column c's |g|^2 at sg[c * gstr]
+  float* stg0 = s_stage + wid * QH * C::WSTG;  // half qh's staging at stg0 + qh * WSTG
+  float* sg = stg0 + (C::SROWS == 32 ? 32 : C::SROWS * C::SP);  // column c's |g|^2 at sg[c * gstr]
   constexpr int gstr = C::SROWS == 32 ? C::SP : 1;
   const int q_own = qb + R_own;
   const float eps_own = q_own < a.Nq ? a.rel * sqrtf(a.qsq[q_own] * gmax) * 1.001f + 1e-3f : 0.f;
@@ -722,7 +740,9 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
 #define KNN_PF 4
 #endif
     constexpr int PF = KB < KNN_PF ? KB : KNN_PF;
-    f32x16 acc = {};
+    f32x16 acc[QH];
+#pragma unroll
+    for (int qh = 0; qh < QH; ++qh) acc[qh] = f32x16{};
     uint4 bq[KB];
 #ifndef KNN_ABL
 #define KNN_ABL 0  // timing ablations of a diagnostic build only (1: no list work, 2: no MFMAs; tools/gpu/r4_knn_abl.sh)
@@ -732,13 +752,29 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
 #pragma unroll
     for (int kb = 0; kb < KB; ++kb) {
       if (kb + PF < KB) bq[kb + PF] = *reinterpret_cast<const uint4*>(bp + (kb + PF) * 32);
-      if (KNN_ABL & 2)
-        acc[kb & 15] += __uint_as_float(bq[kb].x & 0x80000000u);
-      else
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[kb]),
-                                                      *reinterpret_cast<const bf16x8*>(&bq[kb]), acc, 0, 0, 0);
+#pragma unroll
+      for (int qh = 0; qh < QH; ++qh) {
+        if (KNN_ABL & 2)
+          acc[qh][kb & 15] += __uint_as_float(bq[kb].x & 0x80000000u);
+        else if (QH == 2) {
+          // the A fragments stay in AGPRs (the MFMA reads them there; the builtin
+          // had the compiler copy each one to VGPRs first: 244 v_accvgpr_read
+          // per tile); acc in VGPRs for the prefilter
+          typedef unsigned kv_u4 __attribute__((ext_vector_type(4)));
+          const kv_u4 av = __builtin_bit_cast(kv_u4, af[qh][kb]), bv = __builtin_bit_cast(kv_u4, bq[kb]);
+          if (kb == 0)
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=v"(acc[qh]) : "a"(av), "v"(bv));
+          else
+            asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc[qh]) : "a"(av), "v"(bv));
+        } else
+          acc[qh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(&af[qh][kb]),
+                                                            *reinterpret_cast<const bf16x8*>(&bq[kb]), acc[qh], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
+    // the hand-issued MFMAs' results are read by vector instructions next: the
+    // 16-pass XDL write -> VALU read hazard (18 wait states) the compiler cannot see
+    if (QH == 2 && !(KNN_ABL & 2)) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
     const int bn = g0 + t * V2_ROWS;
     const bool cvalid = bn + r32 < a.Ng;
     const float gsq = cvalid ? *reinterpret_cast<const float*>(st + r32 * C::RB + 32 * KB) : INFINITY;
@@ -763,7 +799,9 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
     __syncthreads();
     bool any = false;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[e], gsq) <= critp[e];
+    for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) any |= fmaf(-2.f, acc[qh][e], gsq) <= critp[qh][e];
     if (KNN_ABL & 1) {
       st_entries += __builtin_amdgcn_ballot_w64(any) ? 1u : 0u;
       any = false;
@@ -776,13 +814,18 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
       unsigned mymask = 0;
       if (lane < 32) sg[r32 * gstr] = gsq;  // column r32's |g|^2 (INF past Ng)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(fmaf(-2.f, acc[e], gsq) <= critp[e]);
-        if (m) {
-          if (C::SROWS == 32) stg[((e & 3) + 8 * (e >> 2) + 4 * h) * C::SP + r32] = acc[e];
-          if (oe == e) mymask = oh ? (unsigned)(m >> 32) : (unsigned)m;
+      for (int qh = 0; qh < QH; ++qh) {
+        float* stg = stg0 + qh * C::WSTG;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const unsigned long long m = __builtin_amdgcn_ballot_w64(fmaf(-2.f, acc[qh][e], gsq) <= critp[qh][e]);
+          if (m) {
+            if (C::SROWS == 32) stg[((e & 3) + 8 * (e >> 2) + 4 * h) * C::SP + r32] = acc[qh][e];
+            if (oe == e && ohalf == qh) mymask = oh ? (unsigned)(m >> 32) : (unsigned)m;
+          }
         }
       }
+      float* stg = stg0 + ohalf * C::WSTG;  // the owner's half
       bool changed = false;
       // every lane reads its (owner) row's state: lanes >= 32 mirror row lane - 32
       const float qs = s_qsq[R_own], hi = s_hi[R_own];
@@ -798,12 +841,12 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
         }
         if (h == hp) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) stg[((e & 3) + 4 * (e >> 2)) * C::SP + r32] = acc[e];
+          for (int e = 0; e < 16; ++e) stg[((e & 3) + 4 * (e >> 2)) * C::SP + r32] = acc[0][e];
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      if (lane < 32 && mymask && (C::SROWS == 32 || oh == hp)) {
+      if (owner && mymask && (C::SROWS == 32 || oh == hp)) {
         const float lo = s_lo[R_own];
         const float* srow = stg + (C::SROWS == 32 ? orow : oe) * C::SP;
         while (mymask) {
@@ -855,12 +898,14 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
         // (padding rows q >= Nq keep -INF, as load_crit() reads them)
         const float mine = q_own < a.Nq ? (fmaxf(thr, hi) - qs) + 0x1p-18f * (qs + gmax) : -INFINITY;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int r0 = (e & 3) + 8 * (e >> 2);
-          const float n0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), r0));
-          const float n1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), r0 + 4));
-          critp[e] = h ? n1 : n0;
-        }
+        for (int qh = 0; qh < QH; ++qh)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int r0 = qh * 32 + (e & 3) + 8 * (e >> 2);
+            const float n0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), r0));
+            const float n1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), r0 + 4));
+            critp[qh][e] = h ? n1 : n0;
+          }
       }
     }
     if (a.kb && (((t & (KB_SYNC - 1)) == KB_SYNC - 1) || t + 1 == ntiles)) {
@@ -875,7 +920,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
       // the global top k (kb_bound above).
       rvm_wait<0>();
       bool upd = false, pub = false;
-      if (lane < 32 && q_own < a.Nq) {
+      if (owner && q_own < a.Nq) {
         float kth = INFINITY;
 #pragma unroll
         for (int i = 0; i < KT; ++i) kth = (i == a.kq - 1 && lst_i[i] >= 0) ? lst_d[i] : kth;
@@ -938,7 +983,7 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
       atomicAdd(&g_knn_stat[2], (unsigned long long)ins);
     }
   }
-  if (lane < 32) {
+  if (owner) {
     const int q = qb + R_own;
     if (q < a.Nq) {
       if (mycnt) atomicAdd(a.cnt + q, mycnt);
@@ -949,6 +994,26 @@ __global__ void __launch_bounds__(512, 1) knn_scan_v2_kernel(KnnScanArgs a, int 
         a.cand_i[o + i] = lst_i[i];
       }
     }
+  }
+}
+
+// queries per wave of the v2 scan: ARTSBIR_KNN_QH=2 (64, one wave per SIMD) or 1 (32)
+static int knn_qh() {
+  static const int qh = [] { const char* e = getenv("ARTSBIR_KNN_QH"); return e && atoi(e) == 2 ? 2 : 1; }();
+  return qh;
+}
+
+static void knn_scan_v2_launch(int Dp, unsigned grid, const KnnScanArgs& a, int stat, hipStream_t st) {
+  const dim3 g(grid);
+  if (knn_qh() == 2 && Dp == 512) {  // the register budget of two halves is sized for D = 512
+    hipLaunchKernelGGL((knn_scan_v2_kernel<32, 2>), g, dim3(256), 0, st, a, stat);
+    return;
+  }
+  switch (Dp) {
+    case 64: hipLaunchKernelGGL((knn_scan_v2_kernel<4, 1>), g, dim3(512), 0, st, a, stat); break;
+    case 128: hipLaunchKernelGGL((knn_scan_v2_kernel<8, 1>), g, dim3(512), 0, st, a, stat); break;
+    case 256: hipLaunchKernelGGL((knn_scan_v2_kernel<16, 1>), g, dim3(512), 0, st, a, stat); break;
+    default: hipLaunchKernelGGL((knn_scan_v2_kernel<32, 1>), g, dim3(512), 0, st, a, stat); break;
   }
 }
 
@@ -1722,13 +1787,7 @@ extern "C" int artsbir_knn_scan_aug(const void* qc, const void* ga, const float*
   a.nchunks = (tiles + tiles_per_chunk - 1) / tiles_per_chunk;
   a.lo = lo; a.hi = hi; a.cnt = cnt; a.unc = unc; a.unc_cap = unc_cap; a.cand_d = cand_d; a.cand_i = cand_i;
   const unsigned grid = (unsigned)(a.nchunks * ((nq + 255) / 256));
-  hipStream_t s = (hipStream_t)stream;
-  switch (Dp) {
-    case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, s, a, 0); break;
-    case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, s, a, 0); break;
-    case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, s, a, 0); break;
-    default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, s, a, 0); break;
-  }
+  knn_scan_v2_launch(Dp, grid, a, 0, (hipStream_t)stream);
   ARTSBIR_CHECK_LAUNCH("knn_scan_aug");
   return 0;
 }
@@ -1942,12 +2001,7 @@ extern "C" int artsbir_pairwise_l2_topk(int dtype, int metric, const float* q, i
   if (p.v2) {
     const unsigned grid = (unsigned)(p.nchunks * ((Q + 255) / 256));
     const int sstat = knn_stat_on() ? 1 : 0;
-    switch (p.Dp) {
-      case 64: hipLaunchKernelGGL(knn_scan_v2_kernel<4>, dim3(grid), dim3(512), 0, st, a, sstat); break;
-      case 128: hipLaunchKernelGGL(knn_scan_v2_kernel<8>, dim3(grid), dim3(512), 0, st, a, sstat); break;
-      case 256: hipLaunchKernelGGL(knn_scan_v2_kernel<16>, dim3(grid), dim3(512), 0, st, a, sstat); break;
-      default: hipLaunchKernelGGL(knn_scan_v2_kernel<32>, dim3(grid), dim3(512), 0, st, a, sstat); break;
-    }
+    knn_scan_v2_launch(p.Dp, grid, a, sstat, st);
     set_last_kernel("knn_scan_v2_kernel");
   } else {
     // knn_scan_kernel's chunks are tiles_per_chunk x 128 rows as well
