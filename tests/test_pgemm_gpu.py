@@ -182,6 +182,44 @@ def test_wgrad_accumulates(case, cfg, dev):
             os.environ["ARTSBIR_WGRAD_CFG"] = old
 
 
+@pytest.mark.parametrize("cus", [96, 224])
+@pytest.mark.parametrize("cfg", ["0", "9", "34", "38", "100", "101"])
+@pytest.mark.parametrize("case", [WG_CASES[3], WG_CASES[5], WG_CASES[-1]])
+def test_wgrad_grids_sized_for_fewer_cus(case, cfg, cus, dev):
+    """artsbir_set_wgrad_cus (the grids of a CU-masked weight-gradient stream):
+    the split-K targets and the halo kernel's persistent groups scale with the
+    CU count, the result does not change"""
+    lib = _hip.lib()
+    old_env = os.environ.get("ARTSBIR_WGRAD_CFG")
+    os.environ["ARTSBIR_WGRAD_CFG"] = cfg
+    old = lib.artsbir_set_wgrad_cus(cus)
+    try:
+        N, H, W, C, Co, R, S, st, pd = case
+        g = torch.Generator().manual_seed(5)
+        x = torch.randn(N, C, H, W, generator=g).bfloat16().float()
+        w = torch.randn(Co, C, R, S, generator=g)
+        Ho = (H + 2 * pd - R) // st + 1
+        Wo = (W + 2 * pd - S) // st + 1
+        dy = torch.randn(N, Co, Ho, Wo, generator=g).bfloat16().float()
+        wr = w.clone().requires_grad_(True)
+        F.conv2d(x, wr, stride=st, padding=pd).backward(dy)
+        ref = wr.grad.permute(0, 2, 3, 1)
+        dw = torch.zeros(Co, R, S, C, device=dev)
+        d = _hip.conv_desc(torch.bfloat16, N, H, W, C, Co, R, S, st, pd)
+        dyd, xd = _nhwc(dy).to(dev, torch.bfloat16), _nhwc(x).to(dev, torch.bfloat16)
+        _hip.call("artsbir_conv2d_wgrad", d, dyd.data_ptr(), xd.data_ptr(), None, None, 0, dw.data_ptr(),
+                  _hip.stream())
+        torch.cuda.synchronize()
+        _kernels.require(cfg, wgrad=True)
+        assert torch.allclose(dw.cpu(), ref, atol=2e-2, rtol=1e-3), (dw.cpu() - ref).abs().max()
+    finally:
+        lib.artsbir_set_wgrad_cus(old)
+        if old_env is None:
+            os.environ.pop("ARTSBIR_WGRAD_CFG", None)
+        else:
+            os.environ["ARTSBIR_WGRAD_CFG"] = old_env
+
+
 @pytest.mark.parametrize("cfg", ["-1", "0", "1", "2", "3", "6", "7", "8"])
 @pytest.mark.parametrize("M,N,K,ldd,ldx", [(100, 96, 64, 96, 64), (3000, 512, 2048, 512, 2048), (77, 40, 24, 48, 32)])
 def test_gemm_tn_strided(M, N, K, ldd, ldx, cfg, dev):
