@@ -572,10 +572,12 @@ __device__ __forceinline__ void bnb_seg(BnBwdArgs& a) {
 // after the ReLU: the quad's pooled gradient d is read once and spread over its
 // four pixels.  Each thread owns one 8-channel group for the whole kernel, so
 // per-channel parameters are loaded once; no per-element index division.
+// yk (KIND 1): the BN inputs y_0 the mask was computed from, handed back so the
+// caller's target-0 pass does not load them a second time
 template <typename T, int KIND, int POOL>
 __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, long long (&offs)[POOL * POOL],
                                           float (&g)[POOL * POOL][8], const float (&mm)[8], const float (&ms)[8],
-                                          const float (&mh)[8]) {
+                                          const float (&mh)[8], float (*yk)[8] = nullptr) {
   if constexpr (POOL == 1) {
     offs[0] = (long long)u * a.C + cg * 8;
   } else {
@@ -613,6 +615,10 @@ __device__ __forceinline__ void bnb_unit_g(const BnBwdArgs& a, int u, int cg, lo
       load8<T>(reinterpret_cast<const T*>(a.y[0]) + offs[q], y);
 #pragma unroll
       for (int e = 0; e < 8; ++e) g[q][e] = ((y[e] - mm[e]) * ms[e] + mh[e]) > 0.f ? dv[e] * inv : 0.f;
+      if (yk) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) yk[q][e] = y[e];
+      }
     }
   }
 }
@@ -642,8 +648,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
     if constexpr (KIND == 1) load_bn8(a.mbn, a.C, cg * 8, mm, ms, mh);
     for (int u = u0 + rl; u < u1; u += RL) {
       long long offs[NQ];
-      float g[NQ][8];
-      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, mm, ms, mh);
+      float g[NQ][8], yk[NQ][8];
+      bnb_unit_g<T, KIND, POOL>(a, u, cg, offs, g, mm, ms, mh, KIND == 1 ? yk : nullptr);
       if constexpr (POOL == 1) {  // g written back (in place over d allowed)
         if (a.gout) store8<T>(reinterpret_cast<T*>(a.gout) + offs[0], g[0]);
       }
@@ -652,7 +658,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, int uni
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
           float y[8];
-          load8<T>(reinterpret_cast<const T*>(a.y[t]) + offs[q], y);
+          if (KIND == 1 && t == 0) {  // the mask's y_0, loaded once
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[e] = yk[q][e];
+          } else {
+            load8<T>(reinterpret_cast<const T*>(a.y[t]) + offs[q], y);
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             acc[t][0][e] += g[q][e];
@@ -800,12 +811,15 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, int unit
         offs[i][0] = (long long)u * a.C + cg * 8;
         load8_last<T>(reinterpret_cast<const T*>(a.d) + offs[i][0], g[i][0]);
       } else {
-        bnb_unit_g<T, KIND, POOL>(a, u, cg, offs[i], g[i], mm, ms, mh);
+        bnb_unit_g<T, KIND, POOL>(a, u, cg, offs[i], g[i], mm, ms, mh, KIND == 1 ? y[i][0] : nullptr);
       }
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) load8_last<T>(yp[t] + offs[i][q], y[i][t][q]);
+        for (int q = 0; q < NQ; ++q) {
+          if (KIND == 1 && t == 0) continue;  // the mask's y_0, loaded once in bnb_unit_g
+          load8_last<T>(yp[t] + offs[i][q], y[i][t][q]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < UN; ++i) {
